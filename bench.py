@@ -1,0 +1,225 @@
+"""bench.py — BASELINE metric: device-resident RS(30,3) encode & 3-erasure
+decode of 32 MiB segments (BASELINE.json configs[1] + configs[2]).
+
+One step = one pass of the hot path over one batch resident in HBM:
+  encode : 128 x 32 MiB segments -> 4 x RS(30,3) + 1 x RS(8,3) parity
+           (exactly the blocks src/chunker/commit.rs:359,402-416 forms for a 4 GiB file)
+  decode : per block, 3 data shards erased (seed 0xDEC0DE+block), restored from
+           the survivors + parity (src/filestore/recovery.rs:118-173 semantics)
+Both go through the C-ABI (bfrs_encode_batch_dev / bfrs_decode_batch_dev) on
+torch's current stream, one kernel launch each.
+
+value = original-data GiB processed by all ranks (encode + decode) / max-rank time.
+Multi-GPU (torchrun): every rank owns an independent batch (weak scaling, no
+collective on the data path; the only collectives are the barrier and the
+max-time reduction).
+
+Extra fields: per-direction GiB/s, `roofline` for gf_apply_kernel measured
+with HIP events on the launch stream, `cpu_baseline` = the oracle's AVX2
+engine (restatement of reed-solomon-simd, not the crate) on a bounded sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "blockframe-rs_amd"))
+
+METRIC = "GiB/s device-resident RS(30,3) encode & 3-erasure decode, 32MB segments"
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--segments", type=int, default=128, help="segments per GPU (C2: 128)")
+    ap.add_argument("--segment-bytes", type=int, default=32 * 1024 * 1024)
+    ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
+    ap.add_argument("--cpu-shard-bytes", type=int, default=8 * 1024 * 1024)
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    return ap.parse_args()
+
+
+def cpu_baseline(args):
+    """Oracle (AVX2 nibble-table engine, the crate's Avx2 technique) on host
+    cores: T independent RS(30,3) blocks, one per thread (rayon over blocks,
+    src/chunker/commit.rs:391), encode then 3-erasure decode."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    from bfrs import synth
+    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    eng = oracle.ENGINE_AVX2 if oracle.lib().oracle_have_avx2() else oracle.ENGINE_SCALAR
+    n = args.cpu_shard_bytes
+    ks = [30] * threads
+    data = [[synth.segment_np(0xC0, b * 30 + i, n) for i in range(30)] for b in range(threads)]
+    par = [[np.empty(n, np.uint8) for _ in range(3)] for _ in range(threads)]
+    t0 = time.perf_counter()
+    oracle.batch(eng, False, threads, ks, 3, n, data, [[None] * 3] * threads, par)
+    t_enc = time.perf_counter() - t0
+    orig = [[None if i in (1, 12, 25) else blk[i] for i in range(30)] for blk in data]
+    out = [[np.empty(n, np.uint8) if i in (1, 12, 25) else None for i in range(30)]
+           for _ in range(threads)]
+    t0 = time.perf_counter()
+    oracle.batch(eng, True, threads, ks, 3, n, orig, par, out)
+    t_dec = time.perf_counter() - t0
+    assert np.array_equal(out[0][12], data[0][12])
+    gib = threads * 30 * n / 2**30
+    return {
+        "value": round(2 * gib / (t_enc + t_dec), 3),
+        "unit": "GiB/s",
+        "cores": threads,
+        "kind": "port",
+        "engine": "avx2" if eng == oracle.ENGINE_AVX2 else "scalar",
+        "encode_GiBps": round(gib / t_enc, 3),
+        "decode_GiBps": round(gib / t_dec, 3),
+        "sample": f"{threads} blocks x RS(30,3) x {n // 2**20} MiB shards, one block per thread; "
+                  "encode + 3-erasure decode (restatement of reed-solomon-simd 3.1.0, not the crate)",
+    }
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import bfrs
+    from bfrs import synth
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    S = args.segment_bytes
+    nseg = args.segments
+    shapes = synth.block_shapes(nseg)
+    nb = len(shapes)
+    seed = 0xB10C + rank
+
+    # ---- resident workload
+    data = torch.empty(nseg, S, dtype=torch.uint8, device="cuda")
+    for s in range(nseg):
+        synth.fill_segment_torch(data[s], seed, s)
+    parity = torch.empty(3 * nb, S, dtype=torch.uint8, device="cuda")
+    restored = torch.empty(3 * nb, S, dtype=torch.uint8, device="cuda")
+    enc_in = [data[s] for s in range(nseg)]
+    enc_out = [parity[i] for i in range(3 * nb)]
+    dec_in, dec_out, seg = [], [], 0
+    erased = []
+    for b, k in enumerate(shapes):
+        er = sorted(np.random.default_rng(0xDEC0DE + b).choice(k, 3, replace=False).tolist())
+        erased.append(er)
+        for i in range(k):
+            dec_in.append(None if i in er else data[seg + i])
+            dec_out.append(restored[3 * b + er.index(i)] if i in er else None)
+        seg += k
+
+    ctx = bfrs.Context(local)
+    stream = torch.cuda.current_stream()
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        ctx.encode_batch_dev(shapes, 3, S, enc_in, enc_out, stream=stream)
+        if ev is not None:
+            ev[1].record(stream)
+        ctx.decode_batch_dev(shapes, 3, S, dec_in, enc_out, dec_out, stream=stream)
+        if ev is not None:
+            ev[2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    # correctness guard on the measured buffers (cheap: compare on device)
+    seg = 0
+    for b, k in enumerate(shapes):
+        for t, i in enumerate(erased[b]):
+            assert torch.equal(restored[3 * b + t], data[seg + i]), "decode mismatch"
+        seg += k
+
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(events[i])
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in events]))
+    dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in events]))
+    data_bytes = sum(shapes) * S                     # original data per direction
+    alg_bytes = sum(k + 3 for k in shapes) * S        # HBM bytes per launch (both directions)
+    gib_step = 2 * data_bytes / 2**30
+    value = world * gib_step * args.steps / elapsed
+
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+
+    launch_ms = (enc_ms + dec_ms) / 2
+    achieved = alg_bytes / (launch_ms * 1e-3) / 1e9
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc):
+        try:
+            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    cpu = None
+    if world == 1 and args.cpu_baseline == "auto":
+        cpu = cpu_baseline(args)
+
+    line = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": f"synthetic splitmix64 bytes (seed 0xB10C+rank), resident in HBM",
+        "config": {
+            "workload": "BASELINE configs[1]+[2]: 128 x 32 MiB segments = 4xRS(30,3)+1xRS(8,3); "
+                        "step = encode batch + 3-erasure decode of every block",
+            "segments_per_gpu": nseg, "segment_bytes": S, "blocks": shapes, "parity_shards": 3,
+            "parallelism": f"independent batch per GPU x{world}",
+        },
+        "encode_GiBps_per_gpu": round(data_bytes / 2**30 / (enc_ms * 1e-3), 2),
+        "decode_GiBps_per_gpu": round(data_bytes / 2**30 / (dec_ms * 1e-3), 2),
+        "roofline": {
+            "bound": "hbm", "kernel": "gf_apply_kernel",
+            "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+            "alg_bytes_per_launch": alg_bytes,
+            "launch_ms": {"encode": round(enc_ms, 4), "decode": round(dec_ms, 4)},
+        },
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,399 @@
+"""bfrs — Python binding of the MI355X BlockFrame Reed-Solomon C-ABI.
+
+Thin ctypes layer over blockframe-rs_amd/libbfrs.so (include/bfrs.h), used by
+the tests and bench.py.  It mirrors the reference's codec surface:
+
+    ReedSolomonEncoder / ReedSolomonDecoder   (reed-solomon-simd 3.1.0, as called at
+                                               src/chunker/generate.rs:37-49,84-96 and
+                                               src/filestore/recovery.rs:58-69,152-170)
+    Chunker.generate_parity(_segmented)       (src/chunker/generate.rs:26-104)
+    recover_segment_rs13 / recover_segment_rs30_3  (src/filestore/recovery.rs:43-173)
+
+All arithmetic runs in the HIP kernels of libbfrs.so.  If the library is
+missing, import fails loudly; if no GPU is present, every codec call raises
+BfrsError(BFRS_E_NO_DEVICE).  There is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional, Sequence
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "libbfrs.so")
+
+# Error codes (include/bfrs.h)
+OK = 0
+E_DIFFERENT_SHARD_SIZE = -1
+E_DUPLICATE_ORIGINAL_SHARD_INDEX = -2
+E_DUPLICATE_RECOVERY_SHARD_INDEX = -3
+E_INVALID_ORIGINAL_SHARD_INDEX = -4
+E_INVALID_RECOVERY_SHARD_INDEX = -5
+E_INVALID_SHARD_SIZE = -6
+E_NOT_ENOUGH_SHARDS = -7
+E_TOO_FEW_ORIGINAL_SHARDS = -8
+E_TOO_MANY_ORIGINAL_SHARDS = -9
+E_UNSUPPORTED_SHARD_COUNT = -10
+E_WRAPPER = -20
+E_INVALID_ARGUMENT = -30
+E_HIP = -31
+E_NO_DEVICE = -32
+E_NOMEM = -33
+E_NOT_RESTORED = -34
+
+# Every symbol include/bfrs.h declares (tests check the library exports them).
+EXPORTS = (
+    "bfrs_abi_version", "bfrs_strerror", "bfrs_last_error", "bfrs_device_count", "bfrs_open",
+    "bfrs_close", "bfrs_synchronize", "bfrs_use_high_rate", "bfrs_encode_coefficient",
+    "bfrs_plan_decode", "bfrs_encoder_new", "bfrs_encoder_add_original_shard",
+    "bfrs_encoder_encode", "bfrs_encoder_recovery", "bfrs_encoder_free", "bfrs_decoder_new",
+    "bfrs_decoder_add_original_shard", "bfrs_decoder_add_recovery_shard", "bfrs_decoder_decode",
+    "bfrs_decoder_restored_original", "bfrs_decoder_free", "bfrs_encode", "bfrs_decode",
+    "bfrs_encode_batch_dev", "bfrs_decode_batch_dev", "bfrs_generate_parity",
+    "bfrs_generate_parity_segmented", "bfrs_recover_segment_rs13", "bfrs_recover_segment_rs30_3",
+)
+
+SIZE_MAX = ctypes.c_size_t(-1).value
+
+
+class BfrsError(RuntimeError):
+    def __init__(self, code: int, message: str):
+        super().__init__(message)
+        self.code = code
+
+
+_lib: Optional[ctypes.CDLL] = None
+
+_vp = ctypes.c_void_p
+_sz = ctypes.c_size_t
+_pp = ctypes.POINTER(ctypes.c_void_p)
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"libbfrs.so not built at {LIB_PATH}; run __graft_entry__.build()")
+        L = ctypes.CDLL(LIB_PATH)
+        sig = {
+            "bfrs_abi_version": ([], ctypes.c_int),
+            "bfrs_strerror": ([ctypes.c_int], ctypes.c_char_p),
+            "bfrs_last_error": ([], ctypes.c_char_p),
+            "bfrs_device_count": ([], ctypes.c_int),
+            "bfrs_open": ([ctypes.c_int, ctypes.POINTER(_vp)], ctypes.c_int),
+            "bfrs_close": ([_vp], None),
+            "bfrs_synchronize": ([_vp], ctypes.c_int),
+            "bfrs_use_high_rate": ([_sz, _sz], ctypes.c_int),
+            "bfrs_encode_coefficient": ([_sz, _sz, _sz, _sz, ctypes.POINTER(ctypes.c_uint16)],
+                                        ctypes.c_int),
+            "bfrs_plan_decode": ([_sz, _sz, _vp, _vp, _vp, _sz, ctypes.POINTER(_sz),
+                                  ctypes.POINTER(_sz)], ctypes.c_int),
+            "bfrs_encoder_new": ([_vp, _sz, _sz, _sz, ctypes.POINTER(_vp)], ctypes.c_int),
+            "bfrs_encoder_add_original_shard": ([_vp, _vp, _sz], ctypes.c_int),
+            "bfrs_encoder_encode": ([_vp], ctypes.c_int),
+            "bfrs_encoder_recovery": ([_vp, _sz, ctypes.POINTER(_vp), ctypes.POINTER(_sz)],
+                                      ctypes.c_int),
+            "bfrs_encoder_free": ([_vp], None),
+            "bfrs_decoder_new": ([_vp, _sz, _sz, _sz, ctypes.POINTER(_vp)], ctypes.c_int),
+            "bfrs_decoder_add_original_shard": ([_vp, _sz, _vp, _sz], ctypes.c_int),
+            "bfrs_decoder_add_recovery_shard": ([_vp, _sz, _vp, _sz], ctypes.c_int),
+            "bfrs_decoder_decode": ([_vp], ctypes.c_int),
+            "bfrs_decoder_restored_original": ([_vp, _sz, ctypes.POINTER(_vp),
+                                                ctypes.POINTER(_sz)], ctypes.c_int),
+            "bfrs_decoder_free": ([_vp], None),
+            "bfrs_encode": ([_vp, _sz, _sz, _sz, _pp, _pp], ctypes.c_int),
+            "bfrs_decode": ([_vp, _sz, _sz, _sz, _pp, _pp, _pp], ctypes.c_int),
+            "bfrs_encode_batch_dev": ([_vp, _sz, ctypes.POINTER(ctypes.c_uint32), _sz, _sz, _pp,
+                                       _pp, _vp], ctypes.c_int),
+            "bfrs_decode_batch_dev": ([_vp, _sz, ctypes.POINTER(ctypes.c_uint32), _sz, _sz, _pp,
+                                       _pp, _pp, _vp], ctypes.c_int),
+            "bfrs_generate_parity": ([_vp, _pp, ctypes.POINTER(_sz), _sz, _sz, _sz, _pp,
+                                      ctypes.POINTER(_sz)], ctypes.c_int),
+            "bfrs_generate_parity_segmented": ([_vp, _vp, _sz, _pp, ctypes.POINTER(_sz)],
+                                               ctypes.c_int),
+            "bfrs_recover_segment_rs13": ([_vp, _pp, ctypes.POINTER(_sz), _sz, _sz, _vp,
+                                           ctypes.POINTER(_sz)], ctypes.c_int),
+            "bfrs_recover_segment_rs30_3": ([_vp, _pp, ctypes.POINTER(_sz), _sz, _pp,
+                                             ctypes.POINTER(_sz), _sz, _sz, _vp,
+                                             ctypes.POINTER(_sz)], ctypes.c_int),
+        }
+        for name, (args, res) in sig.items():
+            f = getattr(L, name)
+            f.argtypes = args
+            f.restype = res
+        _lib = L
+    return _lib
+
+
+def _check(rc: int) -> None:
+    if rc != OK:
+        msg = lib().bfrs_last_error().decode(errors="replace")
+        raise BfrsError(rc, msg or lib().bfrs_strerror(rc).decode())
+
+
+def _ptr_array(ptrs: Sequence[Optional[int]]):
+    arr = (ctypes.c_void_p * max(1, len(ptrs)))()
+    for i, p in enumerate(ptrs):
+        arr[i] = p
+    return ctypes.cast(arr, _pp), arr
+
+
+def _host_ptr(buf) -> int:
+    """Address of a host buffer (bytes / bytearray / numpy array)."""
+    import numpy as np
+    if isinstance(buf, np.ndarray):
+        if not buf.flags.c_contiguous:
+            raise ValueError("host buffer must be C-contiguous")
+        return buf.ctypes.data
+    if isinstance(buf, bytes):
+        return ctypes.cast(ctypes.c_char_p(buf), ctypes.c_void_p).value
+    if isinstance(buf, bytearray):
+        return ctypes.addressof((ctypes.c_char * len(buf)).from_buffer(buf))
+    raise TypeError(f"unsupported host buffer type {type(buf)}")
+
+
+def _as_np(buf):
+    import numpy as np
+    if isinstance(buf, np.ndarray):
+        return np.ascontiguousarray(buf, dtype=np.uint8).reshape(-1)
+    return np.frombuffer(bytes(buf), dtype=np.uint8)
+
+
+def use_high_rate(original_count: int, recovery_count: int) -> bool:
+    rc = lib().bfrs_use_high_rate(original_count, recovery_count)
+    if rc < 0:
+        raise BfrsError(rc, "unsupported shard count")
+    return rc == 1
+
+
+def encode_coefficient(k: int, m: int, j: int, i: int) -> int:
+    c = ctypes.c_uint16()
+    _check(lib().bfrs_encode_coefficient(k, m, j, i, ctypes.byref(c)))
+    return c.value
+
+
+def plan_decode(k: int, m: int, orig_present, rec_present):
+    """Decode coefficient matrix (rows = missing originals, cols = present
+    recovery then present originals) as a list of lists."""
+    op = (ctypes.c_uint8 * k)(*[1 if x else 0 for x in orig_present])
+    rp = (ctypes.c_uint8 * m)(*[1 if x else 0 for x in rec_present])
+    rows, cols = _sz(), _sz()
+    _check(lib().bfrs_plan_decode(k, m, op, rp, None, 0, ctypes.byref(rows), ctypes.byref(cols)))
+    n = rows.value * cols.value
+    buf = (ctypes.c_uint16 * max(1, n))()
+    _check(lib().bfrs_plan_decode(k, m, op, rp, buf, n, ctypes.byref(rows), ctypes.byref(cols)))
+    return [[buf[r * cols.value + c] for c in range(cols.value)] for r in range(rows.value)]
+
+
+def device_count() -> int:
+    return int(lib().bfrs_device_count())
+
+
+class Context:
+    """A bfrs_ctx on one HIP device (no CPU fallback)."""
+
+    def __init__(self, device: int = 0):
+        h = ctypes.c_void_p()
+        _check(lib().bfrs_open(device, ctypes.byref(h)))
+        self.handle = h
+        self.device = device
+
+    def close(self) -> None:
+        if self.handle:
+            lib().bfrs_close(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def synchronize(self) -> None:
+        _check(lib().bfrs_synchronize(self.handle))
+
+    # ---- device-resident batch API (torch tensors or raw device addresses)
+    @staticmethod
+    def _addr(t) -> Optional[int]:
+        if t is None:
+            return None
+        return t if isinstance(t, int) else t.data_ptr()
+
+    def encode_batch_dev(self, original_counts, recovery_count, shard_bytes, d_originals,
+                         d_recovery, stream=None) -> None:
+        ks = (ctypes.c_uint32 * len(original_counts))(*original_counts)
+        po, ko = _ptr_array([self._addr(t) for t in d_originals])
+        pr, kr = _ptr_array([self._addr(t) for t in d_recovery])
+        _check(lib().bfrs_encode_batch_dev(self.handle, len(original_counts), ks, recovery_count,
+                                           shard_bytes, po, pr, _stream_handle(stream)))
+
+    def decode_batch_dev(self, original_counts, recovery_count, shard_bytes, d_originals,
+                         d_recovery, d_restored, stream=None) -> None:
+        ks = (ctypes.c_uint32 * len(original_counts))(*original_counts)
+        po, ko = _ptr_array([self._addr(t) for t in d_originals])
+        pr, kr = _ptr_array([self._addr(t) for t in d_recovery])
+        pd, kd = _ptr_array([self._addr(t) for t in d_restored])
+        _check(lib().bfrs_decode_batch_dev(self.handle, len(original_counts), ks, recovery_count,
+                                           shard_bytes, po, pr, pd, _stream_handle(stream)))
+
+    # ---- one-shot host API (numpy in, numpy out)
+    def encode(self, originals, recovery_count=3):
+        import numpy as np
+        orig = [_as_np(o) for o in originals]
+        n = orig[0].size
+        rec = [np.empty(n, dtype=np.uint8) for _ in range(recovery_count)]
+        po, ko = _ptr_array([o.ctypes.data for o in orig])
+        pr, kr = _ptr_array([r.ctypes.data for r in rec])
+        _check(lib().bfrs_encode(self.handle, len(orig), recovery_count, n, po, pr))
+        return rec
+
+    def decode(self, originals, recovery):
+        import numpy as np
+        orig = [None if o is None else _as_np(o) for o in originals]
+        rec = [None if r is None else _as_np(r) for r in recovery]
+        n = next(a.size for a in orig + rec if a is not None)
+        out = [np.empty(n, dtype=np.uint8) if o is None else None for o in orig]
+        po, ko = _ptr_array([None if o is None else o.ctypes.data for o in orig])
+        pr, kr = _ptr_array([None if r is None else r.ctypes.data for r in rec])
+        pd, kd = _ptr_array([None if a is None else a.ctypes.data for a in out])
+        _check(lib().bfrs_decode(self.handle, len(orig), len(rec), n, po, pr, pd))
+        return {i: a for i, a in enumerate(out) if a is not None}
+
+
+def _stream_handle(stream) -> Optional[int]:
+    if stream is None:
+        return None
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream  # torch.cuda.Stream
+
+
+class ReedSolomonEncoder:
+    """reed_solomon_simd::ReedSolomonEncoder over the HIP path."""
+
+    def __init__(self, ctx: Context, original_count: int, recovery_count: int, shard_bytes: int):
+        h = ctypes.c_void_p()
+        _check(lib().bfrs_encoder_new(ctx.handle, original_count, recovery_count, shard_bytes,
+                                      ctypes.byref(h)))
+        self.handle, self.ctx, self.recovery_count = h, ctx, recovery_count
+
+    def __del__(self):
+        if getattr(self, "handle", None):
+            lib().bfrs_encoder_free(self.handle)
+            self.handle = None
+
+    def add_original_shard(self, shard) -> None:
+        a = _as_np(shard)
+        _check(lib().bfrs_encoder_add_original_shard(self.handle, a.ctypes.data, a.size))
+
+    def encode(self) -> "ReedSolomonEncoder":
+        _check(lib().bfrs_encoder_encode(self.handle))
+        return self
+
+    def recovery_iter(self):
+        for j in range(self.recovery_count):
+            p, n = ctypes.c_void_p(), _sz()
+            _check(lib().bfrs_encoder_recovery(self.handle, j, ctypes.byref(p), ctypes.byref(n)))
+            yield ctypes.string_at(p, n.value)
+
+
+class ReedSolomonDecoder:
+    """reed_solomon_simd::ReedSolomonDecoder over the HIP path."""
+
+    def __init__(self, ctx: Context, original_count: int, recovery_count: int, shard_bytes: int):
+        h = ctypes.c_void_p()
+        _check(lib().bfrs_decoder_new(ctx.handle, original_count, recovery_count, shard_bytes,
+                                      ctypes.byref(h)))
+        self.handle, self.ctx = h, ctx
+
+    def __del__(self):
+        if getattr(self, "handle", None):
+            lib().bfrs_decoder_free(self.handle)
+            self.handle = None
+
+    def add_original_shard(self, index: int, shard) -> None:
+        a = _as_np(shard)
+        _check(lib().bfrs_decoder_add_original_shard(self.handle, index, a.ctypes.data, a.size))
+
+    def add_recovery_shard(self, index: int, shard) -> None:
+        a = _as_np(shard)
+        _check(lib().bfrs_decoder_add_recovery_shard(self.handle, index, a.ctypes.data, a.size))
+
+    def decode(self) -> "ReedSolomonDecoder":
+        _check(lib().bfrs_decoder_decode(self.handle))
+        return self
+
+    def restored_original(self, index: int) -> Optional[bytes]:
+        p, n = ctypes.c_void_p(), _sz()
+        rc = lib().bfrs_decoder_restored_original(self.handle, index, ctypes.byref(p),
+                                                  ctypes.byref(n))
+        if rc == E_NOT_RESTORED:
+            return None
+        _check(rc)
+        return ctypes.string_at(p, n.value)
+
+
+class Chunker:
+    """The codec-facing part of src/chunker (generate.rs)."""
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+
+    def generate_parity(self, segments, data_shards: int, parity_shards: int):
+        import numpy as np
+        segs = [_as_np(s) for s in segments]
+        maxlen = max((s.size for s in segs), default=0)
+        outs = [np.empty(maxlen, dtype=np.uint8) for _ in range(parity_shards)]
+        ps, ks = _ptr_array([s.ctypes.data if s.size else None for s in segs])
+        lens = (_sz * max(1, len(segs)))(*[s.size for s in segs])
+        po, ko = _ptr_array([o.ctypes.data for o in outs])
+        plen = _sz()
+        _check(lib().bfrs_generate_parity(self.ctx.handle, ps, lens, len(segs), data_shards,
+                                          parity_shards, po, ctypes.byref(plen)))
+        return [o.tobytes() for o in outs]
+
+    def generate_parity_segmented(self, segment_data):
+        import numpy as np
+        a = _as_np(segment_data)
+        padded = (a.size + 63) // 64 * 64
+        outs = [np.empty(max(1, padded), dtype=np.uint8) for _ in range(3)]
+        po, ko = _ptr_array([o.ctypes.data for o in outs])
+        plen = _sz()
+        _check(lib().bfrs_generate_parity_segmented(self.ctx.handle,
+                                                    a.ctypes.data if a.size else None, a.size,
+                                                    po, ctypes.byref(plen)))
+        return [o[:plen.value].tobytes() for o in outs]
+
+
+def recover_segment_rs13(ctx: Context, parity_shards, expected_size: Optional[int] = None) -> bytes:
+    """src/filestore/recovery.rs:43-79"""
+    import numpy as np
+    ps = [_as_np(p) for p in parity_shards]
+    n = max((p.size for p in ps), default=0)
+    out = np.empty(max(1, n), dtype=np.uint8)
+    pp, kp = _ptr_array([p.ctypes.data for p in ps])
+    lens = (_sz * max(1, len(ps)))(*[p.size for p in ps])
+    olen = _sz()
+    _check(lib().bfrs_recover_segment_rs13(ctx.handle, pp, lens, len(ps),
+                                           SIZE_MAX if expected_size is None else expected_size,
+                                           out.ctypes.data, ctypes.byref(olen)))
+    return out[:olen.value].tobytes()
+
+
+def recover_segment_rs30_3(ctx: Context, valid_segments, block_parity, target_index: int) -> bytes:
+    """src/filestore/recovery.rs:118-173 (valid_segments: 30 slots, None = missing)."""
+    import numpy as np
+    segs = [None if s is None else _as_np(s) for s in valid_segments]
+    par = [_as_np(p) for p in block_parity]
+    sizes = [s.size for s in segs if s is not None] + [p.size for p in par]
+    n = max(sizes, default=0)
+    out = np.empty(max(1, n), dtype=np.uint8)
+    ps, ks = _ptr_array([None if s is None else s.ctypes.data for s in segs])
+    slens = (_sz * max(1, len(segs)))(*[0 if s is None else s.size for s in segs])
+    pp, kp = _ptr_array([p.ctypes.data for p in par])
+    plens = (_sz * max(1, len(par)))(*[p.size for p in par])
+    olen = _sz()
+    _check(lib().bfrs_recover_segment_rs30_3(ctx.handle, ps, slens, len(segs), pp, plens,
+                                             len(par), target_index, out.ctypes.data,
+                                             ctypes.byref(olen)))
+    return out[:olen.value].tobytes()

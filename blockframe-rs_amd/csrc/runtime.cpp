@@ -1,0 +1,525 @@
+// runtime.cpp — context, plan cache, pass scheduling and the codec C-ABI.
+//
+// Mirrors the reed-solomon-simd 3.1.0 surface the reference uses
+// (ReedSolomonEncoder/Decoder) on top of the HIP kernels.
+// There is no CPU compute path: without a HIP device every codec entry point
+// fails with BFRS_E_NO_DEVICE.
+#include "runtime.hpp"
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <sstream>
+
+namespace bfrs {
+
+namespace {
+thread_local std::string g_last_error;
+
+// Device-path limits (the crate allows up to 65535; the matrix form here is
+// sized for BlockFrame's RS(<=30, 3) and moderate generalisations).
+constexpr size_t kMaxOriginal = 1024;
+constexpr size_t kMaxRecovery = 1024;
+
+size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+}  // namespace
+
+int set_error(int code, const std::string &msg) {
+  g_last_error = msg;
+  return code;
+}
+
+int hip_error(hipError_t e, const char *what) {
+  std::ostringstream os;
+  os << what << ": " << hipGetErrorString(e);
+  return set_error(BFRS_E_HIP, os.str());
+}
+
+#define HIP_TRY(expr)                                 \
+  do {                                                \
+    hipError_t e_ = (expr);                           \
+    if (e_ != hipSuccess) return hip_error(e_, #expr); \
+  } while (0)
+
+int check_shape(size_t k, size_t m, size_t shard_bytes) {
+  if (shard_bytes == 0 || (shard_bytes & 1)) {
+    std::ostringstream os;
+    os << "invalid shard size: " << shard_bytes << " bytes (must non-zero and multiple of 2)";
+    return set_error(BFRS_E_INVALID_SHARD_SIZE, os.str());
+  }
+  Rate rate;
+  if (!choose_rate(k, m, &rate) || k > kMaxOriginal || m > kMaxRecovery) {
+    std::ostringstream os;
+    os << "unsupported shard count: " << k << " original shards with " << m
+       << " recovery shards";
+    return set_error(BFRS_E_UNSUPPORTED_SHARD_COUNT, os.str());
+  }
+  return BFRS_OK;
+}
+
+Plan::~Plan() {
+  if (d_tables) (void)hipFree(d_tables);
+}
+
+static int upload_plan(Plan *p) {
+  const CoefMatrix &c = p->coef;
+  std::vector<uint32_t> all, t;
+  std::vector<size_t> offs;
+  for (size_t r0 = 0; r0 < c.rows; r0 += kMaxPassOutputs) {
+    const size_t r1 = std::min(c.rows, r0 + kMaxPassOutputs);
+    for (size_t c0 = 0; c0 < c.cols; c0 += kMaxPassInputs) {
+      const size_t c1 = std::min(c.cols, c0 + kMaxPassInputs);
+      build_tables(c, r0, r1, c0, c1, &t);
+      offs.push_back(all.size());
+      all.insert(all.end(), t.begin(), t.end());
+      PlanPass pp;
+      pp.r0 = uint32_t(r0);
+      pp.r1 = uint32_t(r1);
+      pp.c0 = uint32_t(c0);
+      pp.c1 = uint32_t(c1);
+      pp.phase = uint32_t(c0 / kMaxPassInputs);
+      p->passes.push_back(pp);
+      p->n_phases = std::max(p->n_phases, pp.phase + 1);
+    }
+  }
+  if (all.empty()) return BFRS_OK;
+  HIP_TRY(hipMalloc(&p->d_tables, all.size() * sizeof(uint32_t)));
+  HIP_TRY(hipMemcpy(p->d_tables, all.data(), all.size() * sizeof(uint32_t),
+                    hipMemcpyHostToDevice));
+  for (size_t i = 0; i < p->passes.size(); ++i)
+    p->passes[i].d_table =
+        reinterpret_cast<const uint2 *>(static_cast<uint32_t *>(p->d_tables) + offs[i]);
+  return BFRS_OK;
+}
+
+Context::~Context() {
+  if (device >= 0) (void)hipSetDevice(device);
+  if (stream) (void)hipStreamSynchronize(stream);
+  for (auto &s : slots) {
+    if (s.host) (void)hipHostFree(s.host);
+    if (s.dev) (void)hipFree(s.dev);
+    if (s.done) (void)hipEventDestroy(s.done);
+  }
+  plans.clear();
+  if (d_scratch) (void)hipFree(d_scratch);
+  if (stream) (void)hipStreamDestroy(stream);
+}
+
+int Context::init(int dev) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+    return set_error(BFRS_E_NO_DEVICE, "no HIP device available (no CPU fallback)");
+  if (dev < 0 || dev >= n) return set_error(BFRS_E_NO_DEVICE, "HIP device id out of range");
+  device = dev;
+  HIP_TRY(hipSetDevice(dev));
+  HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+  slots.resize(8);
+  for (auto &s : slots) HIP_TRY(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+  return BFRS_OK;
+}
+
+int Context::scratch(size_t bytes, void **out) {
+  if (bytes > scratch_cap) {
+    if (d_scratch) {
+      HIP_TRY(hipStreamSynchronize(stream));
+      HIP_TRY(hipFree(d_scratch));
+      d_scratch = nullptr;
+      scratch_cap = 0;
+    }
+    HIP_TRY(hipMalloc(&d_scratch, bytes));
+    scratch_cap = bytes;
+  }
+  *out = d_scratch;
+  return BFRS_OK;
+}
+
+int Context::get_encode_plan(size_t k, size_t m, const Plan **out) {
+  std::ostringstream key;
+  key << "E" << k << "," << m;
+  std::lock_guard<std::mutex> g(mu);
+  auto it = plans.find(key.str());
+  if (it == plans.end()) {
+    auto p = std::make_unique<Plan>();
+    p->coef = plan_encode(k, m);
+    int rc = upload_plan(p.get());
+    if (rc) return rc;
+    it = plans.emplace(key.str(), std::move(p)).first;
+  }
+  *out = it->second.get();
+  return BFRS_OK;
+}
+
+int Context::get_decode_plan(size_t k, size_t m, const std::vector<uint8_t> &orig_present,
+                             const std::vector<uint8_t> &rec_present, const Plan **out) {
+  std::string key = "D" + std::to_string(k) + "," + std::to_string(m) + ":";
+  for (uint8_t b : orig_present) key.push_back(b ? '1' : '0');
+  key.push_back('/');
+  for (uint8_t b : rec_present) key.push_back(b ? '1' : '0');
+  std::lock_guard<std::mutex> g(mu);
+  auto it = plans.find(key);
+  if (it == plans.end()) {
+    if (plans.size() > 4096) plans.clear();  // bound the cache
+    auto p = std::make_unique<Plan>();
+    p->coef = plan_decode(k, m, orig_present, rec_present);
+    int rc = upload_plan(p.get());
+    if (rc) return rc;
+    it = plans.emplace(key, std::move(p)).first;
+  }
+  *out = it->second.get();
+  return BFRS_OK;
+}
+
+int Context::run_blocks(const std::vector<BlockIO> &blocks, size_t shard_bytes,
+                        hipStream_t s) {
+  const uint64_t full_chunks = shard_bytes / 64;
+  const uint32_t tail = uint32_t(shard_bytes % 64);
+  const uint32_t n_tiles = uint32_t((full_chunks * 2 + kTileHalfChunks - 1) / kTileHalfChunks);
+  uint32_t max_phase = 0;
+  for (const BlockIO &b : blocks) max_phase = std::max(max_phase, b.plan->n_phases);
+
+  for (uint32_t phase = 0; phase < max_phase; ++phase) {
+    // Gather this phase's passes.
+    struct Item {
+      const BlockIO *b;
+      const PlanPass *p;
+    };
+    std::vector<Item> items;
+    uint32_t max_in = 0;
+    for (const BlockIO &b : blocks)
+      for (const PlanPass &p : b.plan->passes)
+        if (p.phase == phase) {
+          items.push_back({&b, &p});
+          max_in = std::max(max_in, p.c1 - p.c0);
+        }
+    if (items.empty()) continue;
+
+    // Workgroup sizing: ~4096 workgroups in flight-order, >= 1 tile each.
+    const uint64_t total_tiles = uint64_t(n_tiles) * items.size();
+    uint32_t tpw = uint32_t(std::max<uint64_t>(1, total_tiles / 4096));
+    if (const char *e = std::getenv("BFRS_TILES_PER_WG")) tpw = std::max(1, atoi(e));
+    const uint32_t wgs_per_pass = (n_tiles + tpw - 1) / tpw;
+
+    // Staging layout: [PassDesc x n][pointer arrays].
+    size_t n_ptrs = 0;
+    for (const Item &it : items) n_ptrs += (it.p->c1 - it.p->c0) + (it.p->r1 - it.p->r0);
+    const size_t desc_bytes = round_up(items.size() * sizeof(PassDesc), 16);
+    const size_t bytes = desc_bytes + n_ptrs * sizeof(void *);
+
+    Slot &slot = slots[next_slot];
+    next_slot = (next_slot + 1) % slots.size();
+    if (slot.used) HIP_TRY(hipEventSynchronize(slot.done));
+    if (bytes > slot.cap) {
+      if (slot.host) HIP_TRY(hipHostFree(slot.host));
+      if (slot.dev) HIP_TRY(hipFree(slot.dev));
+      const size_t cap = std::max<size_t>(round_up(bytes, 4096), 64 * 1024);
+      HIP_TRY(hipHostMalloc(&slot.host, cap, hipHostMallocDefault));
+      HIP_TRY(hipMalloc(&slot.dev, cap));
+      slot.cap = cap;
+    }
+    auto *desc = static_cast<PassDesc *>(slot.host);
+    auto *ptrs = reinterpret_cast<uint64_t *>(static_cast<char *>(slot.host) + desc_bytes);
+    const uint64_t dev_ptrs = reinterpret_cast<uint64_t>(slot.dev) + desc_bytes;
+    size_t pi = 0;
+    uint32_t wg = 0;
+    for (size_t i = 0; i < items.size(); ++i) {
+      const BlockIO &b = *items[i].b;
+      const PlanPass &p = *items[i].p;
+      PassDesc d{};
+      d.in = reinterpret_cast<const uint8_t *const *>(dev_ptrs + pi * 8);
+      for (uint32_t c = p.c0; c < p.c1; ++c) ptrs[pi++] = reinterpret_cast<uint64_t>(b.in[c]);
+      d.out = reinterpret_cast<uint8_t *const *>(dev_ptrs + pi * 8);
+      for (uint32_t r = p.r0; r < p.r1; ++r) ptrs[pi++] = reinterpret_cast<uint64_t>(b.out[r]);
+      d.table = p.d_table;
+      d.n_in = p.c1 - p.c0;
+      d.n_out = p.r1 - p.r0;
+      d.wg_begin = wg;
+      d.n_tiles = n_tiles;
+      d.full_chunks = full_chunks;
+      d.tail_bytes = tail;
+      d.accumulate = phase > 0;
+      desc[i] = d;
+      wg += wgs_per_pass;
+    }
+    HIP_TRY(hipMemcpyAsync(slot.dev, slot.host, bytes, hipMemcpyHostToDevice, s));
+    const auto *d_desc = static_cast<const PassDesc *>(slot.dev);
+    if (wg) HIP_TRY(launch_gf_apply(d_desc, uint32_t(items.size()), wg, tpw, max_in, s));
+    if (tail) HIP_TRY(launch_gf_tail(d_desc, uint32_t(items.size()), s));
+    HIP_TRY(hipEventRecord(slot.done, s));
+    slot.used = true;
+  }
+  return BFRS_OK;
+}
+
+}  // namespace bfrs
+
+using namespace bfrs;
+
+// ---------------------------------------------------------------------------
+// C-ABI
+// ---------------------------------------------------------------------------
+extern "C" {
+
+int bfrs_abi_version(void) { return BFRS_ABI_VERSION; }
+
+const char *bfrs_strerror(int code) {
+  switch (code) {
+    case BFRS_OK: return "ok";
+    case BFRS_E_DIFFERENT_SHARD_SIZE: return "different shard size";
+    case BFRS_E_DUPLICATE_ORIGINAL_SHARD_INDEX: return "duplicate original shard index";
+    case BFRS_E_DUPLICATE_RECOVERY_SHARD_INDEX: return "duplicate recovery shard index";
+    case BFRS_E_INVALID_ORIGINAL_SHARD_INDEX: return "invalid original shard index";
+    case BFRS_E_INVALID_RECOVERY_SHARD_INDEX: return "invalid recovery shard index";
+    case BFRS_E_INVALID_SHARD_SIZE: return "invalid shard size";
+    case BFRS_E_NOT_ENOUGH_SHARDS: return "not enough shards";
+    case BFRS_E_TOO_FEW_ORIGINAL_SHARDS: return "too few original shards";
+    case BFRS_E_TOO_MANY_ORIGINAL_SHARDS: return "too many original shards";
+    case BFRS_E_UNSUPPORTED_SHARD_COUNT: return "unsupported shard count";
+    case BFRS_E_WRAPPER: return "blockframe wrapper error";
+    case BFRS_E_INVALID_ARGUMENT: return "invalid argument";
+    case BFRS_E_HIP: return "HIP runtime error";
+    case BFRS_E_NO_DEVICE: return "no HIP device";
+    case BFRS_E_NOMEM: return "out of memory";
+    case BFRS_E_NOT_RESTORED: return "original shard was not restored";
+    default: return "unknown error";
+  }
+}
+
+const char *bfrs_last_error(void) { return g_last_error.c_str(); }
+
+int bfrs_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int bfrs_open(int device, bfrs_ctx **out) {
+  if (!out) return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_open: out is NULL");
+  *out = nullptr;
+  auto *c = new (std::nothrow) bfrs_ctx;
+  if (!c) return set_error(BFRS_E_NOMEM, "bfrs_open: allocation failed");
+  int rc = c->impl.init(device);
+  if (rc) {
+    delete c;
+    return rc;
+  }
+  *out = c;
+  return BFRS_OK;
+}
+
+void bfrs_close(bfrs_ctx *ctx) { delete ctx; }
+
+int bfrs_synchronize(bfrs_ctx *ctx) {
+  if (!ctx) return set_error(BFRS_E_INVALID_ARGUMENT, "NULL context");
+  HIP_TRY(hipSetDevice(ctx->impl.device));
+  HIP_TRY(hipStreamSynchronize(ctx->impl.stream));
+  return BFRS_OK;
+}
+
+int bfrs_use_high_rate(size_t k, size_t m) {
+  Rate r;
+  if (!choose_rate(k, m, &r)) return BFRS_E_UNSUPPORTED_SHARD_COUNT;
+  return r == Rate::kHigh ? 1 : 0;
+}
+
+int bfrs_encode_coefficient(size_t k, size_t m, size_t j, size_t i, uint16_t *coef_out) {
+  if (!coef_out) return set_error(BFRS_E_INVALID_ARGUMENT, "coef_out is NULL");
+  int rc = check_shape(k, m, 2);
+  if (rc) return rc;
+  if (j >= m || i >= k) return set_error(BFRS_E_INVALID_ARGUMENT, "index out of range");
+  CoefMatrix c = plan_encode(k, m);
+  *coef_out = c.at(j, i);
+  return BFRS_OK;
+}
+
+int bfrs_plan_decode(size_t k, size_t m, const uint8_t *orig_present, const uint8_t *rec_present,
+                     uint16_t *coef_out, size_t cap, size_t *rows, size_t *cols) {
+  if (!orig_present || !rec_present || !rows || !cols)
+    return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_plan_decode: NULL argument");
+  int rc = check_shape(k, m, 2);
+  if (rc) return rc;
+  std::vector<uint8_t> op(orig_present, orig_present + k), rp(rec_present, rec_present + m);
+  size_t orecv = 0, rrecv = 0;
+  for (uint8_t b : op) orecv += b != 0;
+  for (uint8_t b : rp) rrecv += b != 0;
+  if (orecv + rrecv < k) return set_error(BFRS_E_NOT_ENOUGH_SHARDS, "not enough shards");
+  if (orecv == k) {
+    *rows = 0;
+    *cols = 0;
+    return BFRS_OK;
+  }
+  CoefMatrix c = plan_decode(k, m, op, rp);
+  *rows = c.rows;
+  *cols = c.cols;
+  if (coef_out && cap >= c.c.size()) std::copy(c.c.begin(), c.c.end(), coef_out);
+  return BFRS_OK;
+}
+
+// ---- batch (device-resident) ------------------------------------------------
+static int check_dev_ptr(const void *p, const char *what) {
+  if (!p) return set_error(BFRS_E_INVALID_ARGUMENT, std::string(what) + " is NULL");
+  if (reinterpret_cast<uintptr_t>(p) & 15)
+    return set_error(BFRS_E_INVALID_ARGUMENT, std::string(what) + " is not 16-byte aligned");
+  return BFRS_OK;
+}
+
+int bfrs_encode_batch_dev(bfrs_ctx *ctx, size_t nblocks, const uint32_t *ks, size_t m,
+                          size_t shard_bytes, const uint8_t *const *d_orig,
+                          uint8_t *const *d_rec, void *hip_stream) {
+  if (!ctx || (nblocks && (!ks || !d_orig || !d_rec)))
+    return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_encode_batch_dev: NULL argument");
+  Context &c = ctx->impl;
+  HIP_TRY(hipSetDevice(c.device));
+  std::vector<BlockIO> blocks(nblocks);
+  size_t oi = 0;
+  for (size_t b = 0; b < nblocks; ++b) {
+    int rc = check_shape(ks[b], m, shard_bytes);
+    if (rc) return rc;
+    rc = c.get_encode_plan(ks[b], m, &blocks[b].plan);
+    if (rc) return rc;
+    blocks[b].in.resize(ks[b]);
+    for (uint32_t i = 0; i < ks[b]; ++i) {
+      if ((rc = check_dev_ptr(d_orig[oi], "original shard pointer"))) return rc;
+      blocks[b].in[i] = d_orig[oi++];
+    }
+    blocks[b].out.resize(m);
+    for (size_t j = 0; j < m; ++j) {
+      if ((rc = check_dev_ptr(d_rec[b * m + j], "recovery shard pointer"))) return rc;
+      blocks[b].out[j] = d_rec[b * m + j];
+    }
+  }
+  hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : c.stream;
+  return c.run_blocks(blocks, shard_bytes, s);
+}
+
+int bfrs_decode_batch_dev(bfrs_ctx *ctx, size_t nblocks, const uint32_t *ks, size_t m,
+                          size_t shard_bytes, const uint8_t *const *d_orig,
+                          const uint8_t *const *d_rec, uint8_t *const *d_restored,
+                          void *hip_stream) {
+  if (!ctx || (nblocks && (!ks || !d_orig || !d_rec || !d_restored)))
+    return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_decode_batch_dev: NULL argument");
+  Context &c = ctx->impl;
+  HIP_TRY(hipSetDevice(c.device));
+  std::vector<BlockIO> blocks;
+  blocks.reserve(nblocks);
+  size_t oi = 0;
+  for (size_t b = 0; b < nblocks; ++b) {
+    const size_t k = ks[b];
+    int rc = check_shape(k, m, shard_bytes);
+    if (rc) return rc;
+    std::vector<uint8_t> op(k), rp(m);
+    size_t orig_recv = 0, rec_recv = 0;
+    for (size_t i = 0; i < k; ++i) orig_recv += (op[i] = d_orig[oi + i] != nullptr);
+    for (size_t j = 0; j < m; ++j) rec_recv += (rp[j] = d_rec[b * m + j] != nullptr);
+    if (orig_recv + rec_recv < k) {
+      std::ostringstream os;
+      os << "not enough shards: " << orig_recv << " original + " << rec_recv << " recovery < "
+         << k << " original_count";
+      return set_error(BFRS_E_NOT_ENOUGH_SHARDS, os.str());
+    }
+    if (orig_recv == k) {  // nothing to restore (crate returns an empty result)
+      oi += k;
+      continue;
+    }
+    BlockIO io;
+    if ((rc = c.get_decode_plan(k, m, op, rp, &io.plan))) return rc;
+    for (size_t j = 0; j < m; ++j)
+      if (rp[j]) {
+        if ((rc = check_dev_ptr(d_rec[b * m + j], "recovery shard pointer"))) return rc;
+        io.in.push_back(d_rec[b * m + j]);
+      }
+    for (size_t i = 0; i < k; ++i)
+      if (op[i]) {
+        if ((rc = check_dev_ptr(d_orig[oi + i], "original shard pointer"))) return rc;
+        io.in.push_back(d_orig[oi + i]);
+      } else {
+        if ((rc = check_dev_ptr(d_restored[oi + i], "restored shard pointer"))) return rc;
+        io.out.push_back(d_restored[oi + i]);
+      }
+    oi += k;
+    blocks.push_back(std::move(io));
+  }
+  hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : c.stream;
+  return c.run_blocks(blocks, shard_bytes, s);
+}
+
+// ---- one-shot host-memory API ----------------------------------------------
+int bfrs_encode(bfrs_ctx *ctx, size_t k, size_t m, size_t shard_bytes,
+                const uint8_t *const *originals, uint8_t *const *recovery_out) {
+  if (!ctx || !originals || !recovery_out)
+    return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_encode: NULL argument");
+  int rc = check_shape(k, m, shard_bytes);
+  if (rc) return rc;
+  for (size_t i = 0; i < k; ++i)
+    if (!originals[i]) return set_error(BFRS_E_INVALID_ARGUMENT, "original shard is NULL");
+  for (size_t j = 0; j < m; ++j)
+    if (!recovery_out[j]) return set_error(BFRS_E_INVALID_ARGUMENT, "recovery buffer is NULL");
+  Context &c = ctx->impl;
+  HIP_TRY(hipSetDevice(c.device));
+  const size_t stride = round_up(shard_bytes, 256);
+  void *base;
+  if ((rc = c.scratch(stride * (k + m), &base))) return rc;
+  auto *d = static_cast<uint8_t *>(base);
+  std::vector<const uint8_t *> din(k);
+  std::vector<uint8_t *> dout(m);
+  for (size_t i = 0; i < k; ++i) {
+    din[i] = d + i * stride;
+    HIP_TRY(hipMemcpyAsync(d + i * stride, originals[i], shard_bytes, hipMemcpyHostToDevice,
+                           c.stream));
+  }
+  for (size_t j = 0; j < m; ++j) dout[j] = d + (k + j) * stride;
+  uint32_t kk = uint32_t(k);
+  if ((rc = bfrs_encode_batch_dev(ctx, 1, &kk, m, shard_bytes, din.data(), dout.data(),
+                                  nullptr)))
+    return rc;
+  for (size_t j = 0; j < m; ++j)
+    HIP_TRY(hipMemcpyAsync(recovery_out[j], dout[j], shard_bytes, hipMemcpyDeviceToHost,
+                           c.stream));
+  HIP_TRY(hipStreamSynchronize(c.stream));
+  return BFRS_OK;
+}
+
+int bfrs_decode(bfrs_ctx *ctx, size_t k, size_t m, size_t shard_bytes,
+                const uint8_t *const *originals, const uint8_t *const *recovery,
+                uint8_t *const *restored_out) {
+  if (!ctx || !originals || !recovery || !restored_out)
+    return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_decode: NULL argument");
+  int rc = check_shape(k, m, shard_bytes);
+  if (rc) return rc;
+  Context &c = ctx->impl;
+  HIP_TRY(hipSetDevice(c.device));
+  const size_t stride = round_up(shard_bytes, 256);
+  void *base;
+  if ((rc = c.scratch(stride * (k + m), &base))) return rc;
+  auto *d = static_cast<uint8_t *>(base);
+  std::vector<const uint8_t *> dorig(k), drec(m);
+  std::vector<uint8_t *> drest(k, nullptr);
+  for (size_t i = 0; i < k; ++i) {
+    uint8_t *slot = d + i * stride;
+    if (originals[i]) {
+      HIP_TRY(hipMemcpyAsync(slot, originals[i], shard_bytes, hipMemcpyHostToDevice, c.stream));
+      dorig[i] = slot;
+    } else {
+      if (!restored_out[i])
+        return set_error(BFRS_E_INVALID_ARGUMENT, "restored buffer for erased shard is NULL");
+      drest[i] = slot;
+    }
+  }
+  for (size_t j = 0; j < m; ++j) {
+    if (!recovery[j]) continue;
+    uint8_t *slot = d + (k + j) * stride;
+    HIP_TRY(hipMemcpyAsync(slot, recovery[j], shard_bytes, hipMemcpyHostToDevice, c.stream));
+    drec[j] = slot;
+  }
+  uint32_t kk = uint32_t(k);
+  if ((rc = bfrs_decode_batch_dev(ctx, 1, &kk, m, shard_bytes, dorig.data(), drec.data(),
+                                  drest.data(), nullptr)))
+    return rc;
+  for (size_t i = 0; i < k; ++i)
+    if (!originals[i])
+      HIP_TRY(hipMemcpyAsync(restored_out[i], drest[i], shard_bytes, hipMemcpyDeviceToHost,
+                             c.stream));
+  HIP_TRY(hipStreamSynchronize(c.stream));
+  return BFRS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,86 @@
+// runtime.hpp — internal C++ runtime behind include/bfrs.h.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/bfrs.h"
+#include "kernels.hpp"
+#include "plan.hpp"
+
+namespace bfrs {
+
+// Thread-local error reporting (bfrs_last_error).
+int set_error(int code, const std::string &msg);
+int hip_error(hipError_t e, const char *what);
+
+// One kernel pass of a plan: outputs [r0, r1) x inputs [c0, c1) with its
+// nibble tables resident on the device.
+struct PlanPass {
+  uint32_t r0, r1, c0, c1;
+  uint32_t phase;  // input-group index; phase > 0 accumulates
+  const uint2 *d_table = nullptr;
+};
+
+// A coefficient plan for one (k, m, erasure pattern), tables on device.
+struct Plan {
+  CoefMatrix coef;
+  std::vector<PlanPass> passes;
+  uint32_t n_phases = 0;
+  void *d_tables = nullptr;  // one allocation for all pass tables
+  ~Plan();
+};
+
+// One RS block in a batch: device addresses of its pass inputs/outputs.
+struct BlockIO {
+  const Plan *plan;
+  std::vector<const uint8_t *> in;  // plan.coef.cols device pointers
+  std::vector<uint8_t *> out;       // plan.coef.rows device pointers
+};
+
+struct Context {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::mutex mu;  // guards the plan cache (contexts are single-threaded otherwise)
+  std::map<std::string, std::unique_ptr<Plan>> plans;
+
+  // Descriptor staging ring: pinned host slots + device slots + events.
+  struct Slot {
+    void *host = nullptr;
+    void *dev = nullptr;
+    size_t cap = 0;
+    hipEvent_t done = nullptr;
+    bool used = false;
+  };
+  std::vector<Slot> slots;
+  size_t next_slot = 0;
+
+  // Scratch device memory for the host-memory API.
+  void *d_scratch = nullptr;
+  size_t scratch_cap = 0;
+
+  ~Context();
+  int init(int dev);
+  int get_encode_plan(size_t k, size_t m, const Plan **out);
+  int get_decode_plan(size_t k, size_t m, const std::vector<uint8_t> &orig_present,
+                      const std::vector<uint8_t> &rec_present, const Plan **out);
+  // Queue the passes of all blocks (same shard_bytes) on `stream`.
+  int run_blocks(const std::vector<BlockIO> &blocks, size_t shard_bytes, hipStream_t stream);
+  int scratch(size_t bytes, void **out);
+};
+
+// Argument validation shared by every entry point (crate's Error variants).
+int check_shape(size_t k, size_t m, size_t shard_bytes);
+
+}  // namespace bfrs
+
+struct bfrs_ctx {
+  bfrs::Context impl;
+};

@@ -1,0 +1,175 @@
+/*
+ * bfrs.h — C-ABI of the MI355X-native Reed-Solomon path for BlockFrame.
+ *
+ * This library replaces the bottom box of the reference's hot path: the
+ * third-party crate reed-solomon-simd 3.1.0 (Cargo.toml:18) that BlockFrame
+ * calls from src/chunker/generate.rs, src/filestore/recovery.rs and
+ * src/filestore/health.rs.  Output is bit-exact with that crate's algorithm
+ * (GF(2^16) Leopard/LCH code, 64-byte lo/hi shard layout).
+ *
+ * Plain C types only: pointers, sizes, opaque handles.  No torch, no HIP
+ * types in signatures (a HIP stream is passed as `void *`).
+ *
+ * Error convention: every entry point returns 0 on success or a negative
+ * BFRS_E_* code; it never aborts on bad input (the reference builds with
+ * panic = "abort", Cargo.toml:79).  bfrs_last_error() returns the message of
+ * the calling thread's last failure, using the reference's own strings where
+ * the reference has them (src/filestore/recovery.rs:48,55,124,128,132,138).
+ *
+ * Threading: a context may be used by one thread at a time; distinct
+ * contexts may be used concurrently (also on the same device), mirroring
+ * rayon's one-encoder-per-block use at src/chunker/commit.rs:391-466.
+ */
+#ifndef BFRS_H
+#define BFRS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BFRS_ABI_VERSION 1
+
+/* Error codes.  -1..-10 mirror reed_solomon_simd::Error (3.x). */
+enum {
+  BFRS_OK = 0,
+  BFRS_E_DIFFERENT_SHARD_SIZE = -1,
+  BFRS_E_DUPLICATE_ORIGINAL_SHARD_INDEX = -2,
+  BFRS_E_DUPLICATE_RECOVERY_SHARD_INDEX = -3,
+  BFRS_E_INVALID_ORIGINAL_SHARD_INDEX = -4,
+  BFRS_E_INVALID_RECOVERY_SHARD_INDEX = -5,
+  BFRS_E_INVALID_SHARD_SIZE = -6,
+  BFRS_E_NOT_ENOUGH_SHARDS = -7,
+  BFRS_E_TOO_FEW_ORIGINAL_SHARDS = -8,
+  BFRS_E_TOO_MANY_ORIGINAL_SHARDS = -9,
+  BFRS_E_UNSUPPORTED_SHARD_COUNT = -10,
+  /* BlockFrame wrapper errors (src/chunker/generate.rs, src/filestore/recovery.rs) */
+  BFRS_E_WRAPPER = -20,          /* message in bfrs_last_error(), reference wording */
+  /* Boundary / device errors */
+  BFRS_E_INVALID_ARGUMENT = -30, /* NULL handle/pointer, misaligned device pointer */
+  BFRS_E_HIP = -31,              /* HIP runtime failure; message has hipGetErrorString */
+  BFRS_E_NO_DEVICE = -32,        /* no usable gfx950 device / device id out of range */
+  BFRS_E_NOMEM = -33,
+  BFRS_E_NOT_RESTORED = -34,     /* restored_original(i): index was not restored (None) */
+};
+
+typedef struct bfrs_ctx bfrs_ctx;
+typedef struct bfrs_encoder bfrs_encoder;
+typedef struct bfrs_decoder bfrs_decoder;
+
+/* ---- context --------------------------------------------------------- */
+int bfrs_abi_version(void);
+const char *bfrs_strerror(int code);
+const char *bfrs_last_error(void);
+int bfrs_device_count(void);
+/* Opens a context on HIP device `device` (>= 0).  Fails with BFRS_E_NO_DEVICE
+ * if the device is absent — there is no CPU fallback. */
+int bfrs_open(int device, bfrs_ctx **out);
+void bfrs_close(bfrs_ctx *ctx);
+/* Blocks until all work the context queued has finished. */
+int bfrs_synchronize(bfrs_ctx *ctx);
+
+/* ---- codec rules (pure host logic) ------------------------------------ */
+/* 1 = HighRate, 0 = LowRate (reed-solomon-simd DefaultRate), <0 = unsupported. */
+int bfrs_use_high_rate(size_t original_count, size_t recovery_count);
+/* Encode/decode coefficient of output `out_index` w.r.t. input `in_index`
+ * (GF(2^16), Cantor basis) — exposed for tests and INTEGRATION.md. */
+int bfrs_encode_coefficient(size_t original_count, size_t recovery_count, size_t recovery_index,
+                            size_t original_index, uint16_t *coef_out);
+/* Decode coefficient matrix for an erasure pattern (host logic only).
+ * orig_present[k], rec_present[m] are 0/1.  Rows = missing originals
+ * ascending; cols = present recovery ascending, then present originals
+ * ascending.  Writes rows*cols values row-major if cap allows. */
+int bfrs_plan_decode(size_t original_count, size_t recovery_count, const uint8_t *orig_present,
+                     const uint8_t *rec_present, uint16_t *coef_out, size_t cap, size_t *rows,
+                     size_t *cols);
+
+/* ---- streaming API: mirrors reed_solomon_simd::ReedSolomonEncoder ----- */
+/* replaces ReedSolomonEncoder::new (generate.rs:37,84) */
+int bfrs_encoder_new(bfrs_ctx *ctx, size_t original_count, size_t recovery_count,
+                     size_t shard_bytes, bfrs_encoder **out);
+/* replaces add_original_shard (generate.rs:41,44,88); host memory, copied. */
+int bfrs_encoder_add_original_shard(bfrs_encoder *enc, const uint8_t *shard, size_t len);
+/* replaces encode() (generate.rs:47,92) */
+int bfrs_encoder_encode(bfrs_encoder *enc);
+/* replaces EncoderResult::recovery_iter() (generate.rs:48,96): pointer valid
+ * until the next call on this encoder. */
+int bfrs_encoder_recovery(bfrs_encoder *enc, size_t index, const uint8_t **data, size_t *len);
+void bfrs_encoder_free(bfrs_encoder *enc);
+
+/* ---- streaming API: mirrors reed_solomon_simd::ReedSolomonDecoder ----- */
+/* replaces ReedSolomonDecoder::new (recovery.rs:58,152; health.rs:514,613,733) */
+int bfrs_decoder_new(bfrs_ctx *ctx, size_t original_count, size_t recovery_count,
+                     size_t shard_bytes, bfrs_decoder **out);
+/* replaces add_original_shard(index, shard) (recovery.rs:157; health.rs:737) */
+int bfrs_decoder_add_original_shard(bfrs_decoder *dec, size_t index, const uint8_t *shard,
+                                    size_t len);
+/* replaces add_recovery_shard(index, shard) (recovery.rs:61-63,162-164; health.rs:742) */
+int bfrs_decoder_add_recovery_shard(bfrs_decoder *dec, size_t index, const uint8_t *shard,
+                                    size_t len);
+/* replaces decode() (recovery.rs:65,166; health.rs:746) */
+int bfrs_decoder_decode(bfrs_decoder *dec);
+/* replaces DecoderResult::restored_original(index) (recovery.rs:66-69,167-169):
+ * BFRS_E_NOT_RESTORED plays the role of Option::None. */
+int bfrs_decoder_restored_original(bfrs_decoder *dec, size_t index, const uint8_t **data,
+                                   size_t *len);
+void bfrs_decoder_free(bfrs_decoder *dec);
+
+/* ---- one-shot host-memory API (host buffers in, host buffers out) ----- */
+/* k originals -> m recovery shards; every buffer shard_bytes long, caller-owned. */
+int bfrs_encode(bfrs_ctx *ctx, size_t original_count, size_t recovery_count, size_t shard_bytes,
+                const uint8_t *const *originals, uint8_t *const *recovery_out);
+/* originals[i] == NULL: erased; recovery[j] == NULL: missing.  restored_out[i]
+ * is written only where originals[i] == NULL. */
+int bfrs_decode(bfrs_ctx *ctx, size_t original_count, size_t recovery_count, size_t shard_bytes,
+                const uint8_t *const *originals, const uint8_t *const *recovery,
+                uint8_t *const *restored_out);
+
+/* ---- device-resident batch API (pointers are device memory) ----------- */
+/* Encodes nblocks independent RS blocks in one launch.  Block b has
+ * original_counts[b] originals, all blocks share recovery_count and
+ * shard_bytes.  d_originals holds sum(original_counts) pointers, block by
+ * block; d_recovery holds nblocks*recovery_count pointers.  Pointer arrays
+ * are host arrays of device addresses; shard pointers must be 16-byte
+ * aligned.  Work is queued on `hip_stream` (NULL = the context's stream). */
+int bfrs_encode_batch_dev(bfrs_ctx *ctx, size_t nblocks, const uint32_t *original_counts,
+                          size_t recovery_count, size_t shard_bytes,
+                          const uint8_t *const *d_originals, uint8_t *const *d_recovery,
+                          void *hip_stream);
+/* Same shape; NULL entries mark erased originals / missing recovery shards.
+ * d_restored holds sum(original_counts) pointers; written where erased. */
+int bfrs_decode_batch_dev(bfrs_ctx *ctx, size_t nblocks, const uint32_t *original_counts,
+                          size_t recovery_count, size_t shard_bytes,
+                          const uint8_t *const *d_originals, const uint8_t *const *d_recovery,
+                          uint8_t *const *d_restored, void *hip_stream);
+
+/* ---- BlockFrame wrappers (C++ restatement of the reference functions) -- */
+/* Chunker::generate_parity (src/chunker/generate.rs:59-104): pads every
+ * segment to the longest one, RS(data_shards, parity_shards) encode.
+ * parity_out[p] must hold max(seg_lens) bytes; *parity_len receives it. */
+int bfrs_generate_parity(bfrs_ctx *ctx, const uint8_t *const *segments, const size_t *seg_lens,
+                         size_t n_segments, size_t data_shards, size_t parity_shards,
+                         uint8_t *const *parity_out, size_t *parity_len);
+/* Chunker::generate_parity_segmented (generate.rs:26-57): RS(1,3) of the
+ * data padded to a multiple of 64.  parity_out[0..3] hold ceil64(len) bytes. */
+int bfrs_generate_parity_segmented(bfrs_ctx *ctx, const uint8_t *segment, size_t len,
+                                   uint8_t *const *parity_out, size_t *parity_len);
+/* recover_segment_rs13 (src/filestore/recovery.rs:43-79).  expected_size ==
+ * SIZE_MAX means None.  out must hold the parity length. */
+int bfrs_recover_segment_rs13(bfrs_ctx *ctx, const uint8_t *const *parity,
+                              const size_t *parity_lens, size_t n_parity, size_t expected_size,
+                              uint8_t *out, size_t *out_len);
+/* recover_segment_rs30_3 (recovery.rs:118-173): segments[30] with NULL for
+ * None, block_parity[3], target index.  out must hold the shard size. */
+int bfrs_recover_segment_rs30_3(bfrs_ctx *ctx, const uint8_t *const *segments,
+                                const size_t *seg_lens, size_t n_slots,
+                                const uint8_t *const *block_parity, const size_t *parity_lens,
+                                size_t n_parity, size_t target_index, uint8_t *out,
+                                size_t *out_len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BFRS_H */

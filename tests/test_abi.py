@@ -1,0 +1,102 @@
+"""CPU: the C-ABI library loads, exports exactly what include/bfrs.h declares,
+and its host-side planner reproduces the oracle (no GPU compute here)."""
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from gfnp import apply_matrix
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "bfrs.h")
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def declared_symbols():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(bfrs_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_and_binding_agree(bfrs):
+    assert declared_symbols() == sorted(bfrs.EXPORTS)
+
+
+def test_library_exports_every_declared_symbol(bfrs):
+    lib = bfrs.lib()
+    for name in declared_symbols():
+        assert hasattr(lib, name), name
+    # nothing but the C-ABI is exported
+    import subprocess
+    out = subprocess.run(["nm", "-D", "--defined-only", bfrs.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = sorted(l.split()[-1] for l in out.splitlines() if " T " in l)
+    assert exported == declared_symbols()
+
+
+def test_library_links_hip_not_oracle(bfrs):
+    import subprocess
+    out = subprocess.run(["ldd", bfrs.LIB_PATH], capture_output=True, text=True).stdout
+    assert "amdhip64" in out
+    assert "oracle" not in out
+
+
+def test_abi_version_and_strerror(bfrs):
+    L = bfrs.lib()
+    assert L.bfrs_abi_version() == 1
+    assert L.bfrs_strerror(bfrs.E_NOT_ENOUGH_SHARDS) == b"not enough shards"
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-device path")
+def test_open_without_device_fails_loudly(bfrs):
+    with pytest.raises(bfrs.BfrsError) as e:
+        bfrs.Context(0)
+    assert e.value.code == bfrs.E_NO_DEVICE
+
+
+def test_default_rate_matches_oracle(bfrs, oracle):
+    for k in range(1, 70):
+        for m in (1, 2, 3, 4, 5, 8, 17):
+            assert bfrs.use_high_rate(k, m) == oracle.use_high_rate(k, m), (k, m)
+
+
+@pytest.mark.parametrize("k,m", [(30, 3), (8, 3), (20, 3), (1, 3), (2, 3), (3, 3), (4, 3),
+                                 (16, 4), (10, 1), (65, 5)])
+def test_encode_coefficients_match_oracle(bfrs, oracle, k, m):
+    for i in range(k):
+        unit = [np.zeros(64, np.uint8) for _ in range(k)]
+        unit[i][0] = 1
+        rec = oracle.encode(unit, m)
+        for j in range(m):
+            sym = int(rec[j][0]) | int(rec[j][32]) << 8
+            assert bfrs.encode_coefficient(k, m, j, i) == sym, (j, i)
+
+
+def test_planner_decode_matrices_reproduce_oracle(bfrs, gf_tables):
+    """Applying bfrs_plan_decode's matrix (numpy, test-only) to the golden
+    inputs gives the oracle's restored bytes, including the decodes whose
+    recovery input was deliberately corrupted (pins the exact linear map)."""
+    exp, log = gf_tables
+    g = json.load(open(os.path.join(GOLDEN, "rs_small.json")))
+    checked = 0
+    for c in g["cases"]:
+        k, m, n = c["k"], c["m"], c["shard_bytes"]
+        if n % 64:
+            continue
+        orig = [np.frombuffer(bytes.fromhex(h), np.uint8) for h in c["originals"]]
+        for d in c["decodes"]:
+            rec = [None if h is None else np.frombuffer(bytes.fromhex(h), np.uint8)
+                   for h in d["recovery_used"]]
+            op = [i not in d["erased"] for i in range(k)]
+            rp = [r is not None for r in rec]
+            mat = bfrs.plan_decode(k, m, op, rp)
+            inputs = [r for r in rec if r is not None] + [orig[i] for i in range(k) if op[i]]
+            outs = apply_matrix(mat, inputs, exp, log)
+            missing = [i for i in range(k) if not op[i]]
+            for i, a in zip(missing, outs):
+                assert a.tobytes().hex() == d["restored"][str(i)], (k, m, d["erased"])
+            checked += 1
+    assert checked >= 30

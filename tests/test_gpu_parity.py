@@ -1,0 +1,321 @@
+"""GPU parity: the HIP path through the C-ABI vs the oracle / golden fixtures.
+
+Bit-exact for every byte (integer GF(2^16) work, no tolerance).  Small and
+medium cases compare with the oracle directly; BASELINE config sizes compare
+with committed SHA-256 digests (tests/golden/rs_large.json) and use
+size-independent properties (encode -> erase -> decode round trip, BLAKE3 of
+restored segments against the manifest-style hash of the original).
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _small_cases():
+    return json.load(open(os.path.join(GOLDEN, "rs_small.json")))["cases"]
+
+
+def _np(h):
+    return np.frombuffer(bytes.fromhex(h), np.uint8)
+
+
+# ---------------------------------------------------------------- golden, host API
+@pytest.mark.parametrize("case", _small_cases(), ids=lambda c: f"k{c['k']}m{c['m']}n{c['shard_bytes']}")
+def test_host_encode_golden(ctx, case):
+    orig = [_np(h) for h in case["originals"]]
+    rec = ctx.encode(orig, case["m"])
+    assert [r.tobytes().hex() for r in rec] == case["recovery"]
+
+
+@pytest.mark.parametrize("case", _small_cases(), ids=lambda c: f"k{c['k']}m{c['m']}n{c['shard_bytes']}")
+def test_host_decode_golden(ctx, case):
+    k = case["k"]
+    orig = [_np(h) for h in case["originals"]]
+    for d in case["decodes"]:
+        o = [None if i in d["erased"] else orig[i] for i in range(k)]
+        r = [None if h is None else _np(h) for h in d["recovery_used"]]
+        out = ctx.decode(o, r)
+        assert {str(i): a.tobytes().hex() for i, a in out.items()} == d["restored"]
+
+
+# ---------------------------------------------------------------- device batch API vs oracle
+def _dev_shards(arrs, dev="cuda"):
+    return [torch.from_numpy(a.copy()).to(dev) for a in arrs]
+
+
+@pytest.mark.parametrize("shard_bytes", [64, 8192, 1 << 20, (1 << 20) + 64 * 3, 65536 + 38])
+def test_batch_encode_mixed_blocks_vs_oracle(ctx, oracle, shard_bytes):
+    rng = np.random.default_rng(shard_bytes)
+    ks = [30, 8, 1, 20, 2, 3]
+    host = [[rng.integers(0, 256, shard_bytes, dtype=np.uint8) for _ in range(k)] for k in ks]
+    d_orig = [t for blk in host for t in _dev_shards(blk)]
+    d_rec = [torch.empty(shard_bytes, dtype=torch.uint8, device="cuda") for _ in range(3 * len(ks))]
+    ctx.encode_batch_dev(ks, 3, shard_bytes, d_orig, d_rec)
+    torch.cuda.synchronize()
+    for b, blk in enumerate(host):
+        want = oracle.encode(blk, 3)
+        for j in range(3):
+            got = d_rec[3 * b + j].cpu().numpy()
+            assert np.array_equal(got, want[j]), (b, ks[b], j)
+
+
+def test_batch_decode_random_erasures_vs_oracle(ctx, oracle):
+    rng = np.random.default_rng(7)
+    n = 256 * 1024
+    ks = [30, 30, 8, 20]
+    host = [[rng.integers(0, 256, n, dtype=np.uint8) for _ in range(k)] for k in ks]
+    pars = [oracle.encode(blk, 3) for blk in host]
+    d_orig, d_rec, d_out, erased = [], [], [], []
+    for b, k in enumerate(ks):
+        e = int(rng.integers(1, 4))
+        # erase e data shards, and when e < 3 also drop a parity shard sometimes
+        er = set(rng.choice(k, size=e, replace=False).tolist())
+        drop_par = set() if e == 3 else {int(rng.integers(0, 3))}
+        erased.append((er, drop_par))
+        for i in range(k):
+            d_orig.append(None if i in er else torch.from_numpy(host[b][i]).cuda())
+            d_out.append(torch.empty(n, dtype=torch.uint8, device="cuda") if i in er else None)
+        for j in range(3):
+            d_rec.append(None if j in drop_par else torch.from_numpy(pars[b][j]).cuda())
+    ctx.decode_batch_dev(ks, 3, n, d_orig, d_rec, d_out)
+    torch.cuda.synchronize()
+    off = 0
+    for b, k in enumerate(ks):
+        er, _ = erased[b]
+        for i in range(k):
+            if i in er:
+                assert np.array_equal(d_out[off + i].cpu().numpy(), host[b][i]), (b, i)
+        off += k
+
+
+def test_decode_inconsistent_input_matches_oracle(ctx, oracle):
+    """Corrupted (non-codeword) input: restored bytes must equal the crate
+    decoder's output, i.e. the same linear map, not just 'a' valid decode."""
+    rng = np.random.default_rng(11)
+    n = 4096
+    data = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(30)]
+    par = oracle.encode(data, 3)
+    par[1] = par[1] ^ rng.integers(0, 256, n, dtype=np.uint8)
+    o = [None if i in (4, 17) else data[i] for i in range(30)]
+    want = oracle.decode(o, par)
+    got = ctx.decode(o, par)
+    for i in (4, 17):
+        assert np.array_equal(got[i], want[i])
+
+
+def test_large_code_multiphase(ctx, oracle):
+    """k > 64 inputs (two accumulate phases) and m > 4 outputs (two output groups)."""
+    rng = np.random.default_rng(5)
+    for k, m, n in ((100, 6, 4096), (200, 3, 640)):
+        d = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(k)]
+        want = oracle.encode(d, m)
+        got = ctx.encode(d, m)
+        assert all(np.array_equal(a, b) for a, b in zip(got, want)), (k, m)
+        er = [1, 50, k - 1] + [2, 3, 4][: m - 3]
+        o = [None if i in er else d[i] for i in range(k)]
+        rest = ctx.decode(o, want)
+        for i in er:
+            assert np.array_equal(rest[i], d[i])
+
+
+def test_misaligned_device_pointer_rejected(ctx, bfrs):
+    buf = torch.zeros(4096 + 16, dtype=torch.uint8, device="cuda")
+    bad = buf.data_ptr() + 8
+    outs = [torch.empty(4096, dtype=torch.uint8, device="cuda") for _ in range(3)]
+    with pytest.raises(bfrs.BfrsError) as e:
+        ctx.encode_batch_dev([1], 3, 4096, [bad], outs)
+    assert e.value.code == bfrs.E_INVALID_ARGUMENT
+
+
+# ---------------------------------------------------------------- crate-API mirror
+def test_streaming_encoder_decoder(ctx, bfrs, oracle):
+    rng = np.random.default_rng(2)
+    n = 64 * 100
+    data = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(30)]
+    enc = bfrs.ReedSolomonEncoder(ctx, 30, 3, n)
+    for d in data:
+        enc.add_original_shard(d)
+    rec = list(enc.encode().recovery_iter())
+    assert rec == [r.tobytes() for r in oracle.encode(data, 3)]
+    with pytest.raises(bfrs.BfrsError) as e:
+        enc.add_original_shard(data[0][:64])
+    assert e.value.code == bfrs.E_DIFFERENT_SHARD_SIZE
+
+    dec = bfrs.ReedSolomonDecoder(ctx, 30, 3, n)
+    for i in range(30):
+        if i not in (0, 9, 29):
+            dec.add_original_shard(i, data[i])
+    for j in range(3):
+        dec.add_recovery_shard(j, rec[j])
+    with pytest.raises(bfrs.BfrsError) as e:
+        dec.add_recovery_shard(0, rec[0])
+    assert e.value.code == bfrs.E_DUPLICATE_RECOVERY_SHARD_INDEX
+    dec.decode()
+    for i in (0, 9, 29):
+        assert dec.restored_original(i) == data[i].tobytes()
+    assert dec.restored_original(1) is None  # crate: Option::None for present shards
+
+
+def test_codec_argument_errors(ctx, bfrs):
+    E = bfrs.BfrsError
+    for args, code in (((30, 3, 0), bfrs.E_INVALID_SHARD_SIZE), ((30, 3, 63), bfrs.E_INVALID_SHARD_SIZE),
+                       ((0, 3, 64), bfrs.E_UNSUPPORTED_SHARD_COUNT)):
+        with pytest.raises(E) as e:
+            bfrs.ReedSolomonEncoder(ctx, *args)
+        assert e.value.code == code
+    enc = bfrs.ReedSolomonEncoder(ctx, 2, 3, 64)
+    enc.add_original_shard(np.zeros(64, np.uint8))
+    with pytest.raises(E) as e:
+        enc.encode()
+    assert e.value.code == bfrs.E_TOO_FEW_ORIGINAL_SHARDS
+    enc.add_original_shard(np.zeros(64, np.uint8))
+    with pytest.raises(E) as e:
+        enc.add_original_shard(np.zeros(64, np.uint8))
+    assert e.value.code == bfrs.E_TOO_MANY_ORIGINAL_SHARDS
+    dec = bfrs.ReedSolomonDecoder(ctx, 30, 3, 64)
+    with pytest.raises(E) as e:
+        dec.add_original_shard(30, np.zeros(64, np.uint8))
+    assert e.value.code == bfrs.E_INVALID_ORIGINAL_SHARD_INDEX
+    with pytest.raises(E) as e:
+        dec.add_recovery_shard(3, np.zeros(64, np.uint8))
+    assert e.value.code == bfrs.E_INVALID_RECOVERY_SHARD_INDEX
+    dec.add_original_shard(0, np.zeros(64, np.uint8))
+    with pytest.raises(E) as e:
+        dec.decode()
+    assert e.value.code == bfrs.E_NOT_ENOUGH_SHARDS
+
+
+# ---------------------------------------------------------------- BlockFrame wrappers
+def test_generate_parity_pads_like_reference(ctx, bfrs, oracle):
+    """generate.rs:59-104: segments zero-padded to the longest one."""
+    rng = np.random.default_rng(4)
+    segs = [rng.integers(0, 256, 4096, dtype=np.uint8) for _ in range(7)] + \
+           [rng.integers(0, 256, 1000, dtype=np.uint8)]
+    par = bfrs.Chunker(ctx).generate_parity(segs, 8, 3)
+    padded = [np.pad(s, (0, 4096 - s.size)) for s in segs]
+    assert par == [r.tobytes() for r in oracle.encode(padded, 3)]
+    with pytest.raises(bfrs.BfrsError) as e:
+        bfrs.Chunker(ctx).generate_parity([], 0, 3)
+    assert "No chunks provided" in str(e.value)
+
+
+def test_config1_tier1_8MB_rs13(ctx, bfrs, oracle):
+    """BASELINE config 1: single 8 MB file -> RS(1,3) (copies of the 64-padded
+    data, generate.rs:26-57) and back through recover_segment_rs13."""
+    from bfrs import synth
+    for n in (8 * 1024 * 1024, 8_000_000, 8_000_002):
+        data = synth.segment_np(1, 0, n)
+        par = bfrs.Chunker(ctx).generate_parity_segmented(data)
+        padded = (n + 63) // 64 * 64
+        want = np.pad(data, (0, padded - n)).tobytes()
+        assert par == [want] * 3
+        assert par == [r.tobytes() for r in oracle.encode([np.frombuffer(want, np.uint8)], 3)]
+        rec = bfrs.recover_segment_rs13(ctx, par, expected_size=n)
+        assert rec == data.tobytes()
+        assert oracle.blake3_hex(np.frombuffer(rec, np.uint8)) == oracle.blake3_hex(data)
+    with pytest.raises(bfrs.BfrsError):  # empty file errors (src/chunker/tests.rs:181-194)
+        bfrs.Chunker(ctx).generate_parity_segmented(b"")
+
+
+def test_recovery_wrapper_errors_like_reference(ctx, bfrs):
+    """src/filestore/recovery.rs:196-222."""
+    p = [np.zeros(1024, np.uint8)] * 2
+    with pytest.raises(bfrs.BfrsError) as e:
+        bfrs.recover_segment_rs13(ctx, p)
+    assert "Exactly 3 parity shards required" in str(e.value)
+    with pytest.raises(bfrs.BfrsError) as e:
+        bfrs.recover_segment_rs30_3(ctx, [None] * 30, [np.zeros(1024, np.uint8)] * 3, 0)
+    assert "Too many missing segments" in str(e.value)
+    with pytest.raises(bfrs.BfrsError) as e:
+        bfrs.recover_segment_rs30_3(ctx, [None] * 29, [np.zeros(1024, np.uint8)] * 3, 0)
+    assert "Exactly 30 segment slots required" in str(e.value)
+
+
+def test_recover_segment_rs30_3_roundtrip(ctx, bfrs, oracle):
+    rng = np.random.default_rng(9)
+    n = 1 << 20
+    data = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(30)]
+    par = [np.frombuffer(p, np.uint8) for p in bfrs.Chunker(ctx).generate_parity(data, 30, 3)]
+    slots = [None if i in (3, 14, 27) else data[i] for i in range(30)]
+    for t in (3, 14, 27):
+        got = bfrs.recover_segment_rs30_3(ctx, slots, par, t)
+        assert got == data[t].tobytes()
+    with pytest.raises(bfrs.BfrsError) as e:  # target present -> restored_original None
+        bfrs.recover_segment_rs30_3(ctx, slots, par, 0)
+    assert "Failed to restore target segment" in str(e.value)
+
+
+# ---------------------------------------------------------------- BASELINE config sizes
+def _c2_workload(seed, nseg):
+    from bfrs import synth
+    shapes = synth.block_shapes(nseg)
+    S = synth.SEGMENT_SIZE
+    data = torch.empty(nseg, S, dtype=torch.uint8, device="cuda")
+    for s in range(nseg):
+        synth.fill_segment_torch(data[s], seed, s)
+    return shapes, data
+
+
+@pytest.mark.slow
+def test_config2_encode_128x32MiB_golden(ctx):
+    """BASELINE config 2: 4 x RS(30,3) + RS(8,3) at 32 MiB, bit-exact parity
+    (SHA-256 per shard vs tests/golden/rs_large.json from the oracle)."""
+    g = json.load(open(os.path.join(GOLDEN, "rs_large.json")))["c2_128x32MiB"]
+    shapes, data = _c2_workload(g["seed"], g["segments"])
+    S = g["segment_size"]
+    rec = torch.empty(3 * len(shapes), S, dtype=torch.uint8, device="cuda")
+    d_orig = [data[s] for s in range(g["segments"])]
+    ctx.encode_batch_dev(shapes, 3, S, d_orig, [rec[i] for i in range(rec.shape[0])])
+    torch.cuda.synchronize()
+    for b in range(len(shapes)):
+        for j in range(3):
+            h = hashlib.sha256(rec[3 * b + j].cpu().numpy().tobytes()).hexdigest()
+            assert h == g["parity_sha256"][b][j], (b, j)
+
+
+@pytest.mark.slow
+def test_config3_decode_3_erasures_128x32MiB(ctx, oracle):
+    """BASELINE config 3: per block erase 3 random data shards (seed
+    0xDEC0DE+block), restore on the GPU; restored == original bytes and BLAKE3
+    (the manifest's per-segment hash, src/chunker/commit.rs:429) matches."""
+    from bfrs import synth
+    shapes, data = _c2_workload(0xB10C, 128)
+    S = synth.SEGMENT_SIZE
+    nb = len(shapes)
+    rec = torch.empty(3 * nb, S, dtype=torch.uint8, device="cuda")
+    d_orig = [data[s] for s in range(128)]
+    ctx.encode_batch_dev(shapes, 3, S, d_orig, [rec[i] for i in range(3 * nb)])
+    out = torch.empty(3 * nb, S, dtype=torch.uint8, device="cuda")
+    dd_orig, dd_out, erased = [], [], []
+    seg = 0
+    for b, k in enumerate(shapes):
+        er = sorted(np.random.default_rng(0xDEC0DE + b).choice(k, 3, replace=False).tolist())
+        erased.append(er)
+        for i in range(k):
+            dd_orig.append(None if i in er else data[seg + i])
+            dd_out.append(out[3 * b + er.index(i)] if i in er else None)
+        seg += k
+    ctx.decode_batch_dev(shapes, 3, S, dd_orig, [rec[i] for i in range(3 * nb)], dd_out)
+    torch.cuda.synchronize()
+    seg = 0
+    for b, k in enumerate(shapes):
+        for t, i in enumerate(erased[b]):
+            assert torch.equal(out[3 * b + t], data[seg + i]), (b, i)
+        seg += k
+    # BLAKE3 re-verify of one restored segment against its original's hash
+    b0 = out[0].cpu().numpy()
+    assert oracle.blake3_hex(b0) == oracle.blake3_hex(data[erased[0][0]].cpu().numpy())
+
+
+def test_in_tree_library_is_the_one_loaded(bfrs):
+    import ctypes.util  # noqa: F401
+    maps = open("/proc/self/maps").read()
+    assert bfrs.LIB_PATH in maps
