@@ -225,7 +225,8 @@ class Context:
         po, ko = _ptr_array([self._addr(t) for t in d_originals])
         pr, kr = _ptr_array([self._addr(t) for t in d_recovery])
         _check(lib().bfrs_encode_batch_dev(self.handle, len(original_counts), ks, recovery_count,
-                                           shard_bytes, po, pr, _stream_handle(stream)))
+                                           shard_bytes, po, pr,
+                                           _stream_handle(stream, list(d_originals) + list(d_recovery))))
 
     def decode_batch_dev(self, original_counts, recovery_count, shard_bytes, d_originals,
                          d_recovery, d_restored, stream=None) -> None:
@@ -234,7 +235,9 @@ class Context:
         pr, kr = _ptr_array([self._addr(t) for t in d_recovery])
         pd, kd = _ptr_array([self._addr(t) for t in d_restored])
         _check(lib().bfrs_decode_batch_dev(self.handle, len(original_counts), ks, recovery_count,
-                                           shard_bytes, po, pr, pd, _stream_handle(stream)))
+                                           shard_bytes, po, pr, pd,
+                                           _stream_handle(stream, list(d_originals) + list(d_recovery)
+                                                          + list(d_restored))))
 
     # ---- one-shot host API (numpy in, numpy out)
     def encode(self, originals, recovery_count=3):
@@ -260,8 +263,14 @@ class Context:
         return {i: a for i, a in enumerate(out) if a is not None}
 
 
-def _stream_handle(stream) -> Optional[int]:
+def _stream_handle(stream, tensors=()) -> Optional[int]:
+    """None -> torch's current stream when torch tensors are passed (so the
+    codec is ordered after the kernels that produced them), else the
+    context's own stream."""
     if stream is None:
+        if any(hasattr(t, "data_ptr") for t in tensors):
+            import torch
+            return torch.cuda.current_stream().cuda_stream
         return None
     if isinstance(stream, int):
         return stream
