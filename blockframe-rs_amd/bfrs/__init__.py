@@ -265,8 +265,8 @@ class Context:
 
 def _stream_handle(stream, tensors=()) -> Optional[int]:
     """None -> torch's current stream when torch tensors are passed (so the
-    codec is ordered after the kernels that produced them), else the
-    context's own stream."""
+    codec is ordered after the kernels that produced them), else HIP's
+    default stream (the C-ABI's NULL)."""
     if stream is None:
         if any(hasattr(t, "data_ptr") for t in tensors):
             import torch

@@ -105,8 +105,8 @@ int bfrs_encoder_encode(bfrs_encoder *e) {
   for (size_t i = 0; i < e->k; ++i) din[i] = d + i * st;
   for (size_t j = 0; j < e->m; ++j) dout[j] = d + (e->k + j) * st;
   uint32_t kk = uint32_t(e->k);
-  int rc = bfrs_encode_batch_dev(e->ctx, 1, &kk, e->m, e->shard_bytes, din.data(), dout.data(),
-                                 nullptr);
+  int rc = encode_batch_on(e->ctx, 1, &kk, e->m, e->shard_bytes, din.data(), dout.data(),
+                           e->ctx->impl.stream);
   if (rc) return rc;
   e->recovery.assign(e->m, std::vector<uint8_t>(e->shard_bytes));
   Context &c = e->ctx->impl;
@@ -240,8 +240,8 @@ int bfrs_decoder_decode(bfrs_decoder *d) {
   for (size_t j = 0; j < d->m; ++j)
     if (d->rec_present[j]) drec[j] = base + (d->k + j) * st;
   uint32_t kk = uint32_t(d->k);
-  int rc = bfrs_decode_batch_dev(d->ctx, 1, &kk, d->m, d->shard_bytes, dorig.data(), drec.data(),
-                                 drest.data(), nullptr);
+  int rc = decode_batch_on(d->ctx, 1, &kk, d->m, d->shard_bytes, dorig.data(), drec.data(),
+                           drest.data(), d->ctx->impl.stream);
   if (rc) return rc;
   Context &c = d->ctx->impl;
   for (size_t i = 0; i < d->k; ++i)

@@ -3,6 +3,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include <cstdint>
 
 namespace bfrs {
@@ -17,9 +19,9 @@ constexpr uint32_t kTileHalfChunks = 256;
 // One pass: out[t] (^)= sum_i coef(t,i) * in[i] for t < n_out, over the
 // 64-byte-chunk symbol layout of reed-solomon-simd.
 struct alignas(16) PassDesc {
-  const uint8_t *const *in;  // n_in device pointers (16-byte aligned)
-  uint8_t *const *out;       // n_out device pointers
-  const uint2 *table;        // n_in * 64 packed nibble products
+  uint64_t in;               // device address of n_in shard addresses (16-byte aligned)
+  uint64_t out;              // device address of n_out shard addresses
+  uint64_t table;            // device address of n_in * 64 packed nibble products (uint2)
   uint32_t n_in, n_out;
   uint32_t wg_begin;         // first workgroup of this pass in the grid
   uint32_t n_tiles;          // tiles in this pass

@@ -13,21 +13,41 @@
 //
 // Arithmetic: multiplication of a 16-bit symbol by a constant is GF(2)-linear,
 // so coef*x = T0[x&15] ^ T1[(x>>4)&15] ^ T2[(x>>8)&15] ^ T3[x>>12] with 16-entry
-// nibble tables.  One table entry packs the products for up to 4 outputs:
-// low dword = the 4 outputs' low bytes, high dword = their high bytes.  A
-// 16-entry x 8-byte table spans 32 LDS banks, so a ds_read_b64 with
-// arbitrary nibbles per lane is bank-conflict free.  Per symbol and input: 4
-// LDS lookups + XORs, independent of the number of outputs (<= 4).
+// nibble tables.  One 8-byte table entry packs the products for up to 4
+// outputs: low dword = the outputs' low bytes, high dword = their high bytes.
+// A 16-entry x 8-byte table spans 32 LDS banks, so a ds_read_b64 with any
+// nibble per lane is bank-conflict free.  Per symbol and input: 4 LDS lookups
+// and ~10 VALU, independent of the number of outputs (<= 4).
+//
+// LDS table layout per input i (512 B): [q][v] at i*512 + q*128 + v*8, with
+// q = 0/1 low/high nibble of the symbol's low byte, q = 2/3 of its high byte.
+// Address of a lookup: byte 0 = (q&1)*128 + 8*v, bytes 1-2 = 2i + (q>>1).
+// Byte 0 for four symbols at once comes from one shift+mask of the data dword
+// (nibble*8 per byte, bit 7 set for the high nibble); one v_perm_b32 then
+// splices byte b of it under the wave-uniform (2i + q>>1) -> 1 VALU/lookup.
 #include "kernels.hpp"
 
 namespace bfrs {
 namespace {
 
-__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) { return a ^ b ^ c; }
+#define AS_GLOBAL __attribute__((address_space(1)))
+#define AS_LDS __attribute__((address_space(3)))
+#define AS_CONST __attribute__((address_space(4)))
 
-// acc_lo[s] / acc_hi[s]: packed low/high output bytes of symbol s (byte t = output t).
-__device__ __forceinline__ void mac_input(const uint4 &L, const uint4 &H, const uint2 *__restrict__ T,
-                                          uint32_t (&acc_lo)[16], uint32_t (&acc_hi)[16]) {
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+// LDS read at an absolute LDS byte address (the dynamic LDS table starts at 0:
+// the kernel declares no static LDS).
+__device__ __forceinline__ uint2 lds_entry(const char *, uint32_t byte_addr) {
+  const uint64_t v = *(const AS_LDS uint64_t *)(uintptr_t)byte_addr;
+  return make_uint2(uint32_t(v), uint32_t(v >> 32));
+}
+
+// Variant 0: straightforward indexing (kept for A/B).
+__device__ __forceinline__ void mac_input_v0(const uint4 &L, const uint4 &H, const uint2 *T,
+                                             uint32_t (&acc_lo)[16], uint32_t (&acc_hi)[16]) {
   const uint32_t l[4] = {L.x, L.y, L.z, L.w};
   const uint32_t h[4] = {H.x, H.y, H.z, H.w};
 #pragma unroll
@@ -37,13 +57,54 @@ __device__ __forceinline__ void mac_input(const uint4 &L, const uint4 &H, const 
       const int s = d * 4 + b;
       const uint32_t lb = (l[d] >> (8 * b)) & 0xFF;
       const uint32_t hb = (h[d] >> (8 * b)) & 0xFF;
-      const uint2 e0 = T[lb & 15];
-      const uint2 e1 = T[16 + (lb >> 4)];
-      const uint2 e2 = T[32 + (hb & 15)];
-      const uint2 e3 = T[48 + (hb >> 4)];
-      acc_lo[s] = xor3(acc_lo[s], e0.x, e1.x) ^ xor3(e2.x, e3.x, 0);
-      acc_hi[s] = xor3(acc_hi[s], e0.y, e1.y) ^ xor3(e2.y, e3.y, 0);
+      const uint2 e0 = T[lb & 15], e1 = T[16 + (lb >> 4)], e2 = T[32 + (hb & 15)],
+                  e3 = T[48 + (hb >> 4)];
+      acc_lo[s] ^= e0.x ^ e1.x ^ e2.x ^ e3.x;
+      acc_hi[s] ^= e0.y ^ e1.y ^ e2.y ^ e3.y;
     }
+  }
+}
+
+// Variant 1: v_perm addressing + 3-input XOR.  base_lo = 2i, base_hi = 2i+1.
+__device__ __forceinline__ void mac_input_v1(const uint4 &L, const uint4 &H, const char *lds,
+                                             uint32_t base_lo, uint32_t base_hi,
+                                             uint32_t (&acc_lo)[16], uint32_t (&acc_hi)[16]) {
+  const uint32_t l[4] = {L.x, L.y, L.z, L.w};
+  const uint32_t h[4] = {H.x, H.y, H.z, H.w};
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const uint32_t ll = (l[d] << 3) & 0x78787878u;
+    const uint32_t lh = ((l[d] >> 1) & 0x78787878u) | 0x80808080u;
+    const uint32_t hl = (h[d] << 3) & 0x78787878u;
+    const uint32_t hh = ((h[d] >> 1) & 0x78787878u) | 0x80808080u;
+    uint2 e[4][4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      // selector: byte0 <- byte b of the nibble word, byte1..2 <- base, byte3 <- 0
+      const uint32_t sel = 0x0C050400u | uint32_t(b);
+      e[b][0] = lds_entry(lds, __builtin_amdgcn_perm(base_lo, ll, sel));
+      e[b][1] = lds_entry(lds, __builtin_amdgcn_perm(base_lo, lh, sel));
+      e[b][2] = lds_entry(lds, __builtin_amdgcn_perm(base_hi, hl, sel));
+      e[b][3] = lds_entry(lds, __builtin_amdgcn_perm(base_hi, hh, sel));
+    }
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int s = d * 4 + b;
+      acc_lo[s] = xor3(xor3(acc_lo[s], e[b][0].x, e[b][1].x), e[b][2].x, e[b][3].x);
+      acc_hi[s] = xor3(xor3(acc_hi[s], e[b][0].y, e[b][1].y), e[b][2].y, e[b][3].y);
+    }
+  }
+}
+
+// Variant 9 (measurement only, NOT a codec): same memory traffic, no tables.
+__device__ __forceinline__ void mac_input_stream(const uint4 &L, const uint4 &H,
+                                                 uint32_t (&acc_lo)[16], uint32_t (&acc_hi)[16]) {
+  const uint32_t l[4] = {L.x, L.y, L.z, L.w};
+  const uint32_t h[4] = {H.x, H.y, H.z, H.w};
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    acc_lo[s] ^= l[s >> 2];
+    acc_hi[s] ^= h[s >> 2];
   }
 }
 
@@ -54,13 +115,55 @@ __device__ __forceinline__ uint32_t gather_byte(const uint32_t (&acc)[16], int d
          (((acc[4 * d + 2] >> sh) & 0xFF) << 16) | (((acc[4 * d + 3] >> sh) & 0xFF) << 24);
 }
 
-__device__ __forceinline__ uint4 load16(const uint8_t *p) {
-  return *reinterpret_cast<const uint4 *>(p);
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint4 load16(uint64_t a) {
+  const u32x4 v = *(const AS_GLOBAL u32x4 *)(uintptr_t)a;
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void store16(uint64_t a, const uint4 &v) {
+  u32x4 w = {v.x, v.y, v.z, v.w};
+  *(AS_GLOBAL u32x4 *)(uintptr_t)a = w;
 }
 
-__global__ __launch_bounds__(256) void gf_apply_kernel(const PassDesc *__restrict__ passes,
+// Inline-asm streaming loads (see the pipeline comment in gf_apply_kernel).
+// saddr form: 64-bit wave-uniform shard base in SGPRs + 32-bit lane offset.
+__device__ __forceinline__ void gload_half_chunk(u32x4 &L, u32x4 &H, uint64_t base,
+                                                 uint32_t voff) {
+  asm volatile(
+      "global_load_dwordx4 %0, %2, %3\n\t"
+      "global_load_dwordx4 %1, %2, %3 offset:32"
+      : "=&v"(L), "=&v"(H)
+      : "v"(voff), "s"(base)
+      : "memory");
+}
+// Wait until at most N vector-memory ops are outstanding; L/H are in/out
+// operands so no consumer can be scheduled above the wait.
+template <int N>
+__device__ __forceinline__ void vm_wait(u32x4 &L, u32x4 &H) {
+  asm volatile("s_waitcnt vmcnt(%2)" : "+v"(L), "+v"(H) : "n"(N) : "memory");
+}
+
+template <int VARIANT>
+__device__ __forceinline__ void mac_input(const u32x4 &Lv, const u32x4 &Hv, uint32_t i,
+                                          uint32_t (&acc_lo)[16], uint32_t (&acc_hi)[16]) {
+  const uint4 L = make_uint4(Lv.x, Lv.y, Lv.z, Lv.w), H = make_uint4(Hv.x, Hv.y, Hv.z, Hv.w);
+  extern __shared__ __attribute__((aligned(16))) uint2 lds_table[];
+  if constexpr (VARIANT == 0) {
+    mac_input_v0(L, H, lds_table + i * 64, acc_lo, acc_hi);
+  } else if constexpr (VARIANT == 9) {
+    mac_input_stream(L, H, acc_lo, acc_hi);
+  } else {
+    mac_input_v1(L, H, nullptr, 2 * i, 2 * i + 1, acc_lo, acc_hi);
+  }
+}
+
+template <int VARIANT>
+__global__ __launch_bounds__(256) void gf_apply_kernel(const PassDesc *__restrict__ passes_g,
                                                        uint32_t n_passes, uint32_t tiles_per_wg) {
   extern __shared__ __attribute__((aligned(16))) uint2 lds_table[];
+  // Descriptors and pointer arrays are read-only and wave-uniform: scalar loads.
+  const AS_CONST PassDesc *passes = (const AS_CONST PassDesc *)(uintptr_t)passes_g;
 
   // Locate this workgroup's pass (wave-uniform binary search over wg_begin).
   const uint32_t wg = blockIdx.x;
@@ -72,10 +175,27 @@ __global__ __launch_bounds__(256) void gf_apply_kernel(const PassDesc *__restric
     else
       hi = mid;
   }
-  const PassDesc &P = passes[lo];
+  const AS_CONST PassDesc &P = passes[lo];
   const uint32_t n_in = P.n_in, n_out = P.n_out;
+  const AS_CONST uint64_t *in = (const AS_CONST uint64_t *)(uintptr_t)P.in;
 
-  for (uint32_t e = threadIdx.x; e < n_in * 64; e += blockDim.x) lds_table[e] = P.table[e];
+  // Table -> LDS: all loads issued before any store (n_in <= 64: <= 8 x 16 B per lane).
+  {
+    const AS_GLOBAL u32x4 *tab = (const AS_GLOBAL u32x4 *)(uintptr_t)P.table;
+    u32x4 *dst = reinterpret_cast<u32x4 *>(lds_table);
+    const uint32_t n16 = n_in * 32;
+    u32x4 v[kMaxPassInputs * 32 / 256];
+#pragma unroll
+    for (int r = 0; r < int(kMaxPassInputs * 32 / 256); ++r) {
+      const uint32_t e = threadIdx.x + 256u * r;
+      v[r] = e < n16 ? tab[e] : u32x4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int r = 0; r < int(kMaxPassInputs * 32 / 256); ++r) {
+      const uint32_t e = threadIdx.x + 256u * r;
+      if (e < n16) dst[e] = v[r];
+    }
+  }
   __syncthreads();
 
   const uint64_t full_hc = P.full_chunks * 2;
@@ -91,33 +211,39 @@ __global__ __launch_bounds__(256) void gf_apply_kernel(const PassDesc *__restric
 #pragma unroll
     for (int s = 0; s < 16; ++s) acc_lo[s] = acc_hi[s] = 0;
 
-    // Software pipeline: loads of input i+1 are in flight while input i computes.
-    uint4 L = load16(P.in[0] + off), H = load16(P.in[0] + off + 32);
-    for (uint32_t i = 0; i < n_in; ++i) {
-      uint4 Ln = L, Hn = H;
-      if (i + 1 < n_in) {
-        const uint8_t *src = P.in[i + 1];
-        Ln = load16(src + off);
-        Hn = load16(src + off + 32);
-      }
-      mac_input(L, H, lds_table + i * 64, acc_lo, acc_hi);
-      L = Ln;
-      H = Hn;
+    // Ping-pong software pipeline: input i+1 loads while input i computes.
+    // The host pads every pass to an even input count (pad inputs have zero
+    // tables) and appends one extra pointer (a duplicate of the last input),
+    // so the loop has no guards.  Loads are inline asm with explicit
+    // vmcnt waits: hipcc otherwise sinks prefetches next to their uses.
+    const uint32_t voff = uint32_t(off);
+    u32x4 La, Ha, Lb, Hb;
+    gload_half_chunk(La, Ha, in[0], voff);
+    for (uint32_t i = 0; i < n_in; i += 2) {
+      gload_half_chunk(Lb, Hb, in[i + 1], voff);
+      vm_wait<2>(La, Ha);
+      mac_input<VARIANT>(La, Ha, i, acc_lo, acc_hi);
+      gload_half_chunk(La, Ha, in[i + 2], voff);
+      vm_wait<2>(Lb, Hb);
+      mac_input<VARIANT>(Lb, Hb, i + 1, acc_lo, acc_hi);
     }
+    vm_wait<0>(La, Ha);  // drain the final (unused) prefetch
 
+    const AS_CONST uint64_t *outp = (const AS_CONST uint64_t *)(uintptr_t)P.out;
+    const bool accumulate = P.accumulate != 0;
     for (uint32_t t = 0; t < n_out; ++t) {
       uint4 ol = make_uint4(gather_byte(acc_lo, 0, t), gather_byte(acc_lo, 1, t),
                             gather_byte(acc_lo, 2, t), gather_byte(acc_lo, 3, t));
       uint4 oh = make_uint4(gather_byte(acc_hi, 0, t), gather_byte(acc_hi, 1, t),
                             gather_byte(acc_hi, 2, t), gather_byte(acc_hi, 3, t));
-      uint8_t *dst = P.out[t] + off;
-      if (P.accumulate) {
+      const uint64_t dst = outp[t] + off;
+      if (accumulate) {
         const uint4 pl = load16(dst), ph = load16(dst + 32);
         ol.x ^= pl.x; ol.y ^= pl.y; ol.z ^= pl.z; ol.w ^= pl.w;
         oh.x ^= ph.x; oh.y ^= ph.y; oh.z ^= ph.z; oh.w ^= ph.w;
       }
-      *reinterpret_cast<uint4 *>(dst) = ol;
-      *reinterpret_cast<uint4 *>(dst + 32) = oh;
+      store16(dst, ol);
+      store16(dst + 32, oh);
     }
   }
 }
@@ -132,16 +258,19 @@ __global__ __launch_bounds__(64) void gf_tail_kernel(const PassDesc *__restrict_
   if (P.tail_bytes == 0 || s >= half) return;
   const uint64_t base = P.full_chunks * 64;
   uint32_t acc_lo = 0, acc_hi = 0;
+  const uint64_t *in = (const uint64_t *)(uintptr_t)P.in;
+  const uint64_t *outp = (const uint64_t *)(uintptr_t)P.out;
   for (uint32_t i = 0; i < P.n_in; ++i) {
-    const uint32_t lb = P.in[i][base + s], hb = P.in[i][base + half + s];
-    const uint2 *T = P.table + i * 64;
+    const uint8_t *src = (const uint8_t *)(uintptr_t)in[i];
+    const uint32_t lb = src[base + s], hb = src[base + half + s];
+    const uint2 *T = (const uint2 *)(uintptr_t)P.table + i * 64;
     const uint2 e0 = T[lb & 15], e1 = T[16 + (lb >> 4)], e2 = T[32 + (hb & 15)],
                 e3 = T[48 + (hb >> 4)];
     acc_lo ^= e0.x ^ e1.x ^ e2.x ^ e3.x;
     acc_hi ^= e0.y ^ e1.y ^ e2.y ^ e3.y;
   }
   for (uint32_t t = 0; t < P.n_out; ++t) {
-    uint8_t *dst = P.out[t] + base;
+    uint8_t *dst = (uint8_t *)(uintptr_t)outp[t] + base;
     uint8_t vl = uint8_t(acc_lo >> (8 * t)), vh = uint8_t(acc_hi >> (8 * t));
     if (P.accumulate) {
       vl ^= dst[s];
@@ -154,12 +283,32 @@ __global__ __launch_bounds__(64) void gf_tail_kernel(const PassDesc *__restrict_
 
 }  // namespace
 
+// Kernel variant selector for A/B measurement (tools/kbench.py).  Variant 9
+// is a traffic-only probe and is refused unless BFRS_ALLOW_PROBE=1.
+int kernel_variant() {
+  const char *e = std::getenv("BFRS_KERNEL_VARIANT");
+  int v = e ? atoi(e) : 1;
+  if (v == 9 && !std::getenv("BFRS_ALLOW_PROBE")) v = 1;
+  return v;
+}
+
 hipError_t launch_gf_apply(const PassDesc *d_passes, uint32_t n_passes, uint32_t n_wgs,
                            uint32_t tiles_per_wg, uint32_t max_in, hipStream_t stream) {
   if (n_wgs == 0) return hipSuccess;
   const size_t lds = size_t(max_in) * 64 * sizeof(uint2);
-  hipLaunchKernelGGL(gf_apply_kernel, dim3(n_wgs), dim3(256), lds, stream, d_passes, n_passes,
-                     tiles_per_wg);
+  switch (kernel_variant()) {
+    case 0:
+      hipLaunchKernelGGL(gf_apply_kernel<0>, dim3(n_wgs), dim3(256), lds, stream, d_passes,
+                         n_passes, tiles_per_wg);
+      break;
+    case 9:
+      hipLaunchKernelGGL(gf_apply_kernel<9>, dim3(n_wgs), dim3(256), lds, stream, d_passes,
+                         n_passes, tiles_per_wg);
+      break;
+    default:
+      hipLaunchKernelGGL(gf_apply_kernel<1>, dim3(n_wgs), dim3(256), lds, stream, d_passes,
+                         n_passes, tiles_per_wg);
+  }
   return hipGetLastError();
 }
 

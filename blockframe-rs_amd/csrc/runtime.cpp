@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 #include <sstream>
 
@@ -70,6 +71,9 @@ static int upload_plan(Plan *p) {
     for (size_t c0 = 0; c0 < c.cols; c0 += kMaxPassInputs) {
       const size_t c1 = std::min(c.cols, c0 + kMaxPassInputs);
       build_tables(c, r0, r1, c0, c1, &t);
+      // The kernel consumes inputs in pairs: pad odd passes with one input
+      // whose table is all zeros (it reads a duplicate pointer, adds nothing).
+      if ((c1 - c0) & 1) t.resize(t.size() + 128, 0);
       offs.push_back(all.size());
       all.insert(all.end(), t.begin(), t.end());
       PlanPass pp;
@@ -189,7 +193,7 @@ int Context::run_blocks(const std::vector<BlockIO> &blocks, size_t shard_bytes,
       for (const PlanPass &p : b.plan->passes)
         if (p.phase == phase) {
           items.push_back({&b, &p});
-          max_in = std::max(max_in, p.c1 - p.c0);
+          max_in = std::max(max_in, (p.c1 - p.c0 + 1) & ~1u);
         }
     if (items.empty()) continue;
 
@@ -201,7 +205,9 @@ int Context::run_blocks(const std::vector<BlockIO> &blocks, size_t shard_bytes,
 
     // Staging layout: [PassDesc x n][pointer arrays].
     size_t n_ptrs = 0;
-    for (const Item &it : items) n_ptrs += (it.p->c1 - it.p->c0) + (it.p->r1 - it.p->r0);
+    // per pass: inputs padded to even + 1 prefetch pointer, then outputs
+    for (const Item &it : items)
+      n_ptrs += ((it.p->c1 - it.p->c0 + 1) & ~1u) + 1 + (it.p->r1 - it.p->r0);
     const size_t desc_bytes = round_up(items.size() * sizeof(PassDesc), 16);
     const size_t bytes = desc_bytes + n_ptrs * sizeof(void *);
 
@@ -225,12 +231,15 @@ int Context::run_blocks(const std::vector<BlockIO> &blocks, size_t shard_bytes,
       const BlockIO &b = *items[i].b;
       const PlanPass &p = *items[i].p;
       PassDesc d{};
-      d.in = reinterpret_cast<const uint8_t *const *>(dev_ptrs + pi * 8);
+      d.in = dev_ptrs + pi * 8;
+      const uint32_t n_real = p.c1 - p.c0, n_pad = (n_real + 1) & ~1u;
       for (uint32_t c = p.c0; c < p.c1; ++c) ptrs[pi++] = reinterpret_cast<uint64_t>(b.in[c]);
-      d.out = reinterpret_cast<uint8_t *const *>(dev_ptrs + pi * 8);
+      const uint64_t last = reinterpret_cast<uint64_t>(b.in[p.c1 - 1]);
+      for (uint32_t c = n_real; c < n_pad + 1; ++c) ptrs[pi++] = last;
+      d.out = dev_ptrs + pi * 8;
       for (uint32_t r = p.r0; r < p.r1; ++r) ptrs[pi++] = reinterpret_cast<uint64_t>(b.out[r]);
-      d.table = p.d_table;
-      d.n_in = p.c1 - p.c0;
+      d.table = reinterpret_cast<uint64_t>(p.d_table);
+      d.n_in = n_pad;
       d.n_out = p.r1 - p.r0;
       d.wg_begin = wg;
       d.n_tiles = n_tiles;
@@ -241,6 +250,14 @@ int Context::run_blocks(const std::vector<BlockIO> &blocks, size_t shard_bytes,
       wg += wgs_per_pass;
     }
     HIP_TRY(hipMemcpyAsync(slot.dev, slot.host, bytes, hipMemcpyHostToDevice, s));
+    if (std::getenv("BFRS_DEBUG_DESC")) {  // diagnostics: verify the upload landed
+      HIP_TRY(hipStreamSynchronize(s));
+      std::vector<char> back(bytes);
+      HIP_TRY(hipMemcpy(back.data(), slot.dev, bytes, hipMemcpyDeviceToHost));
+      if (std::memcmp(back.data(), slot.host, bytes) != 0)
+        fprintf(stderr, "bfrs: descriptor upload mismatch (slot %zu)\n",
+                size_t(&slot - slots.data()));
+    }
     const auto *d_desc = static_cast<const PassDesc *>(slot.dev);
     if (wg) HIP_TRY(launch_gf_apply(d_desc, uint32_t(items.size()), wg, tpw, max_in, s));
     if (tail) HIP_TRY(launch_gf_tail(d_desc, uint32_t(items.size()), s));
@@ -355,7 +372,7 @@ int bfrs_plan_decode(size_t k, size_t m, const uint8_t *orig_present, const uint
 }
 
 // ---- batch (device-resident) ------------------------------------------------
-static int check_dev_ptr(const void *p, const char *what) {
+int check_dev_ptr(const void *p, const char *what) {
   if (!p) return set_error(BFRS_E_INVALID_ARGUMENT, std::string(what) + " is NULL");
   if (reinterpret_cast<uintptr_t>(p) & 15)
     return set_error(BFRS_E_INVALID_ARGUMENT, std::string(what) + " is not 16-byte aligned");
@@ -365,6 +382,25 @@ static int check_dev_ptr(const void *p, const char *what) {
 int bfrs_encode_batch_dev(bfrs_ctx *ctx, size_t nblocks, const uint32_t *ks, size_t m,
                           size_t shard_bytes, const uint8_t *const *d_orig,
                           uint8_t *const *d_rec, void *hip_stream) {
+  return encode_batch_on(ctx, nblocks, ks, m, shard_bytes, d_orig, d_rec,
+                         static_cast<hipStream_t>(hip_stream));
+}
+
+int bfrs_decode_batch_dev(bfrs_ctx *ctx, size_t nblocks, const uint32_t *ks, size_t m,
+                          size_t shard_bytes, const uint8_t *const *d_orig,
+                          const uint8_t *const *d_rec, uint8_t *const *d_restored,
+                          void *hip_stream) {
+  return decode_batch_on(ctx, nblocks, ks, m, shard_bytes, d_orig, d_rec, d_restored,
+                         static_cast<hipStream_t>(hip_stream));
+}
+
+}  // extern "C"
+
+namespace bfrs {
+
+int encode_batch_on(bfrs_ctx *ctx, size_t nblocks, const uint32_t *ks, size_t m,
+                    size_t shard_bytes, const uint8_t *const *d_orig, uint8_t *const *d_rec,
+                    hipStream_t s) {
   if (!ctx || (nblocks && (!ks || !d_orig || !d_rec)))
     return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_encode_batch_dev: NULL argument");
   Context &c = ctx->impl;
@@ -387,14 +423,12 @@ int bfrs_encode_batch_dev(bfrs_ctx *ctx, size_t nblocks, const uint32_t *ks, siz
       blocks[b].out[j] = d_rec[b * m + j];
     }
   }
-  hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : c.stream;
   return c.run_blocks(blocks, shard_bytes, s);
 }
 
-int bfrs_decode_batch_dev(bfrs_ctx *ctx, size_t nblocks, const uint32_t *ks, size_t m,
-                          size_t shard_bytes, const uint8_t *const *d_orig,
-                          const uint8_t *const *d_rec, uint8_t *const *d_restored,
-                          void *hip_stream) {
+int decode_batch_on(bfrs_ctx *ctx, size_t nblocks, const uint32_t *ks, size_t m,
+                    size_t shard_bytes, const uint8_t *const *d_orig, const uint8_t *const *d_rec,
+                    uint8_t *const *d_restored, hipStream_t s) {
   if (!ctx || (nblocks && (!ks || !d_orig || !d_rec || !d_restored)))
     return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_decode_batch_dev: NULL argument");
   Context &c = ctx->impl;
@@ -438,9 +472,12 @@ int bfrs_decode_batch_dev(bfrs_ctx *ctx, size_t nblocks, const uint32_t *ks, siz
     oi += k;
     blocks.push_back(std::move(io));
   }
-  hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : c.stream;
   return c.run_blocks(blocks, shard_bytes, s);
 }
+
+}  // namespace bfrs
+
+extern "C" {
 
 // ---- one-shot host-memory API ----------------------------------------------
 int bfrs_encode(bfrs_ctx *ctx, size_t k, size_t m, size_t shard_bytes,
@@ -468,8 +505,7 @@ int bfrs_encode(bfrs_ctx *ctx, size_t k, size_t m, size_t shard_bytes,
   }
   for (size_t j = 0; j < m; ++j) dout[j] = d + (k + j) * stride;
   uint32_t kk = uint32_t(k);
-  if ((rc = bfrs_encode_batch_dev(ctx, 1, &kk, m, shard_bytes, din.data(), dout.data(),
-                                  nullptr)))
+  if ((rc = encode_batch_on(ctx, 1, &kk, m, shard_bytes, din.data(), dout.data(), c.stream)))
     return rc;
   for (size_t j = 0; j < m; ++j)
     HIP_TRY(hipMemcpyAsync(recovery_out[j], dout[j], shard_bytes, hipMemcpyDeviceToHost,
@@ -511,8 +547,8 @@ int bfrs_decode(bfrs_ctx *ctx, size_t k, size_t m, size_t shard_bytes,
     drec[j] = slot;
   }
   uint32_t kk = uint32_t(k);
-  if ((rc = bfrs_decode_batch_dev(ctx, 1, &kk, m, shard_bytes, dorig.data(), drec.data(),
-                                  drest.data(), nullptr)))
+  if ((rc = decode_batch_on(ctx, 1, &kk, m, shard_bytes, dorig.data(), drec.data(),
+                             drest.data(), c.stream)))
     return rc;
   for (size_t i = 0; i < k; ++i)
     if (!originals[i])

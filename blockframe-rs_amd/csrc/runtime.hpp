@@ -79,6 +79,16 @@ struct Context {
 // Argument validation shared by every entry point (crate's Error variants).
 int check_shape(size_t k, size_t m, size_t shard_bytes);
 
+// Batch entry points with an explicit stream (the C-ABI wrappers pass the
+// caller's stream, NULL meaning HIP's default stream; the host-memory API and
+// the streaming objects pass the context's own stream).
+int encode_batch_on(bfrs_ctx *ctx, size_t nblocks, const uint32_t *ks, size_t m,
+                    size_t shard_bytes, const uint8_t *const *d_orig, uint8_t *const *d_rec,
+                    hipStream_t s);
+int decode_batch_on(bfrs_ctx *ctx, size_t nblocks, const uint32_t *ks, size_t m,
+                    size_t shard_bytes, const uint8_t *const *d_orig, const uint8_t *const *d_rec,
+                    uint8_t *const *d_restored, hipStream_t s);
+
 }  // namespace bfrs
 
 struct bfrs_ctx {

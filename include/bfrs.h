@@ -133,7 +133,8 @@ int bfrs_decode(bfrs_ctx *ctx, size_t original_count, size_t recovery_count, siz
  * shard_bytes.  d_originals holds sum(original_counts) pointers, block by
  * block; d_recovery holds nblocks*recovery_count pointers.  Pointer arrays
  * are host arrays of device addresses; shard pointers must be 16-byte
- * aligned.  Work is queued on `hip_stream` (NULL = the context's stream). */
+ * aligned.  Work is queued on `hip_stream` (a hipStream_t; NULL = HIP's
+ * default stream, as in every HIP API) and ordered after earlier work on it. */
 int bfrs_encode_batch_dev(bfrs_ctx *ctx, size_t nblocks, const uint32_t *original_counts,
                           size_t recovery_count, size_t shard_bytes,
                           const uint8_t *const *d_originals, uint8_t *const *d_recovery,

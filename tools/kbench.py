@@ -1,0 +1,101 @@
+"""A/B timing of gf_apply variants in ONE process (interleaved rounds).
+
+usage: python tools/kbench.py [--rounds R] [--iters N] [--variants 1,0,9] [--tpw 1,2,5]
+Variant 9 is a traffic-only probe (no GF arithmetic, wrong output): it gives the
+ceiling of this exact access pattern.  Also times a torch device copy.
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "blockframe-rs_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--variants", default="1,0,9")
+    ap.add_argument("--tpw", default="0")
+    ap.add_argument("--segments", type=int, default=128)
+    ap.add_argument("--decode", action="store_true")
+    a = ap.parse_args()
+    import numpy as np
+    import torch
+    import bfrs
+    from bfrs import synth
+    os.environ["BFRS_ALLOW_PROBE"] = "1"
+    S = synth.SEGMENT_SIZE
+    shapes = synth.block_shapes(a.segments)
+    nb = len(shapes)
+    data = torch.empty(a.segments, S, dtype=torch.uint8, device="cuda")
+    for s in range(a.segments):
+        synth.fill_segment_torch(data[s], 0xB10C, s)
+    par = torch.empty(3 * nb, S, dtype=torch.uint8, device="cuda")
+    rest = torch.empty(3 * nb, S, dtype=torch.uint8, device="cuda")
+    ctx = bfrs.Context(0)
+    stream = torch.cuda.current_stream()
+    enc_in = [data[i] for i in range(a.segments)]
+    enc_out = [par[i] for i in range(3 * nb)]
+    dec_in, dec_out, seg = [], [], 0
+    for b, k in enumerate(shapes):
+        er = [1, k // 2, k - 1]
+        for i in range(k):
+            dec_in.append(None if i in er else data[seg + i])
+            dec_out.append(rest[3 * b + er.index(i)] if i in er else None)
+        seg += k
+    alg = sum(k + 3 for k in shapes) * S
+
+    def run():
+        if a.decode:
+            ctx.decode_batch_dev(shapes, 3, S, dec_in, enc_out, dec_out, stream=stream)
+        else:
+            ctx.encode_batch_dev(shapes, 3, S, enc_in, enc_out, stream=stream)
+
+    os.environ["BFRS_KERNEL_VARIANT"] = "1"
+    os.environ.pop("BFRS_TILES_PER_WG", None)
+    run()
+    torch.cuda.synchronize()
+    ref = par.clone()
+    configs = [(v, t) for v in a.variants.split(",") for t in a.tpw.split(",")]
+    res = {c: [] for c in configs}
+    src = data.view(-1)[: alg // 2]
+    dst = torch.empty_like(src)
+    copy_ms = []
+    for r in range(a.rounds):
+        for (v, t) in configs:
+            os.environ["BFRS_KERNEL_VARIANT"] = v
+            if t == "0":
+                os.environ.pop("BFRS_TILES_PER_WG", None)
+            else:
+                os.environ["BFRS_TILES_PER_WG"] = t
+            run()  # warm
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(a.iters):
+                run()
+            e1.record(stream)
+            torch.cuda.synchronize()
+            res[(v, t)].append(e0.elapsed_time(e1) / a.iters)
+            if v != "9" and not a.decode:
+                assert torch.equal(par, ref), f"variant {v} output differs"
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(a.iters):
+            dst.copy_(src)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        copy_ms.append(e0.elapsed_time(e1) / a.iters)
+    out = {}
+    for (v, t), ms in res.items():
+        m = float(np.median(ms))
+        out[f"v{v}_tpw{t}"] = {"ms": round(m, 4), "GBps": round(alg / m / 1e6, 1), "all_ms": [round(x, 4) for x in ms]}
+    cm = float(np.median(copy_ms))
+    out["torch_copy_same_bytes"] = {"ms": round(cm, 4), "GBps": round(alg / cm / 1e6, 1)}
+    print(json.dumps({"decode": a.decode, "alg_bytes": alg, **out}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
