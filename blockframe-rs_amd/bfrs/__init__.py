@@ -239,6 +239,31 @@ class Context:
                                            _stream_handle(stream, list(d_originals) + list(d_recovery)
                                                           + list(d_restored))))
 
+    def prepare_encode(self, original_counts, recovery_count, shard_bytes, d_originals,
+                       d_recovery):
+        """Pre-built argument arrays for repeated bfrs_encode_batch_dev calls on
+        the same buffers (bench loops); returns f(stream_handle)."""
+        ks = (ctypes.c_uint32 * len(original_counts))(*original_counts)
+        po, ko = _ptr_array([self._addr(t) for t in d_originals])
+        pr, kr = _ptr_array([self._addr(t) for t in d_recovery])
+        fn, h, n = lib().bfrs_encode_batch_dev, self.handle, len(original_counts)
+
+        def call(stream_handle=None, _keep=(ks, ko, kr)):
+            _check(fn(h, n, ks, recovery_count, shard_bytes, po, pr, stream_handle))
+        return call
+
+    def prepare_decode(self, original_counts, recovery_count, shard_bytes, d_originals,
+                       d_recovery, d_restored):
+        ks = (ctypes.c_uint32 * len(original_counts))(*original_counts)
+        po, ko = _ptr_array([self._addr(t) for t in d_originals])
+        pr, kr = _ptr_array([self._addr(t) for t in d_recovery])
+        pd, kd = _ptr_array([self._addr(t) for t in d_restored])
+        fn, h, n = lib().bfrs_decode_batch_dev, self.handle, len(original_counts)
+
+        def call(stream_handle=None, _keep=(ks, ko, kr, kd)):
+            _check(fn(h, n, ks, recovery_count, shard_bytes, po, pr, pd, stream_handle))
+        return call
+
     # ---- one-shot host API (numpy in, numpy out)
     def encode(self, originals, recovery_count=3):
         import numpy as np

@@ -19,19 +19,40 @@ constexpr uint32_t kTileHalfChunks = 256;
 // One pass: out[t] (^)= sum_i coef(t,i) * in[i] for t < n_out, over the
 // 64-byte-chunk symbol layout of reed-solomon-simd.
 struct alignas(16) PassDesc {
-  uint64_t in;               // device address of n_in shard addresses (16-byte aligned)
-  uint64_t out;              // device address of n_out shard addresses
+  uint64_t in;               // index into KernArgs::ptrs of n_in (+1 prefetch) shard addresses
+  uint64_t out;              // index into KernArgs::ptrs of n_out shard addresses
   uint64_t table;            // device address of n_in * 64 packed nibble products (uint2)
   uint32_t n_in, n_out;
   uint32_t wg_begin;         // first workgroup of this pass in the grid
   uint32_t n_tiles;          // tiles in this pass
   uint64_t full_chunks;      // whole 64-byte chunks per shard
   uint32_t tail_bytes;       // shard_bytes % 64 (tail chunk, crate tail layout)
-  uint32_t accumulate;       // 1: XOR into existing outputs
+  uint16_t accumulate;       // 1: XOR into existing outputs
+  uint16_t rotate;           // 1: waves start at different inputs (even, unpadded passes)
 };
 
-hipError_t launch_gf_apply(const PassDesc *d_passes, uint32_t n_passes, uint32_t n_wgs,
-                           uint32_t tiles_per_wg, uint32_t max_in, hipStream_t stream);
-hipError_t launch_gf_tail(const PassDesc *d_passes, uint32_t n_passes, hipStream_t stream);
+// Kernel-argument form: up to kMaxLaunchPasses passes and kMaxLaunchPtrs shard
+// addresses travel in the dispatch packet's kernarg segment (< 4 KiB), so a
+// launch needs no descriptor upload.  PassDesc::in / ::out are then indices
+// into KernArgs::ptrs.
+constexpr uint32_t kMaxLaunchPasses = 16;
+constexpr uint32_t kMaxLaunchPtrs = 376;
+
+struct alignas(16) KernArgs {
+  uint32_t n_passes;
+  uint32_t tiles_per_wg;
+  uint32_t pad[2];
+  PassDesc passes[kMaxLaunchPasses];
+  uint64_t ptrs[kMaxLaunchPtrs];
+};
+static_assert(sizeof(KernArgs) <= 4096, "kernel arguments must fit 4 KiB");
+
+// Column bytes one workgroup tile covers in the selected kernel variant.
+uint32_t tile_bytes();
+int kernel_variant();
+
+hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in,
+                           hipStream_t stream);
+hipError_t launch_gf_tail(const KernArgs &args, hipStream_t stream);
 
 }  // namespace bfrs

@@ -126,6 +126,10 @@ __device__ __forceinline__ void store16(uint64_t a, const uint4 &v) {
   *(AS_GLOBAL u32x4 *)(uintptr_t)a = w;
 }
 
+__device__ __forceinline__ void store16_nt(uint64_t a, const u32x4 &v) {
+  __builtin_nontemporal_store(v, (AS_GLOBAL u32x4 *)(uintptr_t)a);
+}
+
 // Inline-asm streaming loads (see the pipeline comment in gf_apply_kernel).
 // saddr form: 64-bit wave-uniform shard base in SGPRs + 32-bit lane offset.
 __device__ __forceinline__ void gload_half_chunk(u32x4 &L, u32x4 &H, uint64_t base,
@@ -153,17 +157,19 @@ __device__ __forceinline__ void mac_input(const u32x4 &Lv, const u32x4 &Hv, uint
     mac_input_v0(L, H, lds_table + i * 64, acc_lo, acc_hi);
   } else if constexpr (VARIANT == 9) {
     mac_input_stream(L, H, acc_lo, acc_hi);
-  } else {
+  } else {  // 1, 3, 4
     mac_input_v1(L, H, nullptr, 2 * i, 2 * i + 1, acc_lo, acc_hi);
   }
 }
 
+// VARIANT 1: default; 3 / 4: variant 1 compiled for >= 7 / 8 waves per SIMD.
 template <int VARIANT>
-__global__ __launch_bounds__(256) void gf_apply_kernel(const PassDesc *__restrict__ passes_g,
-                                                       uint32_t n_passes, uint32_t tiles_per_wg) {
+__global__ __launch_bounds__(256, VARIANT == 3 ? 7 : (VARIANT == 4 ? 8 : 1)) void gf_apply_kernel(
+    const KernArgs args) {
   extern __shared__ __attribute__((aligned(16))) uint2 lds_table[];
-  // Descriptors and pointer arrays are read-only and wave-uniform: scalar loads.
-  const AS_CONST PassDesc *passes = (const AS_CONST PassDesc *)(uintptr_t)passes_g;
+  // Descriptors live in the kernarg segment: wave-uniform scalar loads.
+  const PassDesc *passes = args.passes;
+  const uint32_t n_passes = args.n_passes, tiles_per_wg = args.tiles_per_wg;
 
   // Locate this workgroup's pass (wave-uniform binary search over wg_begin).
   const uint32_t wg = blockIdx.x;
@@ -175,9 +181,9 @@ __global__ __launch_bounds__(256) void gf_apply_kernel(const PassDesc *__restric
     else
       hi = mid;
   }
-  const AS_CONST PassDesc &P = passes[lo];
+  const PassDesc &P = passes[lo];
   const uint32_t n_in = P.n_in, n_out = P.n_out;
-  const AS_CONST uint64_t *in = (const AS_CONST uint64_t *)(uintptr_t)P.in;
+  const uint64_t *in = args.ptrs + P.in;
 
   // Table -> LDS: all loads issued before any store (n_in <= 64: <= 8 x 16 B per lane).
   {
@@ -211,25 +217,33 @@ __global__ __launch_bounds__(256) void gf_apply_kernel(const PassDesc *__restric
 #pragma unroll
     for (int s = 0; s < 16; ++s) acc_lo[s] = acc_hi[s] = 0;
 
-    // Ping-pong software pipeline: input i+1 loads while input i computes.
-    // The host pads every pass to an even input count (pad inputs have zero
-    // tables) and appends one extra pointer (a duplicate of the last input),
-    // so the loop has no guards.  Loads are inline asm with explicit
-    // vmcnt waits: hipcc otherwise sinks prefetches next to their uses.
+    // Ping-pong software pipeline: input r' loads while input r computes.
+    // Loads are inline asm with explicit vmcnt waits (hipcc otherwise sinks
+    // prefetches next to their uses).  Each wave starts at a different input
+    // (wave-uniform rotation) so concurrently running waves stream from
+    // different shards; past the last input the prefetch re-reads the input
+    // just loaded (a cache hit), so no guard is needed.  Passes with a
+    // zero-table pad input (odd counts) keep rotation 0 so the pad's
+    // duplicate pointer stays adjacent to its original.
     const uint32_t voff = uint32_t(off);
+    const uint32_t wave_id = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint32_t r = P.rotate ? (tile * 4 + wave_id) % n_in : 0;
     u32x4 La, Ha, Lb, Hb;
-    gload_half_chunk(La, Ha, in[0], voff);
+    gload_half_chunk(La, Ha, in[r], voff);
     for (uint32_t i = 0; i < n_in; i += 2) {
-      gload_half_chunk(Lb, Hb, in[i + 1], voff);
+      const uint32_t r1 = r + 1 == n_in ? 0 : r + 1;
+      gload_half_chunk(Lb, Hb, in[r1], voff);
       vm_wait<2>(La, Ha);
-      mac_input<VARIANT>(La, Ha, i, acc_lo, acc_hi);
-      gload_half_chunk(La, Ha, in[i + 2], voff);
+      mac_input<VARIANT>(La, Ha, r, acc_lo, acc_hi);
+      const uint32_t r2 = i + 2 < n_in ? (r1 + 1 == n_in ? 0 : r1 + 1) : r1;
+      gload_half_chunk(La, Ha, in[r2], voff);
       vm_wait<2>(Lb, Hb);
-      mac_input<VARIANT>(Lb, Hb, i + 1, acc_lo, acc_hi);
+      mac_input<VARIANT>(Lb, Hb, r1, acc_lo, acc_hi);
+      r = r2;
     }
     vm_wait<0>(La, Ha);  // drain the final (unused) prefetch
 
-    const AS_CONST uint64_t *outp = (const AS_CONST uint64_t *)(uintptr_t)P.out;
+    const uint64_t *outp = args.ptrs + P.out;
     const bool accumulate = P.accumulate != 0;
     for (uint32_t t = 0; t < n_out; ++t) {
       uint4 ol = make_uint4(gather_byte(acc_lo, 0, t), gather_byte(acc_lo, 1, t),
@@ -242,8 +256,157 @@ __global__ __launch_bounds__(256) void gf_apply_kernel(const PassDesc *__restric
         ol.x ^= pl.x; ol.y ^= pl.y; ol.z ^= pl.z; ol.w ^= pl.w;
         oh.x ^= ph.x; oh.y ^= ph.y; oh.z ^= ph.z; oh.w ^= ph.w;
       }
-      store16(dst, ol);
-      store16(dst + 32, oh);
+      store16_nt(dst, u32x4{ol.x, ol.y, ol.z, ol.w});
+      store16_nt(dst + 32, u32x4{oh.x, oh.y, oh.z, oh.w});
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Variant 2 (default): contiguous streaming.
+//
+// A wave covers 1 KiB of columns per input with ONE global_load_dwordx4:
+// lane l holds bytes [16l, 16l+16), i.e. part p = l&3 of chunk l>>2 — the low
+// bytes (p = 0,1) or the high bytes (p = 2,3) of 16 symbols.  Each lane looks
+// up only the two nibble tables of the byte it holds and keeps partial sums
+// for its 16 symbols; lanes l and l^2 hold the two halves of the same symbols,
+// so one DPP quad swap + XOR per accumulator at the end of the tile combines
+// them (XOR is the field addition).  Loads are `nt` (read once), with three
+// inputs in flight (4-buffer ring, loop unrolled by 4, no register moves);
+// stores are non-temporal, 1 KiB contiguous per wave instruction.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kV2TileBytes = 4096;  // 256 lanes x 16 B
+
+__device__ __forceinline__ void gload16_nt(u32x4 &v, uint64_t base, uint32_t voff) {
+  asm volatile("global_load_dwordx4 %0, %1, %2 nt" : "=&v"(v) : "v"(voff), "s"(base) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void vm_wait1(u32x4 &v) {
+  asm volatile("s_waitcnt vmcnt(%1)" : "+v"(v) : "n"(N) : "memory");
+}
+
+// 16 half-symbols of one input: 2 lookups each (the byte's two nibbles).
+// base = 2*input + (lane holds high bytes).
+__device__ __forceinline__ void mac_half(const u32x4 &X, uint32_t base, uint32_t (&acc_lo)[16],
+                                         uint32_t (&acc_hi)[16]) {
+  const uint32_t x[4] = {X.x, X.y, X.z, X.w};
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const uint32_t nl = (x[d] << 3) & 0x78787878u;
+    const uint32_t nh = ((x[d] >> 1) & 0x78787878u) | 0x80808080u;
+    uint2 e[4][2];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const uint32_t sel = 0x0C050400u | uint32_t(b);
+      e[b][0] = lds_entry(nullptr, __builtin_amdgcn_perm(base, nl, sel));
+      e[b][1] = lds_entry(nullptr, __builtin_amdgcn_perm(base, nh, sel));
+    }
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int s = d * 4 + b;
+      acc_lo[s] = xor3(acc_lo[s], e[b][0].x, e[b][1].x);
+      acc_hi[s] = xor3(acc_hi[s], e[b][0].y, e[b][1].y);
+    }
+  }
+}
+
+// Swap with lane ^2 inside each quad (quad_perm [2,3,0,1]) and XOR.
+__device__ __forceinline__ uint32_t quad_xor2(uint32_t v) {
+  return v ^ uint32_t(__builtin_amdgcn_mov_dpp(int(v), 0x4E, 0xF, 0xF, true));
+}
+
+
+__global__ __launch_bounds__(256) void gf_apply_v2_kernel(const KernArgs args) {
+  extern __shared__ __attribute__((aligned(16))) uint2 lds_table[];
+  const PassDesc *passes = args.passes;
+  const uint32_t n_passes = args.n_passes, tiles_per_wg = args.tiles_per_wg;
+
+  const uint32_t wg = blockIdx.x;
+  uint32_t lo = 0, hi = n_passes;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (passes[mid].wg_begin <= wg)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  const PassDesc &P = passes[lo];
+  const uint32_t n_in = P.n_in, n_out = P.n_out;
+  const uint64_t *in = args.ptrs + P.in;
+
+  {  // table -> LDS (all loads before stores)
+    const AS_GLOBAL u32x4 *tab = (const AS_GLOBAL u32x4 *)(uintptr_t)P.table;
+    u32x4 *dst = reinterpret_cast<u32x4 *>(lds_table);
+    const uint32_t n16 = n_in * 32;
+    u32x4 v[kMaxPassInputs * 32 / 256];
+#pragma unroll
+    for (int r = 0; r < int(kMaxPassInputs * 32 / 256); ++r) {
+      const uint32_t e = threadIdx.x + 256u * r;
+      v[r] = e < n16 ? tab[e] : u32x4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int r = 0; r < int(kMaxPassInputs * 32 / 256); ++r) {
+      const uint32_t e = threadIdx.x + 256u * r;
+      if (e < n16) dst[e] = v[r];
+    }
+  }
+  __syncthreads();
+
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t is_hi = (lane >> 1) & 1;
+  const uint64_t full_bytes = P.full_chunks * 64;
+  const uint32_t t_begin = (wg - P.wg_begin) * tiles_per_wg;
+  const uint32_t t_end = min(t_begin + tiles_per_wg, P.n_tiles);
+
+  for (uint32_t tile = t_begin; tile < t_end; ++tile) {
+    const uint64_t off = uint64_t(tile) * kV2TileBytes + threadIdx.x * 16u;
+    if (off >= full_bytes) break;
+    const uint32_t voff = uint32_t(off);
+
+    uint32_t acc_lo[16], acc_hi[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) acc_lo[s] = acc_hi[s] = 0;
+
+    // Ring of 4 buffers, 3 inputs in flight.  n_in is even; the host pads
+    // the pointer list with 3 duplicates so every load is unconditional.
+    u32x4 A, B, C, D;
+    gload16_nt(A, in[0], voff);
+    gload16_nt(B, in[1], voff);
+    gload16_nt(C, in[2], voff);
+    for (uint32_t i = 0;; i += 4) {
+      gload16_nt(D, in[i + 3], voff);
+      vm_wait1<3>(A);
+      mac_half(A, 2 * i + is_hi, acc_lo, acc_hi);
+      gload16_nt(A, in[i + 4], voff);
+      vm_wait1<3>(B);
+      mac_half(B, 2 * (i + 1) + is_hi, acc_lo, acc_hi);
+      if (i + 2 >= n_in) break;
+      gload16_nt(B, in[i + 5], voff);
+      vm_wait1<3>(C);
+      mac_half(C, 2 * (i + 2) + is_hi, acc_lo, acc_hi);
+      gload16_nt(C, in[i + 6], voff);
+      vm_wait1<3>(D);
+      mac_half(D, 2 * (i + 3) + is_hi, acc_lo, acc_hi);
+      if (i + 4 >= n_in) break;
+    }
+    vm_wait1<0>(A);  // drain the prefetches past the end
+
+    // Combine the two halves of every symbol (lanes l, l^2), then each lane
+    // keeps the output bytes of the part it owns: low bytes for p = 0,1.
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const uint32_t lo_v = quad_xor2(acc_lo[s]);
+      const uint32_t hi_v = quad_xor2(acc_hi[s]);
+      acc_lo[s] = is_hi ? hi_v : lo_v;
+    }
+    const uint64_t *outp = args.ptrs + P.out;
+    const bool accumulate = P.accumulate != 0;
+    for (uint32_t t = 0; t < n_out; ++t) {
+      u32x4 o = {gather_byte(acc_lo, 0, t), gather_byte(acc_lo, 1, t), gather_byte(acc_lo, 2, t),
+                 gather_byte(acc_lo, 3, t)};
+      const uint64_t dst = outp[t] + off;
+      if (accumulate) o ^= *(const AS_GLOBAL u32x4 *)(uintptr_t)dst;
+      store16_nt(dst, o);
     }
   }
 }
@@ -251,15 +414,15 @@ __global__ __launch_bounds__(256) void gf_apply_kernel(const PassDesc *__restric
 // Tail chunk (shard_bytes % 64 = tb != 0): tb/2 symbols, low bytes at
 // [base, base+tb/2), high bytes at [base+tb/2, base+tb) — the crate's tail rule.
 // One workgroup per pass, one lane per symbol; rare and tiny.
-__global__ __launch_bounds__(64) void gf_tail_kernel(const PassDesc *__restrict__ passes) {
-  const PassDesc &P = passes[blockIdx.x];
+__global__ __launch_bounds__(64) void gf_tail_kernel(const KernArgs args) {
+  const PassDesc &P = args.passes[blockIdx.x];
   const uint32_t half = P.tail_bytes / 2;
   const uint32_t s = threadIdx.x;
   if (P.tail_bytes == 0 || s >= half) return;
   const uint64_t base = P.full_chunks * 64;
   uint32_t acc_lo = 0, acc_hi = 0;
-  const uint64_t *in = (const uint64_t *)(uintptr_t)P.in;
-  const uint64_t *outp = (const uint64_t *)(uintptr_t)P.out;
+  const uint64_t *in = args.ptrs + P.in;
+  const uint64_t *outp = args.ptrs + P.out;
   for (uint32_t i = 0; i < P.n_in; ++i) {
     const uint8_t *src = (const uint8_t *)(uintptr_t)in[i];
     const uint32_t lb = src[base + s], hb = src[base + half + s];
@@ -292,29 +455,37 @@ int kernel_variant() {
   return v;
 }
 
-hipError_t launch_gf_apply(const PassDesc *d_passes, uint32_t n_passes, uint32_t n_wgs,
-                           uint32_t tiles_per_wg, uint32_t max_in, hipStream_t stream) {
+uint32_t tile_bytes() { return kernel_variant() == 2 ? kV2TileBytes : kTileHalfChunks * 32; }
+
+hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in,
+                           hipStream_t stream) {
   if (n_wgs == 0) return hipSuccess;
   const size_t lds = size_t(max_in) * 64 * sizeof(uint2);
   switch (kernel_variant()) {
     case 0:
-      hipLaunchKernelGGL(gf_apply_kernel<0>, dim3(n_wgs), dim3(256), lds, stream, d_passes,
-                         n_passes, tiles_per_wg);
+      hipLaunchKernelGGL(gf_apply_kernel<0>, dim3(n_wgs), dim3(256), lds, stream, args);
       break;
     case 9:
-      hipLaunchKernelGGL(gf_apply_kernel<9>, dim3(n_wgs), dim3(256), lds, stream, d_passes,
-                         n_passes, tiles_per_wg);
+      hipLaunchKernelGGL(gf_apply_kernel<9>, dim3(n_wgs), dim3(256), lds, stream, args);
+      break;
+    case 1:
+      hipLaunchKernelGGL(gf_apply_kernel<1>, dim3(n_wgs), dim3(256), lds, stream, args);
+      break;
+    case 3:
+      hipLaunchKernelGGL(gf_apply_kernel<3>, dim3(n_wgs), dim3(256), lds, stream, args);
+      break;
+    case 4:
+      hipLaunchKernelGGL(gf_apply_kernel<4>, dim3(n_wgs), dim3(256), lds, stream, args);
       break;
     default:
-      hipLaunchKernelGGL(gf_apply_kernel<1>, dim3(n_wgs), dim3(256), lds, stream, d_passes,
-                         n_passes, tiles_per_wg);
+      hipLaunchKernelGGL(gf_apply_v2_kernel, dim3(n_wgs), dim3(256), lds, stream, args);
   }
   return hipGetLastError();
 }
 
-hipError_t launch_gf_tail(const PassDesc *d_passes, uint32_t n_passes, hipStream_t stream) {
-  if (n_passes == 0) return hipSuccess;
-  hipLaunchKernelGGL(gf_tail_kernel, dim3(n_passes), dim3(64), 0, stream, d_passes);
+hipError_t launch_gf_tail(const KernArgs &args, hipStream_t stream) {
+  if (args.n_passes == 0) return hipSuccess;
+  hipLaunchKernelGGL(gf_tail_kernel, dim3(args.n_passes), dim3(64), 0, stream, args);
   return hipGetLastError();
 }
 

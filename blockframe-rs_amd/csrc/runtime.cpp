@@ -99,11 +99,6 @@ static int upload_plan(Plan *p) {
 Context::~Context() {
   if (device >= 0) (void)hipSetDevice(device);
   if (stream) (void)hipStreamSynchronize(stream);
-  for (auto &s : slots) {
-    if (s.host) (void)hipHostFree(s.host);
-    if (s.dev) (void)hipFree(s.dev);
-    if (s.done) (void)hipEventDestroy(s.done);
-  }
   plans.clear();
   if (d_scratch) (void)hipFree(d_scratch);
   if (stream) (void)hipStreamDestroy(stream);
@@ -117,8 +112,6 @@ int Context::init(int dev) {
   device = dev;
   HIP_TRY(hipSetDevice(dev));
   HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
-  slots.resize(8);
-  for (auto &s : slots) HIP_TRY(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
   return BFRS_OK;
 }
 
@@ -177,92 +170,75 @@ int Context::run_blocks(const std::vector<BlockIO> &blocks, size_t shard_bytes,
                         hipStream_t s) {
   const uint64_t full_chunks = shard_bytes / 64;
   const uint32_t tail = uint32_t(shard_bytes % 64);
-  const uint32_t n_tiles = uint32_t((full_chunks * 2 + kTileHalfChunks - 1) / kTileHalfChunks);
+  const uint32_t tb = tile_bytes();
+  const uint32_t n_tiles = uint32_t((full_chunks * 64 + tb - 1) / tb);
   uint32_t max_phase = 0;
   for (const BlockIO &b : blocks) max_phase = std::max(max_phase, b.plan->n_phases);
 
+  struct Item {
+    const BlockIO *b;
+    const PlanPass *p;
+  };
+  // Pointer slots a pass needs: inputs padded to even, +3 prefetch slots
+  // (the kernels read up to 3 inputs past the end; duplicates of the last
+  // input, served from cache, never consumed), outputs.
+  constexpr uint32_t kPrefetchPad = 3;
+  auto ptr_need = [](const PlanPass &p) {
+    return ((p.c1 - p.c0 + 1) & ~1u) + kPrefetchPad + (p.r1 - p.r0);
+  };
+
   for (uint32_t phase = 0; phase < max_phase; ++phase) {
-    // Gather this phase's passes.
-    struct Item {
-      const BlockIO *b;
-      const PlanPass *p;
-    };
     std::vector<Item> items;
-    uint32_t max_in = 0;
     for (const BlockIO &b : blocks)
       for (const PlanPass &p : b.plan->passes)
-        if (p.phase == phase) {
-          items.push_back({&b, &p});
-          max_in = std::max(max_in, (p.c1 - p.c0 + 1) & ~1u);
-        }
-    if (items.empty()) continue;
+        if (p.phase == phase) items.push_back({&b, &p});
 
-    // Workgroup sizing: ~4096 workgroups in flight-order, >= 1 tile each.
-    const uint64_t total_tiles = uint64_t(n_tiles) * items.size();
-    uint32_t tpw = uint32_t(std::max<uint64_t>(1, total_tiles / 4096));
-    if (const char *e = std::getenv("BFRS_TILES_PER_WG")) tpw = std::max(1, atoi(e));
-    const uint32_t wgs_per_pass = (n_tiles + tpw - 1) / tpw;
+    // Launches of up to kMaxLaunchPasses passes / kMaxLaunchPtrs pointers.
+    for (size_t first = 0; first < items.size();) {
+      size_t last = first, nptr = 0;
+      while (last < items.size() && last - first < kMaxLaunchPasses &&
+             nptr + ptr_need(*items[last].p) <= kMaxLaunchPtrs)
+        nptr += ptr_need(*items[last++].p);
+      if (last == first)
+        return set_error(BFRS_E_INVALID_ARGUMENT, "pass exceeds one launch's pointer capacity");
 
-    // Staging layout: [PassDesc x n][pointer arrays].
-    size_t n_ptrs = 0;
-    // per pass: inputs padded to even + 1 prefetch pointer, then outputs
-    for (const Item &it : items)
-      n_ptrs += ((it.p->c1 - it.p->c0 + 1) & ~1u) + 1 + (it.p->r1 - it.p->r0);
-    const size_t desc_bytes = round_up(items.size() * sizeof(PassDesc), 16);
-    const size_t bytes = desc_bytes + n_ptrs * sizeof(void *);
+      // Workgroup sizing: one 8 KiB tile per workgroup unless the grid is huge.
+      const uint64_t total_tiles = uint64_t(n_tiles) * (last - first);
+      uint32_t tpw = uint32_t(std::max<uint64_t>(1, total_tiles / 65536));
+      if (const char *e = std::getenv("BFRS_TILES_PER_WG")) tpw = std::max(1, atoi(e));
+      const uint32_t wgs_per_pass = (n_tiles + tpw - 1) / tpw;
 
-    Slot &slot = slots[next_slot];
-    next_slot = (next_slot + 1) % slots.size();
-    if (slot.used) HIP_TRY(hipEventSynchronize(slot.done));
-    if (bytes > slot.cap) {
-      if (slot.host) HIP_TRY(hipHostFree(slot.host));
-      if (slot.dev) HIP_TRY(hipFree(slot.dev));
-      const size_t cap = std::max<size_t>(round_up(bytes, 4096), 64 * 1024);
-      HIP_TRY(hipHostMalloc(&slot.host, cap, hipHostMallocDefault));
-      HIP_TRY(hipMalloc(&slot.dev, cap));
-      slot.cap = cap;
+      KernArgs ka{};
+      ka.n_passes = uint32_t(last - first);
+      ka.tiles_per_wg = tpw;
+      uint32_t pi = 0, wg = 0, max_in = 0;
+      for (size_t it = first; it < last; ++it) {
+        const BlockIO &b = *items[it].b;
+        const PlanPass &p = *items[it].p;
+        PassDesc &d = ka.passes[it - first];
+        const uint32_t n_real = p.c1 - p.c0, n_pad = (n_real + 1) & ~1u;
+        d.in = pi;
+        for (uint32_t c = p.c0; c < p.c1; ++c) ka.ptrs[pi++] = reinterpret_cast<uint64_t>(b.in[c]);
+        const uint64_t lastp = reinterpret_cast<uint64_t>(b.in[p.c1 - 1]);
+        for (uint32_t c = n_real; c < n_pad + kPrefetchPad; ++c) ka.ptrs[pi++] = lastp;
+        d.out = pi;
+        for (uint32_t r = p.r0; r < p.r1; ++r) ka.ptrs[pi++] = reinterpret_cast<uint64_t>(b.out[r]);
+        d.table = reinterpret_cast<uint64_t>(p.d_table);
+        d.n_in = n_pad;
+        d.n_out = p.r1 - p.r0;
+        d.wg_begin = wg;
+        d.n_tiles = n_tiles;
+        d.full_chunks = full_chunks;
+        d.tail_bytes = tail;
+        d.accumulate = phase > 0;
+        d.rotate = n_real == n_pad;
+        wg += wgs_per_pass;
+        max_in = std::max(max_in, n_pad);
+      }
+      if (n_tiles) HIP_TRY(launch_gf_apply(ka, wg, max_in, s));
+      if (tail) HIP_TRY(launch_gf_tail(ka, s));
+      first = last;
     }
-    auto *desc = static_cast<PassDesc *>(slot.host);
-    auto *ptrs = reinterpret_cast<uint64_t *>(static_cast<char *>(slot.host) + desc_bytes);
-    const uint64_t dev_ptrs = reinterpret_cast<uint64_t>(slot.dev) + desc_bytes;
-    size_t pi = 0;
-    uint32_t wg = 0;
-    for (size_t i = 0; i < items.size(); ++i) {
-      const BlockIO &b = *items[i].b;
-      const PlanPass &p = *items[i].p;
-      PassDesc d{};
-      d.in = dev_ptrs + pi * 8;
-      const uint32_t n_real = p.c1 - p.c0, n_pad = (n_real + 1) & ~1u;
-      for (uint32_t c = p.c0; c < p.c1; ++c) ptrs[pi++] = reinterpret_cast<uint64_t>(b.in[c]);
-      const uint64_t last = reinterpret_cast<uint64_t>(b.in[p.c1 - 1]);
-      for (uint32_t c = n_real; c < n_pad + 1; ++c) ptrs[pi++] = last;
-      d.out = dev_ptrs + pi * 8;
-      for (uint32_t r = p.r0; r < p.r1; ++r) ptrs[pi++] = reinterpret_cast<uint64_t>(b.out[r]);
-      d.table = reinterpret_cast<uint64_t>(p.d_table);
-      d.n_in = n_pad;
-      d.n_out = p.r1 - p.r0;
-      d.wg_begin = wg;
-      d.n_tiles = n_tiles;
-      d.full_chunks = full_chunks;
-      d.tail_bytes = tail;
-      d.accumulate = phase > 0;
-      desc[i] = d;
-      wg += wgs_per_pass;
-    }
-    HIP_TRY(hipMemcpyAsync(slot.dev, slot.host, bytes, hipMemcpyHostToDevice, s));
-    if (std::getenv("BFRS_DEBUG_DESC")) {  // diagnostics: verify the upload landed
-      HIP_TRY(hipStreamSynchronize(s));
-      std::vector<char> back(bytes);
-      HIP_TRY(hipMemcpy(back.data(), slot.dev, bytes, hipMemcpyDeviceToHost));
-      if (std::memcmp(back.data(), slot.host, bytes) != 0)
-        fprintf(stderr, "bfrs: descriptor upload mismatch (slot %zu)\n",
-                size_t(&slot - slots.data()));
-    }
-    const auto *d_desc = static_cast<const PassDesc *>(slot.dev);
-    if (wg) HIP_TRY(launch_gf_apply(d_desc, uint32_t(items.size()), wg, tpw, max_in, s));
-    if (tail) HIP_TRY(launch_gf_tail(d_desc, uint32_t(items.size()), s));
-    HIP_TRY(hipEventRecord(slot.done, s));
-    slot.used = true;
   }
   return BFRS_OK;
 }

@@ -51,17 +51,6 @@ struct Context {
   std::mutex mu;  // guards the plan cache (contexts are single-threaded otherwise)
   std::map<std::string, std::unique_ptr<Plan>> plans;
 
-  // Descriptor staging ring: pinned host slots + device slots + events.
-  struct Slot {
-    void *host = nullptr;
-    void *dev = nullptr;
-    size_t cap = 0;
-    hipEvent_t done = nullptr;
-    bool used = false;
-  };
-  std::vector<Slot> slots;
-  size_t next_slot = 0;
-
   // Scratch device memory for the host-memory API.
   void *d_scratch = nullptr;
   size_t scratch_cap = 0;

@@ -1,0 +1,315 @@
+// membench.hip — memory-pattern probes for the RS(30,3) pass (measurement
+// tool, not product code).  Every probe reads K input shards and writes 3
+// output shards of S bytes per block, B blocks, like gf_apply_kernel, but
+// with no GF arithmetic, to find the access pattern that streams fastest.
+//
+// build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/membench.hip -o tools/membench
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CHECK(x)                                                                   \
+  do {                                                                             \
+    hipError_t e = (x);                                                            \
+    if (e != hipSuccess) {                                                         \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e));     \
+      exit(1);                                                                     \
+    }                                                                              \
+  } while (0)
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+struct Args {
+  const uint8_t *const *in;  // B*K pointers
+  uint8_t *const *out;       // B*3 pointers
+  uint32_t K, B;
+  uint64_t S;
+};
+
+__device__ __forceinline__ uint64_t uni(const uint8_t *p) {
+  const uint64_t x = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(x));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(uint32_t(x >> 32));
+  return (uint64_t(hi) << 32) | lo;
+}
+
+template <int NT>
+__device__ __forceinline__ void ld(u32x4 &v, uint64_t base, uint32_t off) {
+  if constexpr (NT == 1)
+    asm volatile("global_load_dwordx4 %0, %1, %2 nt" : "=&v"(v) : "v"(off), "s"(base) : "memory");
+  else if constexpr (NT == 2)
+    asm volatile("global_load_dwordx4 %0, %1, %2 sc1" : "=&v"(v) : "v"(off), "s"(base) : "memory");
+  else
+    asm volatile("global_load_dwordx4 %0, %1, %2" : "=&v"(v) : "v"(off), "s"(base) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void wt(u32x4 &a) {
+  asm volatile("s_waitcnt vmcnt(%1)" : "+v"(a) : "n"(N) : "memory");
+}
+
+// PAT 0: half-line (lane = 32-byte half-chunk: +0 and +32), the current kernel.
+// PAT 1: contiguous: lane l loads bytes [16l,16l+16) of two consecutive KiB.
+// DEPTH: inputs in flight beyond the one being consumed (1 or 2).
+template <int PAT, int NT, int DEPTH, int STORE_NT>
+__global__ __launch_bounds__(256) void probe(Args a, uint32_t tiles_per_block) {
+  const uint32_t b = blockIdx.x / tiles_per_block;
+  const uint32_t tile = blockIdx.x % tiles_per_block;
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // each wave covers 2 KiB of columns
+  const uint64_t col = (uint64_t(tile) * 4 + wave) * 2048;
+  uint32_t o0, o1;
+  if (PAT == 0) {
+    const uint32_t hc = lane;  // half-chunk within 2 KiB
+    o0 = uint32_t(col + (hc >> 1) * 64 + (hc & 1) * 16);
+    o1 = o0 + 32;
+  } else {
+    o0 = uint32_t(col + lane * 16);
+    o1 = o0 + 1024;
+  }
+  const __attribute__((address_space(4))) uint64_t *in =
+      (const __attribute__((address_space(4))) uint64_t *)(uintptr_t)(a.in + size_t(b) * a.K);
+  u32x4 acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
+  u32x4 x0[3], x1[3];
+  // prologue
+  ld<NT>(x0[0], in[0], o0);
+  ld<NT>(x1[0], in[0], o1);
+  if (DEPTH >= 2) {
+    ld<NT>(x0[1], in[1], o0);
+    ld<NT>(x1[1], in[1], o1);
+  }
+  for (uint32_t i = 0; i < a.K; ++i) {
+    const uint32_t nxt = min(i + DEPTH, a.K - 1);
+    u32x4 n0, n1;
+    ld<NT>(n0, in[nxt], o0);
+    ld<NT>(n1, in[nxt], o1);
+    const int cur = DEPTH == 1 ? 0 : int(i % 2);
+    u32x4 c0 = x0[cur], c1 = x1[cur];
+    if (DEPTH == 1) {
+      wt<2>(c0);
+      wt<2>(c1);
+    } else {
+      wt<4>(c0);
+      wt<4>(c1);
+    }
+    acc0 ^= c0;
+    acc1 ^= c1;
+    if (DEPTH == 1) {
+      x0[0] = n0;
+      x1[0] = n1;
+    } else {
+      x0[cur] = n0;
+      x1[cur] = n1;
+    }
+  }
+  u32x4 d0 = x0[0], d1 = x1[0];
+  wt<0>(d0);
+  wt<0>(d1);
+  acc0 ^= d0 & u32x4{0, 0, 0, 0};
+  for (int j = 0; j < 3; ++j) {
+    uint8_t *dst = a.out[b * 3 + j];
+    u32x4 v0 = acc0 + u32x4{uint32_t(j), 0, 0, 0}, v1 = acc1;
+    if (STORE_NT) {
+      __builtin_nontemporal_store(v0, (u32x4 *)(dst + o0));
+      __builtin_nontemporal_store(v1, (u32x4 *)(dst + o1));
+    } else {
+      *(u32x4 *)(dst + o0) = v0;
+      *(u32x4 *)(dst + o1) = v1;
+    }
+  }
+}
+
+
+// probe2: v1 pattern (half-chunk per lane) with W half-chunks per lane per input
+// (wave column span = W*2 KiB), optional per-wave input rotation, optional writes.
+template <int W, int ROT, int WRITE>
+__global__ __launch_bounds__(256) void probe2(Args a, uint32_t tiles_per_block) {
+  const uint32_t b = blockIdx.x / tiles_per_block;
+  const uint32_t tile = blockIdx.x % tiles_per_block;
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t col = (uint64_t(tile) * 4 + wave) * 2048 * W;
+  const __attribute__((address_space(4))) uint64_t *in =
+      (const __attribute__((address_space(4))) uint64_t *)(uintptr_t)(a.in + size_t(b) * a.K);
+  uint32_t o[W];
+#pragma unroll
+  for (int w = 0; w < W; ++w) o[w] = uint32_t(col + w * 2048 + (lane >> 1) * 64 + (lane & 1) * 16);
+  const uint32_t rot = ROT ? __builtin_amdgcn_readfirstlane((blockIdx.x * 4 + wave) % a.K) : 0;
+  u32x4 acc = {0, 0, 0, 0};
+  u32x4 cur[2 * W], nxt[2 * W];
+  uint32_t idx = rot;
+#pragma unroll
+  for (int w = 0; w < W; ++w) { ld<0>(cur[2 * w], in[idx], o[w]); ld<0>(cur[2 * w + 1], in[idx], o[w] + 32); }
+  for (uint32_t i = 0; i < a.K; ++i) {
+    uint32_t n = idx + 1 == a.K ? 0 : idx + 1;
+#pragma unroll
+    for (int w = 0; w < W; ++w) { ld<0>(nxt[2 * w], in[n], o[w]); ld<0>(nxt[2 * w + 1], in[n], o[w] + 32); }
+#pragma unroll
+    for (int w = 0; w < 2 * W; ++w) { wt<2 * W>(cur[w]); acc ^= cur[w]; }
+#pragma unroll
+    for (int w = 0; w < 2 * W; ++w) cur[w] = nxt[w];
+    idx = n;
+  }
+#pragma unroll
+  for (int w = 0; w < 2 * W; ++w) { wt<0>(cur[w]); acc ^= cur[w] & u32x4{0,0,0,0}; }
+  if (WRITE) {
+    for (int j = 0; j < 3; ++j) {
+      uint8_t *dst = a.out[b * 3 + j];
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        *(u32x4 *)(dst + o[w]) = acc + u32x4{uint32_t(j), 0, 0, 0};
+        *(u32x4 *)(dst + o[w] + 32) = acc;
+      }
+    }
+  } else if (acc.x == 0x9e3779b9u) {
+    *(u32x4 *)(a.out[0]) = acc;
+  }
+}
+
+
+// probe3: v1 loads (half-chunk per lane) with rotation R; store shape SS:
+// 0 = half-chunk (lo,hi separate 16 B at +0/+32), 1 = contiguous 1 KiB per
+// instruction (lane l writes [16l,16l+16) of the wave's 2 KiB: two stores);
+// SNT = non-temporal stores.
+template <int R, int SS, int SNT>
+__global__ __launch_bounds__(256) void probe3(Args a, uint32_t tiles_per_block) {
+  const uint32_t b = blockIdx.x / tiles_per_block;
+  const uint32_t tile = blockIdx.x % tiles_per_block;
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t col = (uint64_t(tile) * 4 + wave) * 2048;
+  const __attribute__((address_space(4))) uint64_t *in =
+      (const __attribute__((address_space(4))) uint64_t *)(uintptr_t)(a.in + size_t(b) * a.K);
+  const uint32_t o = uint32_t(col + (lane >> 1) * 64 + (lane & 1) * 16);
+  const uint32_t rot = R ? __builtin_amdgcn_readfirstlane((blockIdx.x * 4 + wave) % a.K) : 0;
+  u32x4 acc = {0, 0, 0, 0}, c0, c1, n0, n1;
+  uint32_t idx = rot;
+  ld<0>(c0, in[idx], o); ld<0>(c1, in[idx], o + 32);
+  for (uint32_t i = 0; i < a.K; ++i) {
+    uint32_t n = idx + 1 == a.K ? 0 : idx + 1;
+    ld<0>(n0, in[n], o); ld<0>(n1, in[n], o + 32);
+    wt<2>(c0); wt<2>(c1);
+    acc ^= c0 ^ c1;
+    c0 = n0; c1 = n1; idx = n;
+  }
+  wt<0>(c0); wt<0>(c1);
+  for (int j = 0; j < 3; ++j) {
+    uint8_t *dst = a.out[b * 3 + j];
+    const u32x4 v = acc + u32x4{uint32_t(j), 0, 0, 0};
+    uint32_t s0, s1;
+    if (SS == 0) { s0 = o; s1 = o + 32; }
+    else { s0 = uint32_t(col + lane * 16); s1 = s0 + 1024; }
+    if (SNT) {
+      __builtin_nontemporal_store(v, (u32x4 *)(dst + s0));
+      __builtin_nontemporal_store(v, (u32x4 *)(dst + s1));
+    } else {
+      *(u32x4 *)(dst + s0) = v;
+      *(u32x4 *)(dst + s1) = v;
+    }
+  }
+}
+
+__global__ void copy_kernel(const u32x4 *__restrict__ s, u32x4 *__restrict__ d, size_t n) {
+  size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  const size_t stride = size_t(gridDim.x) * blockDim.x;
+  for (; i < n; i += stride) d[i] = s[i];
+}
+
+__global__ void read_kernel(const u32x4 *__restrict__ s, u32x4 *__restrict__ d, size_t n) {
+  size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  const size_t stride = size_t(gridDim.x) * blockDim.x;
+  u32x4 acc = {0, 0, 0, 0};
+  for (; i < n; i += stride) acc ^= s[i];
+  if (acc.x == 0x12345678u) d[0] = acc;
+}
+
+int main(int argc, char **argv) {
+  const uint32_t K = 30, B = 4;
+  const uint64_t S = 32ull << 20;
+  uint8_t *data, *par;
+  CHECK(hipMalloc(&data, S * K * B));
+  CHECK(hipMalloc(&par, S * 3 * B));
+  CHECK(hipMemset(data, 0x5a, S * K * B));
+  std::vector<const uint8_t *> hin(K * B);
+  std::vector<uint8_t *> hout(3 * B);
+  for (uint32_t i = 0; i < K * B; ++i) hin[i] = data + S * i;
+  for (uint32_t i = 0; i < 3 * B; ++i) hout[i] = par + S * i;
+  const uint8_t **din;
+  uint8_t **dout;
+  CHECK(hipMalloc(&din, sizeof(void *) * K * B));
+  CHECK(hipMalloc(&dout, sizeof(void *) * 3 * B));
+  CHECK(hipMemcpy(din, hin.data(), sizeof(void *) * K * B, hipMemcpyHostToDevice));
+  CHECK(hipMemcpy(dout, hout.data(), sizeof(void *) * 3 * B, hipMemcpyHostToDevice));
+  Args a{din, dout, K, B, S};
+  const uint32_t tiles = uint32_t(S / 8192);
+  const double bytes = double(S) * (K + 3) * B;
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  const int iters = 10;
+
+  auto time = [&](const char *name, auto launch, double nbytes) {
+    launch();
+    CHECK(hipDeviceSynchronize());
+    float best = 1e9, sum = 0;
+    for (int r = 0; r < 3; ++r) {
+      CHECK(hipEventRecord(e0));
+      for (int i = 0; i < iters; ++i) launch();
+      CHECK(hipEventRecord(e1));
+      CHECK(hipEventSynchronize(e1));
+      float ms;
+      CHECK(hipEventElapsedTime(&ms, e0, e1));
+      ms /= iters;
+      best = ms < best ? ms : best;
+      sum += ms;
+    }
+    printf("{\"probe\": \"%s\", \"ms\": %.4f, \"GBps\": %.1f}\n", name, best, nbytes / best / 1e6);
+    fflush(stdout);
+  };
+#define P(PAT, NT, D, SNT)                                                                   \
+  time("pat" #PAT "_nt" #NT "_depth" #D "_snt" #SNT,                                          \
+       [&] { hipLaunchKernelGGL((probe<PAT, NT, D, SNT>), dim3(tiles * B), dim3(256), 0, 0, a, tiles); }, \
+       bytes)
+#define P2(W, R, WR)                                                                          \
+  time("p2_span" #W "_rot" #R "_write" #WR,                                                    \
+       [&] { hipLaunchKernelGGL((probe2<W, R, WR>), dim3(tiles * B / W), dim3(256), 0, 0, a, tiles / W); }, \
+       WR ? bytes : bytes * 30 / 33)
+#define P3(R, SS, SNT)                                                                        \
+  time("p3_rot" #R "_store" #SS "_snt" #SNT,                                                   \
+       [&] { hipLaunchKernelGGL((probe3<R, SS, SNT>), dim3(tiles * B), dim3(256), 0, 0, a, tiles); }, bytes)
+  for (int rep = 0; rep < 2; ++rep) {
+    P3(0, 0, 0); P3(0, 0, 1); P3(0, 1, 0); P3(0, 1, 1);
+    P3(1, 0, 0); P3(1, 0, 1); P3(1, 1, 0); P3(1, 1, 1);
+  }
+  for (int rep = 0; rep < 1; ++rep) {
+    P2(1, 0, 1);
+    P2(1, 1, 1);
+    P2(2, 0, 1);
+    P2(2, 1, 1);
+    P2(4, 0, 1);
+    P2(1, 0, 0);
+    P2(1, 1, 0);
+    P2(2, 1, 0);
+  }
+  for (int rep = 0; rep < 1; ++rep) {
+    P(0, 0, 1, 0);
+    P(1, 0, 1, 0);
+    P(0, 1, 1, 0);
+    P(1, 1, 1, 0);
+    P(0, 0, 2, 0);
+    P(1, 0, 2, 0);
+    P(1, 1, 2, 0);
+    P(0, 2, 1, 0);
+    P(1, 0, 1, 1);
+    P(1, 1, 2, 1);
+    const size_t n = size_t(S) * K * B / 2 / 16;  // copy half of data into the other half
+    time("copy_float4", [&] {
+      hipLaunchKernelGGL(copy_kernel, dim3(256 * 8), dim3(256), 0, 0, (const u32x4 *)data,
+                         (u32x4 *)(data + n * 16), n);
+    }, double(n) * 32);
+    time("read_float4", [&] {
+      hipLaunchKernelGGL(read_kernel, dim3(256 * 8), dim3(256), 0, 0, (const u32x4 *)data,
+                         (u32x4 *)par, n * 2);
+    }, double(n) * 32);
+  }
+  return 0;
+}
