@@ -34,8 +34,8 @@ HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--segments", type=int, default=128, help="segments per GPU (C2: 128)")
     ap.add_argument("--segment-bytes", type=int, default=32 * 1024 * 1024)
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
