@@ -41,7 +41,14 @@ def parse():
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-shard-bytes", type=int, default=8 * 1024 * 1024)
     ap.add_argument("--cpu-threads", type=int, default=0)
-    return ap.parse_args()
+    ap.add_argument("--pcie", choices=["auto", "off"], default="auto",
+                    help="also time the host-memory path (pinned buffers, H2D+kernel+D2H)")
+    ap.add_argument("--strong", action="store_true",
+                    help="config C4: one job (default 320 segments) column-striped over the ranks")
+    a = ap.parse_args()
+    if a.strong and a.segments == 128:
+        a.segments = 320
+    return a
 
 
 def cpu_baseline(args):
@@ -82,12 +89,56 @@ def cpu_baseline(args):
     }
 
 
+def pcie_inclusive(ctx, data, shapes, S, dec_in, erased, steps=2):
+    """The reference path starts and ends in host memory: time the same batch
+    through bfrs_encode_host_batch / bfrs_decode_host_batch from pinned host
+    buffers (H2D + kernel + D2H pipelined over 3 streams).  Reported beside
+    `value`, never as `value`."""
+    import torch
+    nseg = data.shape[0]
+    nb = len(shapes)
+    h_data = torch.empty(nseg, S, dtype=torch.uint8, pin_memory=True)
+    h_data.copy_(data)
+    h_par = torch.empty(3 * nb, S, dtype=torch.uint8, pin_memory=True)
+    h_rest = torch.empty(3 * nb, S, dtype=torch.uint8, pin_memory=True)
+    enc_in = [h_data[s] for s in range(nseg)]
+    enc_out = [h_par[i] for i in range(3 * nb)]
+    dec_in_h, dec_out_h, seg = [], [], 0
+    for b, k in enumerate(shapes):
+        for i in range(k):
+            dec_in_h.append(None if i in erased[b] else h_data[seg + i])
+            dec_out_h.append(h_rest[3 * b + erased[b].index(i)] if i in erased[b] else None)
+        seg += k
+    ctx.encode_host_batch(shapes, 3, S, enc_in, enc_out)  # warm
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ctx.encode_host_batch(shapes, 3, S, enc_in, enc_out)
+    t_enc = (time.perf_counter() - t0) / steps
+    ctx.decode_host_batch(shapes, 3, S, dec_in_h, enc_out, dec_out_h)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ctx.decode_host_batch(shapes, 3, S, dec_in_h, enc_out, dec_out_h)
+    t_dec = (time.perf_counter() - t0) / steps
+    seg = 0
+    for b, k in enumerate(shapes):
+        for t, i in enumerate(erased[b]):
+            assert torch.equal(h_rest[3 * b + t], h_data[seg + i]), "host-path decode mismatch"
+        seg += k
+    gib = sum(shapes) * S / 2**30
+    return {
+        "encode_GiBps": round(gib / t_enc, 2), "decode_GiBps": round(gib / t_dec, 2),
+        "encode_ms": round(t_enc * 1e3, 2), "decode_ms": round(t_dec * 1e3, 2),
+        "h2d_bytes_encode": sum(shapes) * S, "d2h_bytes_encode": 3 * nb * S,
+        "note": "pinned host buffers; bfrs_*_host_batch (8 MiB column slabs over 3 HIP streams)",
+    }
+
+
 def main():
     args = parse()
     import numpy as np
     import torch
     import bfrs
-    from bfrs import synth
+    from bfrs import parallel, synth
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -98,16 +149,28 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    S = args.segment_bytes
+    S_full = args.segment_bytes
     nseg = args.segments
     shapes = synth.block_shapes(nseg)
     nb = len(shapes)
-    seed = 0xB10C + rank
+    if args.strong:
+        # C4: every rank owns a 64-byte-aligned column stripe of every shard
+        lo_b, hi_b = parallel.stripe_ranges(S_full, world)[rank]
+        S, seed = hi_b - lo_b, 0xB10C
+    else:
+        lo_b, S, seed = 0, S_full, 0xB10C + rank
 
-    # ---- resident workload
+    # ---- resident workload (this rank's bytes of every segment)
     data = torch.empty(nseg, S, dtype=torch.uint8, device="cuda")
-    for s in range(nseg):
-        synth.fill_segment_torch(data[s], seed, s)
+    if args.strong:
+        row = torch.empty(S_full, dtype=torch.uint8, device="cuda")
+        for s in range(nseg):
+            synth.fill_segment_torch(row, seed, s)
+            data[s].copy_(row[lo_b:lo_b + S])
+        del row
+    else:
+        for s in range(nseg):
+            synth.fill_segment_torch(data[s], seed, s)
     parity = torch.empty(3 * nb, S, dtype=torch.uint8, device="cuda")
     restored = torch.empty(3 * nb, S, dtype=torch.uint8, device="cuda")
     enc_in = [data[s] for s in range(nseg)]
@@ -159,10 +222,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     launch_ms = ev0.elapsed_time(ev1) / (2 * args.steps)
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = parallel.max_over_ranks(elapsed, dist, device="cuda")
 
     # Per-direction rates: short back-to-back loops after the timed region.
     def per_launch(fn, n=max(3, args.steps // 2)):
@@ -174,15 +234,20 @@ def main():
         torch.cuda.synchronize()
         return a.elapsed_time(b) / n
     enc_ms, dec_ms = per_launch(encode), per_launch(decode)
-    data_bytes = sum(shapes) * S                     # original data per direction
+    data_bytes = sum(shapes) * S                     # original data per direction (this rank)
     alg_bytes = sum(k + 3 for k in shapes) * S        # HBM bytes per launch (both directions)
-    gib_step = 2 * data_bytes / 2**30
-    value = world * gib_step * args.steps / elapsed
+    scaling = "strong" if args.strong else "weak"
+    job_bytes_step = 2 * sum(shapes) * (S_full if args.strong else S)
+    value = parallel.throughput(job_bytes_step, world, args.steps, elapsed, scaling)
 
     if rank != 0:
         if dist:
             dist.destroy_process_group()
         return
+
+    pcie = None
+    if world == 1 and args.pcie == "auto" and not args.strong:
+        pcie = pcie_inclusive(ctx, data, shapes, S, dec_in, erased)
 
     achieved = alg_bytes / (launch_ms * 1e-3) / 1e9
     traffic = None
@@ -205,15 +270,19 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "u8",
         "data": f"synthetic splitmix64 bytes (seed 0xB10C+rank), resident in HBM",
         "config": {
-            "workload": "BASELINE configs[1]+[2]: 128 x 32 MiB segments = 4xRS(30,3)+1xRS(8,3); "
-                        "step = encode batch + 3-erasure decode of every block",
-            "segments_per_gpu": nseg, "segment_bytes": S, "blocks": shapes, "parity_shards": 3,
-            "parallelism": f"independent batch per GPU x{world}",
+            "workload": ("BASELINE configs[3]: 10 GiB archive, 320 x 32 MiB segments = "
+                         "10xRS(30,3)+1xRS(20,3), column-striped over the GPUs"
+                         if args.strong else
+                         "BASELINE configs[1]+[2]: 128 x 32 MiB segments = 4xRS(30,3)+1xRS(8,3); "
+                         "step = encode batch + 3-erasure decode of every block"),
+            "segments": nseg, "segment_bytes": S_full, "blocks": shapes, "parity_shards": 3,
+            "parallelism": (f"64-B column stripes x{world}" if args.strong
+                            else f"independent batch per GPU x{world}"),
         },
         "encode_GiBps_per_gpu": round(data_bytes / 2**30 / (enc_ms * 1e-3), 2),
         "decode_GiBps_per_gpu": round(data_bytes / 2**30 / (dec_ms * 1e-3), 2),
@@ -227,6 +296,7 @@ def main():
             "timing": "HIP events on the launch stream over the timed region / launches",
         },
         "cpu_baseline": cpu,
+        "pcie_inclusive": pcie,
     }
     print(json.dumps(line), flush=True)
     if dist:

@@ -49,7 +49,8 @@ EXPORTS = (
     "bfrs_encoder_encode", "bfrs_encoder_recovery", "bfrs_encoder_free", "bfrs_decoder_new",
     "bfrs_decoder_add_original_shard", "bfrs_decoder_add_recovery_shard", "bfrs_decoder_decode",
     "bfrs_decoder_restored_original", "bfrs_decoder_free", "bfrs_encode", "bfrs_decode",
-    "bfrs_encode_batch_dev", "bfrs_decode_batch_dev", "bfrs_generate_parity",
+    "bfrs_encode_batch_dev", "bfrs_decode_batch_dev", "bfrs_encode_host_batch",
+    "bfrs_decode_host_batch", "bfrs_generate_parity",
     "bfrs_generate_parity_segmented", "bfrs_recover_segment_rs13", "bfrs_recover_segment_rs30_3",
 )
 
@@ -107,6 +108,10 @@ def lib() -> ctypes.CDLL:
                                        _pp, _vp], ctypes.c_int),
             "bfrs_decode_batch_dev": ([_vp, _sz, ctypes.POINTER(ctypes.c_uint32), _sz, _sz, _pp,
                                        _pp, _pp, _vp], ctypes.c_int),
+            "bfrs_encode_host_batch": ([_vp, _sz, ctypes.POINTER(ctypes.c_uint32), _sz, _sz, _pp,
+                                        _pp], ctypes.c_int),
+            "bfrs_decode_host_batch": ([_vp, _sz, ctypes.POINTER(ctypes.c_uint32), _sz, _sz, _pp,
+                                        _pp, _pp], ctypes.c_int),
             "bfrs_generate_parity": ([_vp, _pp, ctypes.POINTER(_sz), _sz, _sz, _sz, _pp,
                                       ctypes.POINTER(_sz)], ctypes.c_int),
             "bfrs_generate_parity_segmented": ([_vp, _vp, _sz, _pp, ctypes.POINTER(_sz)],
@@ -263,6 +268,34 @@ class Context:
         def call(stream_handle=None, _keep=(ks, ko, kr, kd)):
             _check(fn(h, n, ks, recovery_count, shard_bytes, po, pr, pd, stream_handle))
         return call
+
+    # ---- host-memory batch API (host buffers: numpy arrays or CPU torch tensors)
+    @staticmethod
+    def _haddr(t) -> Optional[int]:
+        if t is None:
+            return None
+        if isinstance(t, int):
+            return t
+        if hasattr(t, "data_ptr"):
+            return t.data_ptr()
+        return _host_ptr(t)
+
+    def encode_host_batch(self, original_counts, recovery_count, shard_bytes, originals,
+                          recovery_out) -> None:
+        ks = (ctypes.c_uint32 * len(original_counts))(*original_counts)
+        po, ko = _ptr_array([self._haddr(t) for t in originals])
+        pr, kr = _ptr_array([self._haddr(t) for t in recovery_out])
+        _check(lib().bfrs_encode_host_batch(self.handle, len(original_counts), ks, recovery_count,
+                                            shard_bytes, po, pr))
+
+    def decode_host_batch(self, original_counts, recovery_count, shard_bytes, originals,
+                          recovery, restored_out) -> None:
+        ks = (ctypes.c_uint32 * len(original_counts))(*original_counts)
+        po, ko = _ptr_array([self._haddr(t) for t in originals])
+        pr, kr = _ptr_array([self._haddr(t) for t in recovery])
+        pd, kd = _ptr_array([self._haddr(t) for t in restored_out])
+        _check(lib().bfrs_decode_host_batch(self.handle, len(original_counts), ks, recovery_count,
+                                            shard_bytes, po, pr, pd))
 
     # ---- one-shot host API (numpy in, numpy out)
     def encode(self, originals, recovery_count=3):

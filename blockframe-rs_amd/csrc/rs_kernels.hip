@@ -121,10 +121,7 @@ __device__ __forceinline__ uint4 load16(uint64_t a) {
   const u32x4 v = *(const AS_GLOBAL u32x4 *)(uintptr_t)a;
   return make_uint4(v.x, v.y, v.z, v.w);
 }
-__device__ __forceinline__ void store16(uint64_t a, const uint4 &v) {
-  u32x4 w = {v.x, v.y, v.z, v.w};
-  *(AS_GLOBAL u32x4 *)(uintptr_t)a = w;
-}
+
 
 __device__ __forceinline__ void store16_nt(uint64_t a, const u32x4 &v) {
   __builtin_nontemporal_store(v, (AS_GLOBAL u32x4 *)(uintptr_t)a);

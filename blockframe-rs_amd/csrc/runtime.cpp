@@ -101,6 +101,12 @@ Context::~Context() {
   if (stream) (void)hipStreamSynchronize(stream);
   plans.clear();
   if (d_scratch) (void)hipFree(d_scratch);
+  for (auto &ps : pipe_stream)
+    if (ps) {
+      (void)hipStreamSynchronize(ps);
+      (void)hipStreamDestroy(ps);
+    }
+  if (pipe_buf) (void)hipFree(pipe_buf);
   if (stream) (void)hipStreamDestroy(stream);
 }
 
@@ -112,6 +118,7 @@ int Context::init(int dev) {
   device = dev;
   HIP_TRY(hipSetDevice(dev));
   HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+  for (auto &ps : pipe_stream) HIP_TRY(hipStreamCreateWithFlags(&ps, hipStreamNonBlocking));
   return BFRS_OK;
 }
 
@@ -127,6 +134,77 @@ int Context::scratch(size_t bytes, void **out) {
     scratch_cap = bytes;
   }
   *out = d_scratch;
+  return BFRS_OK;
+}
+
+int Context::run_host(bool decode, size_t nblocks, const uint32_t *ks, size_t m,
+                      size_t shard_bytes, const uint8_t *const *orig, const uint8_t *const *rec,
+                      uint8_t *const *out) {
+  // Slab width: whole 64-byte chunks, ~8 MiB of columns per shard (env
+  // BFRS_SLAB_BYTES overrides), the shard's tail chunk rides in the last slab.
+  size_t slab = 8u << 20;
+  if (const char *e = std::getenv("BFRS_SLAB_BYTES")) slab = std::max<size_t>(64, atoll(e));
+  slab = std::max<size_t>(64, slab / 64 * 64);
+  if (slab >= shard_bytes) slab = shard_bytes;
+  size_t kmax = 0;
+  for (size_t b = 0; b < nblocks; ++b) kmax = std::max<size_t>(kmax, ks[b]);
+  // slab + 64 covers a last slab that carries the tail chunk; stride 256-aligned
+  const size_t stride = round_up(slab + 64, 256);
+  const size_t need = stride * (kmax + m);
+  if (need > pipe_cap) {
+    for (auto &ps : pipe_stream) HIP_TRY(hipStreamSynchronize(ps));
+    if (pipe_buf) HIP_TRY(hipFree(pipe_buf));
+    pipe_buf = nullptr;
+    pipe_cap = 0;
+    HIP_TRY(hipMalloc(&pipe_buf, need * kPipeSlots));
+    pipe_cap = need;
+  }
+  int slot = 0;
+  size_t oi = 0;
+  for (size_t b = 0; b < nblocks; ++b) {
+    const size_t k = ks[b];
+    const uint8_t *const *bo = orig + oi;
+    const uint8_t *const *br = decode ? rec + b * m : nullptr;
+    uint8_t *const *bout = decode ? out + oi : out + b * m;
+    oi += k;
+    for (size_t off = 0; off < shard_bytes;) {
+      size_t len = std::min(slab, shard_bytes - off);
+      if (shard_bytes - (off + len) < 64) len = shard_bytes - off;  // fold the tail in
+      hipStream_t st = pipe_stream[slot];
+      uint8_t *base = static_cast<uint8_t *>(pipe_buf) + size_t(slot) * pipe_cap;
+      std::vector<const uint8_t *> din(k, nullptr), drec(m, nullptr);
+      std::vector<uint8_t *> dout(decode ? k : m, nullptr);
+      for (size_t i = 0; i < k; ++i) {
+        if (!bo[i]) {
+          if (decode) dout[i] = base + i * stride;
+          continue;
+        }
+        din[i] = base + i * stride;
+        HIP_TRY(hipMemcpyAsync(base + i * stride, bo[i] + off, len, hipMemcpyHostToDevice, st));
+      }
+      for (size_t j = 0; j < m; ++j) {
+        uint8_t *d = base + (kmax + j) * stride;
+        if (decode) {
+          if (!br[j]) continue;
+          drec[j] = d;
+          HIP_TRY(hipMemcpyAsync(d, br[j] + off, len, hipMemcpyHostToDevice, st));
+        } else {
+          dout[j] = d;
+        }
+      }
+      uint32_t kk = uint32_t(k);
+      bfrs_ctx *self = reinterpret_cast<bfrs_ctx *>(this);
+      int rc = decode ? decode_batch_on(self, 1, &kk, m, len, din.data(), drec.data(),
+                                        dout.data(), st)
+                      : encode_batch_on(self, 1, &kk, m, len, din.data(), dout.data(), st);
+      if (rc) return rc;
+      for (size_t t = 0; t < dout.size(); ++t)
+        if (dout[t]) HIP_TRY(hipMemcpyAsync(bout[t] + off, dout[t], len, hipMemcpyDeviceToHost, st));
+      slot = (slot + 1) % kPipeSlots;
+      off += len;
+    }
+  }
+  for (auto &ps : pipe_stream) HIP_TRY(hipStreamSynchronize(ps));
   return BFRS_OK;
 }
 
@@ -455,39 +533,66 @@ int decode_batch_on(bfrs_ctx *ctx, size_t nblocks, const uint32_t *ks, size_t m,
 
 extern "C" {
 
-// ---- one-shot host-memory API ----------------------------------------------
+// ---- host-memory API: pipelined through HBM ----------------------------------
+static int check_host_batch(bfrs_ctx *ctx, size_t nblocks, const uint32_t *ks, size_t m,
+                            size_t shard_bytes, bool decode, const uint8_t *const *orig,
+                            const uint8_t *const *rec, uint8_t *const *out) {
+  if (!ctx || (nblocks && (!ks || !orig || !out || (decode && !rec))))
+    return set_error(BFRS_E_INVALID_ARGUMENT, "host batch: NULL argument");
+  size_t oi = 0;
+  for (size_t b = 0; b < nblocks; ++b) {
+    int rc = check_shape(ks[b], m, shard_bytes);
+    if (rc) return rc;
+    size_t orecv = 0, rrecv = 0;
+    for (size_t i = 0; i < ks[b]; ++i) {
+      orecv += orig[oi + i] != nullptr;
+      if (!decode && !orig[oi + i]) return set_error(BFRS_E_INVALID_ARGUMENT, "original is NULL");
+      if (decode && !orig[oi + i] && !out[oi + i])
+        return set_error(BFRS_E_INVALID_ARGUMENT, "restored buffer for erased shard is NULL");
+    }
+    if (decode) {
+      for (size_t j = 0; j < m; ++j) rrecv += rec[b * m + j] != nullptr;
+      if (orecv + rrecv < ks[b]) {
+        std::ostringstream os;
+        os << "not enough shards: " << orecv << " original + " << rrecv << " recovery < "
+           << ks[b] << " original_count";
+        return set_error(BFRS_E_NOT_ENOUGH_SHARDS, os.str());
+      }
+    } else {
+      for (size_t j = 0; j < m; ++j)
+        if (!out[b * m + j]) return set_error(BFRS_E_INVALID_ARGUMENT, "recovery buffer is NULL");
+    }
+    oi += ks[b];
+  }
+  return BFRS_OK;
+}
+
+int bfrs_encode_host_batch(bfrs_ctx *ctx, size_t nblocks, const uint32_t *ks, size_t m,
+                           size_t shard_bytes, const uint8_t *const *orig,
+                           uint8_t *const *rec_out) {
+  int rc = check_host_batch(ctx, nblocks, ks, m, shard_bytes, false, orig, nullptr, rec_out);
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(ctx->impl.device));
+  return ctx->impl.run_host(false, nblocks, ks, m, shard_bytes, orig, nullptr, rec_out);
+}
+
+int bfrs_decode_host_batch(bfrs_ctx *ctx, size_t nblocks, const uint32_t *ks, size_t m,
+                           size_t shard_bytes, const uint8_t *const *orig,
+                           const uint8_t *const *rec, uint8_t *const *restored_out) {
+  int rc = check_host_batch(ctx, nblocks, ks, m, shard_bytes, true, orig, rec, restored_out);
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(ctx->impl.device));
+  return ctx->impl.run_host(true, nblocks, ks, m, shard_bytes, orig, rec, restored_out);
+}
+
 int bfrs_encode(bfrs_ctx *ctx, size_t k, size_t m, size_t shard_bytes,
                 const uint8_t *const *originals, uint8_t *const *recovery_out) {
   if (!ctx || !originals || !recovery_out)
     return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_encode: NULL argument");
   int rc = check_shape(k, m, shard_bytes);
   if (rc) return rc;
-  for (size_t i = 0; i < k; ++i)
-    if (!originals[i]) return set_error(BFRS_E_INVALID_ARGUMENT, "original shard is NULL");
-  for (size_t j = 0; j < m; ++j)
-    if (!recovery_out[j]) return set_error(BFRS_E_INVALID_ARGUMENT, "recovery buffer is NULL");
-  Context &c = ctx->impl;
-  HIP_TRY(hipSetDevice(c.device));
-  const size_t stride = round_up(shard_bytes, 256);
-  void *base;
-  if ((rc = c.scratch(stride * (k + m), &base))) return rc;
-  auto *d = static_cast<uint8_t *>(base);
-  std::vector<const uint8_t *> din(k);
-  std::vector<uint8_t *> dout(m);
-  for (size_t i = 0; i < k; ++i) {
-    din[i] = d + i * stride;
-    HIP_TRY(hipMemcpyAsync(d + i * stride, originals[i], shard_bytes, hipMemcpyHostToDevice,
-                           c.stream));
-  }
-  for (size_t j = 0; j < m; ++j) dout[j] = d + (k + j) * stride;
-  uint32_t kk = uint32_t(k);
-  if ((rc = encode_batch_on(ctx, 1, &kk, m, shard_bytes, din.data(), dout.data(), c.stream)))
-    return rc;
-  for (size_t j = 0; j < m; ++j)
-    HIP_TRY(hipMemcpyAsync(recovery_out[j], dout[j], shard_bytes, hipMemcpyDeviceToHost,
-                           c.stream));
-  HIP_TRY(hipStreamSynchronize(c.stream));
-  return BFRS_OK;
+  const uint32_t kk = uint32_t(k);
+  return bfrs_encode_host_batch(ctx, 1, &kk, m, shard_bytes, originals, recovery_out);
 }
 
 int bfrs_decode(bfrs_ctx *ctx, size_t k, size_t m, size_t shard_bytes,
@@ -497,41 +602,8 @@ int bfrs_decode(bfrs_ctx *ctx, size_t k, size_t m, size_t shard_bytes,
     return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_decode: NULL argument");
   int rc = check_shape(k, m, shard_bytes);
   if (rc) return rc;
-  Context &c = ctx->impl;
-  HIP_TRY(hipSetDevice(c.device));
-  const size_t stride = round_up(shard_bytes, 256);
-  void *base;
-  if ((rc = c.scratch(stride * (k + m), &base))) return rc;
-  auto *d = static_cast<uint8_t *>(base);
-  std::vector<const uint8_t *> dorig(k), drec(m);
-  std::vector<uint8_t *> drest(k, nullptr);
-  for (size_t i = 0; i < k; ++i) {
-    uint8_t *slot = d + i * stride;
-    if (originals[i]) {
-      HIP_TRY(hipMemcpyAsync(slot, originals[i], shard_bytes, hipMemcpyHostToDevice, c.stream));
-      dorig[i] = slot;
-    } else {
-      if (!restored_out[i])
-        return set_error(BFRS_E_INVALID_ARGUMENT, "restored buffer for erased shard is NULL");
-      drest[i] = slot;
-    }
-  }
-  for (size_t j = 0; j < m; ++j) {
-    if (!recovery[j]) continue;
-    uint8_t *slot = d + (k + j) * stride;
-    HIP_TRY(hipMemcpyAsync(slot, recovery[j], shard_bytes, hipMemcpyHostToDevice, c.stream));
-    drec[j] = slot;
-  }
-  uint32_t kk = uint32_t(k);
-  if ((rc = decode_batch_on(ctx, 1, &kk, m, shard_bytes, dorig.data(), drec.data(),
-                             drest.data(), c.stream)))
-    return rc;
-  for (size_t i = 0; i < k; ++i)
-    if (!originals[i])
-      HIP_TRY(hipMemcpyAsync(restored_out[i], drest[i], shard_bytes, hipMemcpyDeviceToHost,
-                             c.stream));
-  HIP_TRY(hipStreamSynchronize(c.stream));
-  return BFRS_OK;
+  const uint32_t kk = uint32_t(k);
+  return bfrs_decode_host_batch(ctx, 1, &kk, m, shard_bytes, originals, recovery, restored_out);
 }
 
 }  // extern "C"

@@ -55,6 +55,12 @@ struct Context {
   void *d_scratch = nullptr;
   size_t scratch_cap = 0;
 
+  // Host-path pipeline: slots of device slab buffers, one stream each.
+  static constexpr int kPipeSlots = 3;
+  hipStream_t pipe_stream[kPipeSlots] = {};
+  void *pipe_buf = nullptr;
+  size_t pipe_cap = 0;  // bytes per slot
+
   ~Context();
   int init(int dev);
   int get_encode_plan(size_t k, size_t m, const Plan **out);
@@ -63,6 +69,10 @@ struct Context {
   // Queue the passes of all blocks (same shard_bytes) on `stream`.
   int run_blocks(const std::vector<BlockIO> &blocks, size_t shard_bytes, hipStream_t stream);
   int scratch(size_t bytes, void **out);
+  // Streams host-memory blocks through HBM (see bfrs_encode_host_batch).
+  // orig/rec/out are per-block host pointer lists (decode: NULL = missing).
+  int run_host(bool decode, size_t nblocks, const uint32_t *ks, size_t m, size_t shard_bytes,
+               const uint8_t *const *orig, const uint8_t *const *rec, uint8_t *const *out);
 };
 
 // Argument validation shared by every entry point (crate's Error variants).

@@ -127,6 +127,21 @@ int bfrs_decode(bfrs_ctx *ctx, size_t original_count, size_t recovery_count, siz
                 const uint8_t *const *originals, const uint8_t *const *recovery,
                 uint8_t *const *restored_out);
 
+/* Host-memory batch API (the reference's path starts and ends in host memory:
+ * mmap'd files, fs::read).  Same shapes as the device batch API below but
+ * every pointer is host memory; shards are streamed through HBM in 64-byte
+ * aligned column slabs over several HIP streams so host->device copies,
+ * kernels and device->host copies overlap.  Pinned (page-locked) host
+ * buffers reach PCIe rate; pageable ones work but go through the runtime's
+ * staging.  Blocks until the outputs are in host memory. */
+int bfrs_encode_host_batch(bfrs_ctx *ctx, size_t nblocks, const uint32_t *original_counts,
+                           size_t recovery_count, size_t shard_bytes,
+                           const uint8_t *const *originals, uint8_t *const *recovery_out);
+int bfrs_decode_host_batch(bfrs_ctx *ctx, size_t nblocks, const uint32_t *original_counts,
+                           size_t recovery_count, size_t shard_bytes,
+                           const uint8_t *const *originals, const uint8_t *const *recovery,
+                           uint8_t *const *restored_out);
+
 /* ---- device-resident batch API (pointers are device memory) ----------- */
 /* Encodes nblocks independent RS blocks in one launch.  Block b has
  * original_counts[b] originals, all blocks share recovery_count and

@@ -135,6 +135,39 @@ def test_misaligned_device_pointer_rejected(ctx, bfrs):
     assert e.value.code == bfrs.E_INVALID_ARGUMENT
 
 
+# ---------------------------------------------------------------- host-memory batch (PCIe path)
+@pytest.mark.parametrize("slab", [None, "4096", "1024"])
+def test_host_batch_pipeline_vs_oracle(ctx, oracle, slab, monkeypatch):
+    """Multi-slab streaming through HBM (slab width forced small) must give the
+    same bytes as one-shot: checks slab boundaries, the folded tail chunk and
+    the stream rotation."""
+    if slab:
+        monkeypatch.setenv("BFRS_SLAB_BYTES", slab)
+    rng = np.random.default_rng(21)
+    n = 64 * 150 + 38
+    ks = [30, 8, 1, 20]
+    host = [[rng.integers(0, 256, n, dtype=np.uint8) for _ in range(k)] for k in ks]
+    rec = [np.empty(n, np.uint8) for _ in range(3 * len(ks))]
+    ctx.encode_host_batch(ks, 3, n, [a for blk in host for a in blk], rec)
+    want = [oracle.encode(blk, 3) for blk in host]
+    for b in range(len(ks)):
+        for j in range(3):
+            assert np.array_equal(rec[3 * b + j], want[b][j]), (slab, b, j)
+    orig, out, er_all = [], [], []
+    for b, k in enumerate(ks):
+        er = set(range(min(3, k)))
+        er_all.append(er)
+        for i in range(k):
+            orig.append(None if i in er else host[b][i])
+            out.append(np.empty(n, np.uint8) if i in er else None)
+    ctx.decode_host_batch(ks, 3, n, orig, rec, out)
+    oi = 0
+    for b, k in enumerate(ks):
+        for i in er_all[b]:
+            assert np.array_equal(out[oi + i], host[b][i]), (slab, b, i)
+        oi += k
+
+
 # ---------------------------------------------------------------- crate-API mirror
 def test_streaming_encoder_decoder(ctx, bfrs, oracle):
     rng = np.random.default_rng(2)

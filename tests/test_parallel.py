@@ -1,0 +1,73 @@
+"""CPU: the N>1 path (gloo, world_size 2).
+
+* stripe partitioning: encoding each 64-byte-aligned column stripe separately
+  and concatenating gives exactly the full-shard parity (the property that
+  makes config C4's strong scaling exchange-free), checked with the oracle;
+* the max-over-ranks timing reduction and the whole-job throughput formula
+  bench.py uses, run in two real processes over gloo.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from bfrs import parallel
+
+
+def test_stripe_ranges_cover_and_align():
+    for S in (64, 128, 33554432, 33554432 + 38, 1000):
+        for G in (1, 2, 3, 4, 8):
+            r = parallel.stripe_ranges(S, G)
+            assert r[0][0] == 0 and r[-1][1] == S
+            for (a, b), (c, d) in zip(r, r[1:]):
+                assert b == c and a % 64 == 0 and b % 64 == 0 or b == S
+            sizes = [b - a for a, b in r]
+            assert max(sizes) - min(sizes) <= 64 + S % 64
+
+
+@pytest.mark.parametrize("G", [2, 3, 8])
+def test_striped_encode_equals_full(oracle, G):
+    rng = np.random.default_rng(G)
+    S = 64 * 37 + 38  # ragged: stripes of unequal chunk counts + a tail
+    data = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(30)]
+    full = oracle.encode(data, 3)
+    parts = [[] for _ in range(3)]
+    for a, b in parallel.stripe_ranges(S, G):
+        rec = oracle.encode([d[a:b] for d in data], 3)
+        for j in range(3):
+            parts[j].append(rec[j])
+    for j in range(3):
+        assert np.array_equal(np.concatenate(parts[j]), full[j])
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    elapsed = 1.0 + rank  # rank 1 is the slow one
+    m = parallel.max_over_ranks(elapsed, dist)
+    v = parallel.throughput(2 * 2**30, world, 10, m, "weak")
+    dist.barrier()
+    q.put((rank, m, v))
+    dist.destroy_process_group()
+
+
+def test_gloo_two_ranks_max_and_weak_throughput():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, m, v in res:
+        assert m == 2.0                      # max over ranks
+        assert v == pytest.approx(2 * 2 * 10 / 2.0)  # 2 ranks x 2 GiB x 10 steps / 2 s
