@@ -254,7 +254,10 @@ def main():
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc):
         try:
-            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+            rec = json.load(open(pmc))
+            # only when the profiled launch is this launch shape
+            if rec.get("algorithmic_read_bytes", 0) + rec.get("algorithmic_write_bytes", 0) == alg_bytes:
+                traffic = rec.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
     cpu = None

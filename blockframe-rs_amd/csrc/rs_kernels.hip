@@ -160,6 +160,17 @@ __device__ __forceinline__ void mac_input(const u32x4 &Lv, const u32x4 &Hv, uint
 }
 
 // VARIANT 1: default; 3 / 4: variant 1 compiled for >= 7 / 8 waves per SIMD.
+// XCD-aware remap (speed only, never correctness): hardware deals workgroups
+// round-robin over 8 XCDs; remap so XCD x works through a contiguous range of
+// the grid.  Bijective for any grid size.
+__device__ __forceinline__ uint32_t xcd_swizzle(uint32_t b, uint32_t n) {
+  const uint32_t x = b & 7, q = b >> 3;
+  const uint32_t per = n >> 3, rem = n & 7;
+  // XCDs < rem own per+1 workgroups, the rest per
+  const uint32_t start = x * per + min(x, rem);
+  return start + q;
+}
+
 template <int VARIANT>
 __global__ __launch_bounds__(256, VARIANT == 3 ? 7 : (VARIANT == 4 ? 8 : 1)) void gf_apply_kernel(
     const KernArgs args) {
@@ -169,7 +180,7 @@ __global__ __launch_bounds__(256, VARIANT == 3 ? 7 : (VARIANT == 4 ? 8 : 1)) voi
   const uint32_t n_passes = args.n_passes, tiles_per_wg = args.tiles_per_wg;
 
   // Locate this workgroup's pass (wave-uniform binary search over wg_begin).
-  const uint32_t wg = blockIdx.x;
+  const uint32_t wg = VARIANT == 7 ? xcd_swizzle(blockIdx.x, gridDim.x) : blockIdx.x;
   uint32_t lo = 0, hi = n_passes;
   while (hi - lo > 1) {
     const uint32_t mid = (lo + hi) >> 1;
@@ -239,6 +250,116 @@ __global__ __launch_bounds__(256, VARIANT == 3 ? 7 : (VARIANT == 4 ? 8 : 1)) voi
       r = r2;
     }
     vm_wait<0>(La, Ha);  // drain the final (unused) prefetch
+
+    const uint64_t *outp = args.ptrs + P.out;
+    const bool accumulate = P.accumulate != 0;
+    for (uint32_t t = 0; t < n_out; ++t) {
+      uint4 ol = make_uint4(gather_byte(acc_lo, 0, t), gather_byte(acc_lo, 1, t),
+                            gather_byte(acc_lo, 2, t), gather_byte(acc_lo, 3, t));
+      uint4 oh = make_uint4(gather_byte(acc_hi, 0, t), gather_byte(acc_hi, 1, t),
+                            gather_byte(acc_hi, 2, t), gather_byte(acc_hi, 3, t));
+      const uint64_t dst = outp[t] + off;
+      if (accumulate) {
+        const uint4 pl = load16(dst), ph = load16(dst + 32);
+        ol.x ^= pl.x; ol.y ^= pl.y; ol.z ^= pl.z; ol.w ^= pl.w;
+        oh.x ^= ph.x; oh.y ^= ph.y; oh.z ^= ph.z; oh.w ^= ph.w;
+      }
+      store16_nt(dst, u32x4{ol.x, ol.y, ol.z, ol.w});
+      store16_nt(dst + 32, u32x4{oh.x, oh.y, oh.z, oh.w});
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Variants 5 / 6: variant 1 with an NB-buffer ring (NB-1 inputs in flight per
+// wave instead of 1).  The loop body is unrolled NB times with a uniform exit
+// after every input, so no input padding is needed; past the last input the
+// prefetch re-reads the last processed input (a cache hit, never consumed).
+// ---------------------------------------------------------------------------
+template <int NB>
+__global__ __launch_bounds__(256) void gf_apply_ring_kernel(const KernArgs args) {
+  extern __shared__ __attribute__((aligned(16))) uint2 lds_table[];
+  const PassDesc *passes = args.passes;
+  const uint32_t n_passes = args.n_passes, tiles_per_wg = args.tiles_per_wg;
+  const uint32_t wg = blockIdx.x;
+  uint32_t lo = 0, hi = n_passes;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (passes[mid].wg_begin <= wg)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  const PassDesc &P = passes[lo];
+  const uint32_t n_in = P.n_in, n_out = P.n_out;
+  const uint64_t *in = args.ptrs + P.in;
+  {
+    const AS_GLOBAL u32x4 *tab = (const AS_GLOBAL u32x4 *)(uintptr_t)P.table;
+    u32x4 *dst = reinterpret_cast<u32x4 *>(lds_table);
+    const uint32_t n16 = n_in * 32;
+    u32x4 v[kMaxPassInputs * 32 / 256];
+#pragma unroll
+    for (int r = 0; r < int(kMaxPassInputs * 32 / 256); ++r) {
+      const uint32_t e = threadIdx.x + 256u * r;
+      v[r] = e < n16 ? tab[e] : u32x4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int r = 0; r < int(kMaxPassInputs * 32 / 256); ++r) {
+      const uint32_t e = threadIdx.x + 256u * r;
+      if (e < n16) dst[e] = v[r];
+    }
+  }
+  __syncthreads();
+
+  const uint64_t full_hc = P.full_chunks * 2;
+  const uint32_t t_begin = (wg - P.wg_begin) * tiles_per_wg;
+  const uint32_t t_end = min(t_begin + tiles_per_wg, P.n_tiles);
+  const uint32_t wave_id = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+
+  for (uint32_t tile = t_begin; tile < t_end; ++tile) {
+    const uint64_t hc = uint64_t(tile) * kTileHalfChunks + threadIdx.x;
+    if (hc >= full_hc) break;
+    const uint64_t off = (hc >> 1) * 64 + (hc & 1) * 16;
+    const uint32_t voff = uint32_t(off);
+    uint32_t acc_lo[16], acc_hi[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) acc_lo[s] = acc_hi[s] = 0;
+
+    // input index of step x (x >= n_in: repeat the last input -> cache hit)
+    const uint32_t rot = P.rotate ? (tile * 4 + wave_id) % n_in : 0;
+    auto idx = [&](uint32_t x) -> uint32_t {
+      if (x >= n_in) x = n_in - 1;
+      const uint32_t y = rot + x;
+      return y >= n_in ? y - n_in : y;
+    };
+    auto mac = [&](const u32x4 &Lv, const u32x4 &Hv, uint32_t x) {
+      const uint32_t r = idx(x);
+      mac_input_v1(make_uint4(Lv.x, Lv.y, Lv.z, Lv.w), make_uint4(Hv.x, Hv.y, Hv.z, Hv.w),
+                   nullptr, 2 * r, 2 * r + 1, acc_lo, acc_hi);
+    };
+    // 4-buffer ring, 3 inputs in flight; n_in is even (host pads), exits
+    // every 2 inputs keep the register allocation flat.
+    u32x4 LA, HA, LB, HB, LC, HC, LD, HD;
+    gload_half_chunk(LA, HA, in[idx(0)], voff);
+    gload_half_chunk(LB, HB, in[idx(1)], voff);
+    gload_half_chunk(LC, HC, in[idx(2)], voff);
+    for (uint32_t i = 0;; i += 4) {
+      gload_half_chunk(LD, HD, in[idx(i + 3)], voff);
+      vm_wait<6>(LA, HA);
+      mac(LA, HA, i);
+      gload_half_chunk(LA, HA, in[idx(i + 4)], voff);
+      vm_wait<6>(LB, HB);
+      mac(LB, HB, i + 1);
+      if (i + 2 >= n_in) break;
+      gload_half_chunk(LB, HB, in[idx(i + 5)], voff);
+      vm_wait<6>(LC, HC);
+      mac(LC, HC, i + 2);
+      gload_half_chunk(LC, HC, in[idx(i + 6)], voff);
+      vm_wait<6>(LD, HD);
+      mac(LD, HD, i + 3);
+      if (i + 4 >= n_in) break;
+    }
+    vm_wait<0>(LA, HA);
 
     const uint64_t *outp = args.ptrs + P.out;
     const bool accumulate = P.accumulate != 0;
@@ -447,11 +568,16 @@ __global__ __launch_bounds__(64) void gf_tail_kernel(const KernArgs args) {
 // is a traffic-only probe and is refused unless BFRS_ALLOW_PROBE=1.
 int kernel_variant() {
   const char *e = std::getenv("BFRS_KERNEL_VARIANT");
-  int v = e ? atoi(e) : 1;
+  int v = e ? atoi(e) : 5;
   if (v == 9 && !std::getenv("BFRS_ALLOW_PROBE")) v = 1;
   return v;
 }
 
+// Variants: 5 (default) = v1 arithmetic with a 4-buffer ring (3 inputs in
+// flight per wave); 1 = ping-pong (1 in flight); 0 = naive indexing;
+// 2 = contiguous-load layout; 3/4 = occupancy-bounded builds of 1; 7 = 1 with
+// an XCD-aware grid remap; 9 = traffic-only probe (refused unless
+// BFRS_ALLOW_PROBE=1).  Results of each: DESIGN.md §9.
 uint32_t tile_bytes() { return kernel_variant() == 2 ? kV2TileBytes : kTileHalfChunks * 32; }
 
 hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in,
@@ -474,6 +600,13 @@ hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in
     case 4:
       hipLaunchKernelGGL(gf_apply_kernel<4>, dim3(n_wgs), dim3(256), lds, stream, args);
       break;
+    case 5:
+      hipLaunchKernelGGL(gf_apply_ring_kernel<3>, dim3(n_wgs), dim3(256), lds, stream, args);
+      break;
+    case 7:
+      hipLaunchKernelGGL(gf_apply_kernel<7>, dim3(n_wgs), dim3(256), lds, stream, args);
+      break;
+
     default:
       hipLaunchKernelGGL(gf_apply_v2_kernel, dim3(n_wgs), dim3(256), lds, stream, args);
   }

@@ -208,6 +208,49 @@ __global__ __launch_bounds__(256) void probe3(Args a, uint32_t tiles_per_block) 
   }
 }
 
+
+// probe4: probe3 (rot1) but the 6 output stores are spread through the input
+// loop (store q issued after input 5q) instead of bursting at the end.
+template <int SNT, int SPREAD>
+__global__ __launch_bounds__(256) void probe4(Args a, uint32_t tiles_per_block) {
+  const uint32_t b = blockIdx.x / tiles_per_block;
+  const uint32_t tile = blockIdx.x % tiles_per_block;
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t col = (uint64_t(tile) * 4 + wave) * 2048;
+  const __attribute__((address_space(4))) uint64_t *in =
+      (const __attribute__((address_space(4))) uint64_t *)(uintptr_t)(a.in + size_t(b) * a.K);
+  const uint32_t o = uint32_t(col + (lane >> 1) * 64 + (lane & 1) * 16);
+  const uint32_t rot = __builtin_amdgcn_readfirstlane((blockIdx.x * 4 + wave) % a.K);
+  const __attribute__((address_space(4))) uint64_t *outp =
+      (const __attribute__((address_space(4))) uint64_t *)(uintptr_t)(a.out + size_t(b) * 3);
+  u32x4 acc = {0, 0, 0, 0}, c0, c1, n0, n1;
+  uint32_t idx = rot;
+  ld<0>(c0, in[idx], o); ld<0>(c1, in[idx], o + 32);
+  for (uint32_t i = 0; i < a.K; ++i) {
+    uint32_t n = idx + 1 == a.K ? 0 : idx + 1;
+    ld<0>(n0, in[n], o); ld<0>(n1, in[n], o + 32);
+    wt<2>(c0); wt<2>(c1);
+    acc ^= c0 ^ c1;
+    c0 = n0; c1 = n1; idx = n;
+    if (SPREAD && i % 5 == 4) {
+      const uint32_t q = i / 5;  // 0..5
+      uint8_t *dst = (uint8_t *)outp[q / 2];
+      const uint32_t so = o + (q & 1) * 32;
+      if (SNT) __builtin_nontemporal_store(acc, (u32x4 *)(dst + so));
+      else *(u32x4 *)(dst + so) = acc;
+    }
+  }
+  wt<0>(c0); wt<0>(c1);
+  if (!SPREAD) {
+    for (int q = 0; q < 6; ++q) {
+      uint8_t *dst = (uint8_t *)outp[q / 2];
+      const uint32_t so = o + (q & 1) * 32;
+      if (SNT) __builtin_nontemporal_store(acc, (u32x4 *)(dst + so));
+      else *(u32x4 *)(dst + so) = acc;
+    }
+  }
+}
+
 __global__ void copy_kernel(const u32x4 *__restrict__ s, u32x4 *__restrict__ d, size_t n) {
   size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x;
   const size_t stride = size_t(gridDim.x) * blockDim.x;
@@ -225,14 +268,18 @@ __global__ void read_kernel(const u32x4 *__restrict__ s, u32x4 *__restrict__ d, 
 int main(int argc, char **argv) {
   const uint32_t K = 30, B = 4;
   const uint64_t S = 32ull << 20;
+  // shard stride: S + pad (argv[1] bytes) -- tests DRAM channel/bank aliasing
+  const uint64_t pad = argc > 1 ? strtoull(argv[1], nullptr, 0) : 0;
+  const uint64_t stride = S + pad;
   uint8_t *data, *par;
-  CHECK(hipMalloc(&data, S * K * B));
-  CHECK(hipMalloc(&par, S * 3 * B));
-  CHECK(hipMemset(data, 0x5a, S * K * B));
+  CHECK(hipMalloc(&data, stride * K * B));
+  CHECK(hipMalloc(&par, stride * 3 * B));
+  CHECK(hipMemset(data, 0x5a, stride * K * B));
   std::vector<const uint8_t *> hin(K * B);
   std::vector<uint8_t *> hout(3 * B);
-  for (uint32_t i = 0; i < K * B; ++i) hin[i] = data + S * i;
-  for (uint32_t i = 0; i < 3 * B; ++i) hout[i] = par + S * i;
+  for (uint32_t i = 0; i < K * B; ++i) hin[i] = data + stride * i;
+  for (uint32_t i = 0; i < 3 * B; ++i) hout[i] = par + stride * i;
+  printf("{\"pad\": %llu}\n", (unsigned long long)pad);
   const uint8_t **din;
   uint8_t **dout;
   CHECK(hipMalloc(&din, sizeof(void *) * K * B));
@@ -276,6 +323,15 @@ int main(int argc, char **argv) {
 #define P3(R, SS, SNT)                                                                        \
   time("p3_rot" #R "_store" #SS "_snt" #SNT,                                                   \
        [&] { hipLaunchKernelGGL((probe3<R, SS, SNT>), dim3(tiles * B), dim3(256), 0, 0, a, tiles); }, bytes)
+#define P4(SNT, SP)                                                                           \
+  time("p4_snt" #SNT "_spread" #SP,                                                            \
+       [&] { hipLaunchKernelGGL((probe4<SNT, SP>), dim3(tiles * B), dim3(256), 0, 0, a, tiles); }, bytes)
+  for (int rep = 0; rep < 2; ++rep) {
+    P3(0, 0, 1); P3(1, 0, 1);
+    P2(1, 1, 0);
+    P4(1, 0); P4(1, 1); P4(0, 0); P4(0, 1);
+  }
+  if (getenv("MB_SHORT")) return 0;
   for (int rep = 0; rep < 2; ++rep) {
     P3(0, 0, 0); P3(0, 0, 1); P3(0, 1, 0); P3(0, 1, 1);
     P3(1, 0, 0); P3(1, 0, 1); P3(1, 1, 0); P3(1, 1, 1);
