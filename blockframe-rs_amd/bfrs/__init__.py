@@ -52,6 +52,8 @@ EXPORTS = (
     "bfrs_encode_batch_dev", "bfrs_decode_batch_dev", "bfrs_encode_host_batch",
     "bfrs_decode_host_batch", "bfrs_generate_parity",
     "bfrs_generate_parity_segmented", "bfrs_recover_segment_rs13", "bfrs_recover_segment_rs30_3",
+    "bfrs_blake3_hex", "bfrs_merkle_root_hex", "bfrs_manifest_check", "bfrs_commit", "bfrs_repair", "bfrs_archive_open",
+    "bfrs_archive_size", "bfrs_archive_read", "bfrs_archive_stats_get", "bfrs_archive_close",
 )
 
 SIZE_MAX = ctypes.c_size_t(-1).value
@@ -64,6 +66,25 @@ class BfrsError(RuntimeError):
 
 
 _lib: Optional[ctypes.CDLL] = None
+
+
+class RepairReport(ctypes.Structure):
+    """bfrs_repair_report (include/bfrs.h)."""
+    _fields_ = [(n, ctypes.c_uint64) for n in ("blocks_checked", "segments_checked",
+                                               "segments_repaired", "parity_repaired",
+                                               "unrecoverable_blocks")]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+class ArchiveStats(ctypes.Structure):
+    """bfrs_archive_stats (include/bfrs.h)."""
+    _fields_ = [(n, ctypes.c_uint64) for n in ("hits", "misses", "verified", "recoveries",
+                                               "recovered_segments", "bytes_served")]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
 
 _vp = ctypes.c_void_p
 _sz = ctypes.c_size_t
@@ -121,6 +142,21 @@ def lib() -> ctypes.CDLL:
             "bfrs_recover_segment_rs30_3": ([_vp, _pp, ctypes.POINTER(_sz), _sz, _pp,
                                              ctypes.POINTER(_sz), _sz, _sz, _vp,
                                              ctypes.POINTER(_sz)], ctypes.c_int),
+            "bfrs_blake3_hex": ([_vp, _sz, ctypes.c_int, ctypes.c_char_p], ctypes.c_int),
+            "bfrs_merkle_root_hex": ([ctypes.c_char_p, _sz, ctypes.c_char_p], ctypes.c_int),
+            "bfrs_manifest_check": ([ctypes.c_char_p, _sz, ctypes.POINTER(ctypes.c_int),
+                                     ctypes.c_char_p, _sz, ctypes.POINTER(_sz)], ctypes.c_int),
+            "bfrs_commit": ([_vp, ctypes.c_char_p, ctypes.c_char_p, _sz, ctypes.c_int,
+                             ctypes.c_char_p, _sz],
+                            ctypes.c_int),
+            "bfrs_repair": ([_vp, ctypes.c_char_p, ctypes.POINTER(RepairReport)], ctypes.c_int),
+            "bfrs_archive_open": ([_vp, ctypes.c_char_p, _sz, ctypes.c_int, ctypes.POINTER(_vp)],
+                                  ctypes.c_int),
+            "bfrs_archive_size": ([_vp, ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
+            "bfrs_archive_read": ([_vp, ctypes.c_uint64, _sz, _vp, ctypes.POINTER(_sz)],
+                                  ctypes.c_int),
+            "bfrs_archive_stats_get": ([_vp, ctypes.POINTER(ArchiveStats)], ctypes.c_int),
+            "bfrs_archive_close": ([_vp], None),
         }
         for name, (args, res) in sig.items():
             f = getattr(L, name)
@@ -464,3 +500,110 @@ def recover_segment_rs30_3(ctx: Context, valid_segments, block_parity, target_in
                                              len(par), target_index, out.ctypes.data,
                                              ctypes.byref(olen)))
     return out[:olen.value].tobytes()
+
+
+# ---- integrity helpers + archive pipeline (src/utils.rs, src/merkle_tree,
+# src/chunker/commit.rs, src/filestore/health.rs, src/mount) ----------------
+
+def blake3_hex(data, threads: int = 1) -> str:
+    """blake3_hash_bytes (src/utils.rs:22-28)."""
+    a = _as_np(data)
+    out = ctypes.create_string_buffer(65)
+    _check(lib().bfrs_blake3_hex(a.ctypes.data if a.size else None, a.size, threads, out))
+    return out.value.decode()
+
+
+def merkle_root_hex(leaves) -> str:
+    """MerkleTree::from_hashes(leaves).get_root() (src/merkle_tree/mod.rs:56-100)."""
+    leaves = list(leaves)
+    if any(len(h) != 64 for h in leaves):
+        raise ValueError("leaves must be 64-char hex digests")
+    out = ctypes.create_string_buffer(65)
+    _check(lib().bfrs_merkle_root_hex("".join(leaves).encode(), len(leaves), out))
+    return out.value.decode()
+
+
+def manifest_check(text) -> tuple:
+    """ManifestFile::new + validate (src/merkle_tree/manifest.rs:47-88).
+    Returns (valid, canonical_json)."""
+    raw = text.encode() if isinstance(text, str) else bytes(text)
+    valid, need = ctypes.c_int(), _sz()
+    _check(lib().bfrs_manifest_check(raw, len(raw), ctypes.byref(valid), None, 0,
+                                     ctypes.byref(need)))
+    out = ctypes.create_string_buffer(need.value)
+    _check(lib().bfrs_manifest_check(raw, len(raw), ctypes.byref(valid), out, len(out),
+                                     ctypes.byref(need)))
+    return bool(valid.value), out.value.decode()
+
+
+def commit(ctx: Context, file_path: str, archive_root: str, segment_size: int = 0,
+           tier: int = 0) -> str:
+    """Chunker::commit (src/chunker/commit.rs:593-613); tier 1/2/3 forces
+    commit_tiny/commit_segmented/commit_blocked.  Returns the archive directory."""
+    out = ctypes.create_string_buffer(4096)
+    _check(lib().bfrs_commit(ctx.handle, os.fsencode(file_path), os.fsencode(archive_root),
+                             segment_size, tier, out, len(out)))
+    return out.value.decode()
+
+
+def repair(ctx: Context, archive_dir: str) -> dict:
+    """FileStore::repair (src/filestore/health.rs:470-495), intended semantics."""
+    rep = RepairReport()
+    _check(lib().bfrs_repair(ctx.handle, os.fsencode(archive_dir), ctypes.byref(rep)))
+    return rep.as_dict()
+
+
+class Archive:
+    """Read-path core of the FUSE mount (src/mount/filesystem_unix.rs:176-305):
+    offset reads through an LRU segment cache with BLAKE3 verification and GPU
+    reconstruction of corrupt/missing segments."""
+
+    def __init__(self, ctx: Context, archive_dir: str, cache_segments: int = 64,
+                 write_back: bool = False):
+        self.ctx = ctx
+        h = _vp()
+        _check(lib().bfrs_archive_open(ctx.handle, os.fsencode(archive_dir), cache_segments,
+                                       1 if write_back else 0, ctypes.byref(h)))
+        self.handle = h.value
+
+    @property
+    def size(self) -> int:
+        n = ctypes.c_uint64()
+        _check(lib().bfrs_archive_size(self.handle, ctypes.byref(n)))
+        return n.value
+
+    def read_into(self, offset: int, out) -> int:
+        import numpy as np
+        a = out if isinstance(out, np.ndarray) else np.frombuffer(out, dtype=np.uint8)
+        n = _sz()
+        _check(lib().bfrs_archive_read(self.handle, offset, a.size,
+                                       a.ctypes.data if a.size else None, ctypes.byref(n)))
+        return n.value
+
+    def read(self, offset: int, size: int) -> bytes:
+        import numpy as np
+        buf = np.empty(max(1, size), dtype=np.uint8)
+        n = self.read_into(offset, buf[:size])
+        return buf[:n].tobytes()
+
+    def stats(self) -> dict:
+        st = ArchiveStats()
+        _check(lib().bfrs_archive_stats_get(self.handle, ctypes.byref(st)))
+        return st.as_dict()
+
+    def close(self) -> None:
+        if self.handle:
+            lib().bfrs_archive_close(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

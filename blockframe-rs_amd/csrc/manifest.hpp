@@ -1,0 +1,85 @@
+// manifest.hpp — BlockFrame manifest.json (src/merkle_tree/manifest.rs:12-53,
+// written by src/chunker/io.rs:126-202).
+//
+// The reference serialises with serde_json's json! macro, whose object map is
+// a BTreeMap (no "preserve_order" feature, Cargo.toml:22): keys come out
+// sorted, compact (to_string).  Json below keeps objects in std::map for the
+// same ordering, so manifests written here have the reference's byte layout
+// (only time_of_creation differs).
+#pragma once
+
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+namespace bfrs {
+
+struct Json {
+  enum Kind { kNull, kBool, kInt, kString, kArray, kObject } kind = kNull;
+  bool b = false;
+  int64_t i = 0;
+  std::string s;
+  std::vector<Json> a;
+  std::map<std::string, Json> o;
+
+  static Json str(std::string v) {
+    Json j;
+    j.kind = kString;
+    j.s = std::move(v);
+    return j;
+  }
+  static Json num(int64_t v) {
+    Json j;
+    j.kind = kInt;
+    j.i = v;
+    return j;
+  }
+  static Json arr() {
+    Json j;
+    j.kind = kArray;
+    return j;
+  }
+  static Json obj() {
+    Json j;
+    j.kind = kObject;
+    return j;
+  }
+  Json &operator[](const std::string &k) { return o[k]; }
+  const Json *get(const std::string &k) const {
+    auto it = o.find(k);
+    return it == o.end() ? nullptr : &it->second;
+  }
+  std::string dump() const;                       // compact, sorted keys
+  static bool parse(const std::string &text, Json *out, std::string *err);
+};
+
+// Typed view of the fields the RS path needs.
+struct BlockHashes {
+  std::vector<std::string> segments, parity;
+};
+struct SegmentHashes {
+  std::string data;
+  std::vector<std::string> parity;
+};
+struct Manifest {
+  std::string original_hash, name, time_of_creation, root;
+  int64_t size = 0;
+  int tier = 0;
+  uint64_t segment_size = 0;
+  int data_shards = 0, parity_shards = 0;
+  std::map<int64_t, std::string> leaves;           // tier 1
+  std::map<int64_t, SegmentHashes> segments;       // tier 2
+  std::map<int64_t, BlockHashes> blocks;           // tier 3
+
+  // tier 1 writes merkle_tree = {leaves, root} (MerkleTree::get_json,
+  // src/merkle_tree/mod.rs:240-251); tiers 2/3 the full MerkleTreeStructure.
+  std::string to_json() const;
+  static bool from_json(const std::string &text, Manifest *m, std::string *err);
+};
+
+// chrono's DateTime<Utc> Display, e.g. "2026-10-15 22:07:01.123456789 UTC".
+std::string utc_now_string();
+
+}  // namespace bfrs

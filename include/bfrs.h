@@ -185,6 +185,67 @@ int bfrs_recover_segment_rs30_3(bfrs_ctx *ctx, const uint8_t *const *segments,
                                 size_t n_parity, size_t target_index, uint8_t *out,
                                 size_t *out_len);
 
+/* ---- Integrity helpers (host) -------------------------------------------- */
+/* blake3_hash_bytes (src/utils.rs:22-28): lowercase hex digest + NUL into
+ * out65.  threads > 1 hashes independent chunk subtrees in parallel. */
+int bfrs_blake3_hex(const uint8_t *data, size_t len, int threads, char *out65);
+/* MerkleTree::from_hashes(..).get_root (src/merkle_tree/mod.rs:56-100):
+ * `leaves` is n concatenated 64-char hex digests (no separators). */
+int bfrs_merkle_root_hex(const char *leaves, size_t n, char *out65);
+
+/* ManifestFile::new + validate (src/merkle_tree/manifest.rs:47-88): parses
+ * manifest.json text (BFRS_E_WRAPPER + message on a parse error), sets
+ * *valid, and writes the canonical serialisation this library writes (the
+ * reference's serde_json layout: compact, keys sorted) into canonical/cap;
+ * *needed = its length + 1. */
+int bfrs_manifest_check(const char *text, size_t len, int *valid, char *canonical, size_t cap,
+                        size_t *needed);
+
+/* ---- Archive pipeline (host, arithmetic on the GPU) ----------------------- */
+/* Chunker::commit (src/chunker/commit.rs:593-613): writes
+ * {archive_root}/{basename}_{blake3}/ with the reference's layout and
+ * manifest.json.  tier 0 picks the tier by size like commit (:596-608);
+ * 1/2/3 call commit_tiny (:25) / commit_segmented (:124) / commit_blocked
+ * (:314) directly.  segment_size 0 = 32 MiB (src/utils.rs:68).  The archive
+ * directory is written to out_dir (NUL-terminated, truncated to out_cap). */
+int bfrs_commit(bfrs_ctx *ctx, const char *file_path, const char *archive_root,
+                size_t segment_size, int tier, char *out_dir, size_t out_cap);
+
+typedef struct {
+  uint64_t blocks_checked;      /* tier 3: blocks; tiers 1/2: segments */
+  uint64_t segments_checked;
+  uint64_t segments_repaired;   /* missing or BLAKE3-mismatched, restored + written */
+  uint64_t parity_repaired;     /* tier 3: parity shards re-encoded + written */
+  uint64_t unrecoverable_blocks;
+} bfrs_repair_report;
+/* FileStore::repair (src/filestore/health.rs:470-495 -> repair_tiny :497,
+ * repair_segment :542, repair_blocked :642), with the intended semantics:
+ * every missing or corrupt segment of a block is restored by one RS(k,3)
+ * decode and written to its own in-block index; corrupt parity is
+ * re-encoded.  Blocks with more damage than valid parity are counted, not
+ * errors. */
+int bfrs_repair(bfrs_ctx *ctx, const char *archive_dir, bfrs_repair_report *report);
+
+/* Read-path core of the FUSE mount (src/mount/filesystem_unix.rs:176-305,
+ * src/mount/cache.rs): offset->segment mapping, LRU segment cache,
+ * BLAKE3 verification on every miss and GPU reconstruction of a corrupt or
+ * missing segment (tier 3: RS(k,3) block decode). */
+typedef struct bfrs_archive bfrs_archive;
+typedef struct {
+  uint64_t hits, misses;
+  uint64_t verified;            /* misses served from a segment that hashed clean */
+  uint64_t recoveries;          /* decode calls */
+  uint64_t recovered_segments;  /* segments restored by those calls */
+  uint64_t bytes_served;
+} bfrs_archive_stats;
+int bfrs_archive_open(bfrs_ctx *ctx, const char *archive_dir, size_t cache_segments,
+                      int write_back, bfrs_archive **out);
+int bfrs_archive_size(bfrs_archive *a, uint64_t *size);
+/* Reads up to len bytes at offset (clamped at EOF; *nread = bytes copied). */
+int bfrs_archive_read(bfrs_archive *a, uint64_t offset, size_t len, uint8_t *out, size_t *nread);
+int bfrs_archive_stats_get(bfrs_archive *a, bfrs_archive_stats *out);
+void bfrs_archive_close(bfrs_archive *a);
+
 #ifdef __cplusplus
 }
 #endif

@@ -22,6 +22,11 @@ if [ "${SKIP_TESTS:-0}" != 1 ]; then
   rc=$?; echo "smoke rc=$rc"; tail -3 "$OUT/smoke_$TAG.log"; stop_if_crash $rc smoke
 fi
 
+if [ "${READPATH:-0}" = 1 ]; then
+  timeout -k 10 600 python tools/read_path_bench.py ${READPATH_ARGS:-} > "$OUT/readpath_$TAG.log" 2>&1
+  rc=$?; echo "readpath rc=$rc"; tail -3 "$OUT/readpath_$TAG.log"; stop_if_crash $rc readpath
+fi
+
 timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > "$OUT/bench_$TAG.log" 2>&1
 rc=$?; echo "bench rc=$rc"; tail -3 "$OUT/bench_$TAG.log"; [ $rc -eq 0 ] || exit $rc
 

@@ -1,0 +1,303 @@
+"""GPU tests of the archive pipeline in libbfrs.so: commit (tiers 1-3),
+repair and the FUSE read-path core, checked against the oracle.
+
+Layout/manifest follow the reference (src/chunker/commit.rs:25-536,
+src/chunker/io.rs:126-202); parity files must equal the oracle's RS(k,3) of
+the same (zero-padded) segments; repair and read follow the intended
+semantics (every missing/corrupt segment restored to its own
+index, offsets mapped with %, tier-3 recovery is RS(k,3)).
+"""
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SEG = 256 * 1024  # small segment size so tier-3 geometry fits a test
+
+
+def _write(path, data):
+    with open(path, "wb") as f:
+        f.write(data.tobytes())
+
+
+def _read(path):
+    with open(path, "rb") as f:
+        return np.frombuffer(f.read(), np.uint8)
+
+
+def _file(tmp_path, n, seed=0, name="input.bin"):
+    d = np.random.default_rng(seed).integers(0, 256, size=n, dtype=np.uint8)
+    p = tmp_path / name
+    _write(p, d)
+    return str(p), d
+
+
+def _manifest(adir):
+    text = open(os.path.join(adir, "manifest.json")).read()
+    obj = json.loads(text)
+    # serde_json (BTreeMap) layout: compact, keys sorted
+    assert text == json.dumps(obj, sort_keys=True, separators=(",", ":"))
+    assert re.fullmatch(r"\d{4}-\d{2}-\d{2} \d{2}:\d{2}:\d{2}(\.\d{3}|\.\d{6}|\.\d{9})? UTC", obj["time_of_creation"])
+    return obj
+
+
+def _pad(a, n):
+    out = np.zeros(n, np.uint8)
+    out[:a.size] = a
+    return out
+
+
+def _flip(path, at=0):
+    d = bytearray(open(path, "rb").read())
+    d[at % len(d)] ^= 0x5A
+    open(path, "wb").write(bytes(d))
+
+
+# ---------------------------------------------------------------- commit
+def test_commit_tier1_layout_and_parity(ctx, bfrs, oracle, tmp_path):
+    path, d = _file(tmp_path, 100_003)
+    adir = bfrs.commit(ctx, path, str(tmp_path / "archive"))
+    h = oracle.blake3_hex(d)
+    assert os.path.basename(adir) == f"input.bin_{h}"
+    assert np.array_equal(_read(os.path.join(adir, "data.dat")), d)
+    padded = (d.size + 63) // 64 * 64
+    want = oracle.encode([_pad(d, padded)], 3, oracle.ENGINE_AVX2)
+    leaves = [h]
+    for p in range(3):
+        got = _read(os.path.join(adir, f"parity_{p}.dat"))
+        assert np.array_equal(got, want[p])
+        leaves.append(oracle.blake3_hex(got))
+    m = _manifest(adir)
+    assert m["tier"] == 1 and m["size"] == d.size and m["segment_size"] == padded
+    assert m["erasure_coding"] == {"type": "reed-solomon", "data_shards": 6, "parity_shards": 3}
+    assert m["merkle_tree"] == {"leaves": {str(i): x for i, x in enumerate(leaves)},
+                                "root": oracle.merkle_root_hex(leaves)}
+    assert m["original_hash"] == h and m["name"] == "input.bin"
+
+
+def test_commit_tier2_layout_and_parity(ctx, bfrs, oracle, tmp_path):
+    n = 5 * SEG + 1000
+    path, d = _file(tmp_path, n, seed=2)
+    adir = bfrs.commit(ctx, path, str(tmp_path / "archive"), segment_size=SEG, tier=2)
+    m = _manifest(adir)
+    assert m["tier"] == 2 and m["segment_size"] == SEG
+    assert m["erasure_coding"]["data_shards"] == 6
+    seg_roots = []
+    for i in range(6):
+        seg = d[i * SEG:(i + 1) * SEG]
+        assert np.array_equal(_read(os.path.join(adir, "segments", f"segment_{i}.dat")), seg)
+        padded = (seg.size + 63) // 64 * 64
+        want = oracle.encode([_pad(seg, padded)], 3, oracle.ENGINE_AVX2)
+        ph = []
+        for p in range(3):
+            got = _read(os.path.join(adir, "parity", f"segment_{i}_parity_{p}.dat"))
+            assert np.array_equal(got, want[p]), (i, p)
+            ph.append(oracle.blake3_hex(got))
+        e = m["merkle_tree"]["segments"][str(i)]
+        assert e == {"data": oracle.blake3_hex(seg), "parity": ph}
+        seg_roots.append(oracle.merkle_root_hex([e["data"]] + ph))
+    assert m["merkle_tree"]["root"] == oracle.merkle_root_hex(seg_roots)
+    assert m["merkle_tree"]["blocks"] == {} and m["merkle_tree"]["leaves"] == {}
+
+
+def _tier3(ctx, bfrs, tmp_path, nseg_full=61, tail=1000, seed=3):
+    n = nseg_full * SEG + tail
+    path, d = _file(tmp_path, n, seed=seed)
+    adir = bfrs.commit(ctx, path, str(tmp_path / "archive"), segment_size=SEG, tier=3)
+    return adir, d
+
+
+def _segments(d):
+    return [d[i:i + SEG] for i in range(0, d.size, SEG)]
+
+
+def test_commit_tier3_layout_and_parity(ctx, bfrs, oracle, tmp_path):
+    # 61 full segments + a 1000-byte tail: blocks of 30, 30 and 2 (the last
+    # block's shards are zero-padded to its longest segment, generate.rs:75-82)
+    adir, d = _tier3(ctx, bfrs, tmp_path)
+    m = _manifest(adir)
+    assert m["tier"] == 3 and m["erasure_coding"]["data_shards"] == 30
+    segs = _segments(d)
+    blocks = [segs[i:i + 30] for i in range(0, len(segs), 30)]
+    assert sorted(m["merkle_tree"]["blocks"], key=int) == [str(b) for b in range(len(blocks))]
+    roots = []
+    for b, blk in enumerate(blocks):
+        shard = blk[0].size
+        want = oracle.encode([_pad(s, shard) for s in blk], 3, oracle.ENGINE_AVX2)
+        e = m["merkle_tree"]["blocks"][str(b)]
+        for s, seg in enumerate(blk):
+            got = _read(os.path.join(adir, "blocks", f"block_{b}", "segments", f"segment_{s}.dat"))
+            assert np.array_equal(got, seg)
+            assert e["segments"][s] == oracle.blake3_hex(seg)
+        for p in range(3):
+            got = _read(os.path.join(adir, "blocks", f"block_{b}", "parity", f"block_parity_{p}.dat"))
+            assert np.array_equal(got, want[p]), (b, p)
+            assert e["parity"][p] == oracle.blake3_hex(got)
+        roots.append(oracle.merkle_root_hex(e["segments"] + e["parity"]))
+    assert m["merkle_tree"]["root"] == oracle.merkle_root_hex(roots)
+    assert m["original_hash"] == oracle.blake3_hex(d)
+    assert os.path.basename(adir) == f"input.bin_{oracle.blake3_hex(d)}"
+
+
+def test_commit_tier3_single_segment_last_block(ctx, bfrs, oracle, tmp_path):
+    # last block holds one short segment: RS(1,3) over its own length
+    adir, d = _tier3(ctx, bfrs, tmp_path, nseg_full=30, tail=1000, seed=4)
+    got = _read(os.path.join(adir, "blocks", "block_1", "parity", "block_parity_0.dat"))
+    assert np.array_equal(got, oracle.encode([d[30 * SEG:]], 3, oracle.ENGINE_AVX2)[0])
+
+
+def test_commit_auto_tier_and_overwrite(ctx, bfrs, tmp_path):
+    path, d = _file(tmp_path, 4096, seed=5)
+    a1 = bfrs.commit(ctx, path, str(tmp_path / "archive"))
+    _flip(os.path.join(a1, "parity_1.dat"))
+    a2 = bfrs.commit(ctx, path, str(tmp_path / "archive"))  # duplicate commit overwrites
+    assert a1 == a2 and _manifest(a2)["tier"] == 1
+    assert bfrs.repair(ctx, a2)["segments_repaired"] == 0
+
+
+def test_commit_errors(ctx, bfrs, tmp_path):
+    empty = tmp_path / "empty.bin"
+    empty.write_bytes(b"")
+    with pytest.raises(bfrs.BfrsError, match="empty file"):
+        bfrs.commit(ctx, str(empty), str(tmp_path / "a"))
+    with pytest.raises(bfrs.BfrsError):
+        bfrs.commit(ctx, str(tmp_path / "missing.bin"), str(tmp_path / "a"))
+    path, _ = _file(tmp_path, 100)
+    with pytest.raises(bfrs.BfrsError):
+        bfrs.commit(ctx, path, str(tmp_path / "a"), tier=7)
+
+
+# ---------------------------------------------------------------- repair
+def test_repair_tier3_corrupt_missing_and_parity(ctx, bfrs, tmp_path):
+    adir, d = _tier3(ctx, bfrs, tmp_path)
+    segs = _segments(d)
+    b0 = os.path.join(adir, "blocks", "block_0")
+    b1 = os.path.join(adir, "blocks", "block_1")
+    b2 = os.path.join(adir, "blocks", "block_2")
+    _flip(os.path.join(b0, "segments", "segment_3.dat"), 77)   # corrupt
+    _flip(os.path.join(b0, "segments", "segment_29.dat"), 5)   # corrupt
+    os.remove(os.path.join(b0, "segments", "segment_17.dat"))  # missing
+    os.remove(os.path.join(b1, "segments", "segment_0.dat"))
+    _flip(os.path.join(b1, "parity", "block_parity_2.dat"))    # corrupt parity
+    os.remove(os.path.join(b2, "segments", "segment_1.dat"))   # the short tail segment
+    rep = bfrs.repair(ctx, adir)
+    assert rep == {"blocks_checked": 3, "segments_checked": 62, "segments_repaired": 5,
+                   "parity_repaired": 1, "unrecoverable_blocks": 0}
+    for b, s in [(0, 3), (0, 29), (0, 17), (1, 0), (2, 1)]:
+        got = _read(os.path.join(adir, "blocks", f"block_{b}", "segments", f"segment_{s}.dat"))
+        assert np.array_equal(got, segs[30 * b + s]), (b, s)
+    assert bfrs.repair(ctx, adir) == {"blocks_checked": 3, "segments_checked": 62,
+                                      "segments_repaired": 0, "parity_repaired": 0,
+                                      "unrecoverable_blocks": 0}
+
+
+def test_repair_tier3_unrecoverable_block_is_counted(ctx, bfrs, tmp_path):
+    adir, d = _tier3(ctx, bfrs, tmp_path)
+    b0 = os.path.join(adir, "blocks", "block_0")
+    for s in (1, 2, 3):
+        os.remove(os.path.join(b0, "segments", f"segment_{s}.dat"))
+    _flip(os.path.join(b0, "parity", "block_parity_0.dat"))  # 3 erasures, 2 valid parity
+    _flip(os.path.join(adir, "blocks", "block_1", "segments", "segment_9.dat"))
+    rep = bfrs.repair(ctx, adir)
+    assert rep["unrecoverable_blocks"] == 1 and rep["segments_repaired"] == 1
+    assert np.array_equal(
+        _read(os.path.join(adir, "blocks", "block_1", "segments", "segment_9.dat")),
+        _segments(d)[39])
+
+
+def test_repair_tier2_and_tier1(ctx, bfrs, tmp_path):
+    path, d = _file(tmp_path, 3 * SEG + 10, seed=8, name="t2.bin")
+    a2 = bfrs.commit(ctx, path, str(tmp_path / "archive"), segment_size=SEG, tier=2)
+    os.remove(os.path.join(a2, "segments", "segment_1.dat"))
+    _flip(os.path.join(a2, "segments", "segment_3.dat"))  # the 10-byte tail
+    _flip(os.path.join(a2, "parity", "segment_3_parity_0.dat"))
+    rep = bfrs.repair(ctx, a2)
+    assert rep["segments_repaired"] == 2 and rep["unrecoverable_blocks"] == 0
+    assert np.array_equal(_read(os.path.join(a2, "segments", "segment_1.dat")), d[SEG:2 * SEG])
+    assert np.array_equal(_read(os.path.join(a2, "segments", "segment_3.dat")), d[3 * SEG:])
+
+    path, d = _file(tmp_path, 777, seed=9, name="t1.bin")
+    a1 = bfrs.commit(ctx, path, str(tmp_path / "archive"))
+    os.remove(os.path.join(a1, "data.dat"))
+    os.remove(os.path.join(a1, "parity_0.dat"))
+    rep = bfrs.repair(ctx, a1)
+    assert rep["segments_repaired"] == 1
+    assert np.array_equal(_read(os.path.join(a1, "data.dat")), d)
+
+
+# ---------------------------------------------------------------- read path (FUSE core)
+def test_archive_read_clean_and_boundaries(ctx, bfrs, tmp_path):
+    adir, d = _tier3(ctx, bfrs, tmp_path)
+    with bfrs.Archive(ctx, adir, cache_segments=8) as a:
+        assert a.size == d.size
+        rng = np.random.default_rng(1)
+        for _ in range(40):
+            off = int(rng.integers(0, d.size))
+            ln = int(rng.integers(1, 3 * SEG))
+            assert a.read(off, ln) == d[off:off + ln].tobytes()
+        assert a.read(SEG - 3, 6) == d[SEG - 3:SEG + 3].tobytes()  # spans two segments
+        assert a.read(d.size - 10, 100) == d[-10:].tobytes()        # short read at EOF
+        assert a.read(d.size, 10) == b""
+        st = a.stats()
+        assert st["recoveries"] == 0 and st["hits"] > 0 and st["verified"] == st["misses"]
+
+
+def test_archive_read_reconstructs_corrupt_segments(ctx, bfrs, tmp_path):
+    adir, d = _tier3(ctx, bfrs, tmp_path)
+    b0 = os.path.join(adir, "blocks", "block_0", "segments")
+    _flip(os.path.join(b0, "segment_4.dat"), 100)
+    os.remove(os.path.join(b0, "segment_5.dat"))
+    _flip(os.path.join(adir, "blocks", "block_2", "segments", "segment_1.dat"))
+    with bfrs.Archive(ctx, adir, cache_segments=64, write_back=False) as a:
+        out = np.empty(d.size, np.uint8)
+        step = 1_000_003
+        for off in range(0, d.size, step):
+            assert a.read_into(off, out[off:off + step]) == min(step, d.size - off)
+        assert np.array_equal(out, d)
+        st = a.stats()
+        assert st["recoveries"] == 2 and st["recovered_segments"] == 3
+    assert not os.path.exists(os.path.join(b0, "segment_5.dat"))  # read-only mount
+    with bfrs.Archive(ctx, adir, cache_segments=2, write_back=True) as a:
+        assert a.read(4 * SEG, 2 * SEG) == d[4 * SEG:6 * SEG].tobytes()
+    assert np.array_equal(_read(os.path.join(b0, "segment_5.dat")), d[5 * SEG:6 * SEG])
+    assert np.array_equal(_read(os.path.join(b0, "segment_4.dat")), d[4 * SEG:5 * SEG])
+
+
+def test_archive_read_unrecoverable_raises(ctx, bfrs, tmp_path):
+    adir, d = _tier3(ctx, bfrs, tmp_path)
+    b0 = os.path.join(adir, "blocks", "block_0")
+    for s in range(4):
+        os.remove(os.path.join(b0, "segments", f"segment_{s}.dat"))
+    with bfrs.Archive(ctx, adir) as a:
+        assert a.read(30 * SEG, 10) == d[30 * SEG:30 * SEG + 10].tobytes()
+        with pytest.raises(bfrs.BfrsError) as e:
+            a.read(0, 10)
+        assert e.value.code == bfrs.E_NOT_ENOUGH_SHARDS
+
+
+def test_archive_read_tier1_tier2(ctx, bfrs, tmp_path):
+    path, d = _file(tmp_path, 2 * SEG + 99, seed=11, name="t2.bin")
+    a2 = bfrs.commit(ctx, path, str(tmp_path / "archive"), segment_size=SEG, tier=2)
+    os.remove(os.path.join(a2, "segments", "segment_2.dat"))
+    with bfrs.Archive(ctx, a2) as a:
+        assert a.read(0, d.size) == d.tobytes()
+        assert a.stats()["recovered_segments"] == 1
+    path, d = _file(tmp_path, 5000, seed=12, name="t1.bin")
+    a1 = bfrs.commit(ctx, path, str(tmp_path / "archive"))
+    _flip(os.path.join(a1, "data.dat"))
+    with bfrs.Archive(ctx, a1) as a:
+        assert a.read(17, 4000) == d[17:4017].tobytes()
+        assert a.stats()["recoveries"] == 1
+
+
+def test_archive_open_errors(ctx, bfrs, tmp_path):
+    with pytest.raises(bfrs.BfrsError):
+        bfrs.Archive(ctx, str(tmp_path / "nope"))
+    (tmp_path / "bad").mkdir()
+    (tmp_path / "bad" / "manifest.json").write_text("{not json")
+    with pytest.raises(bfrs.BfrsError):
+        bfrs.Archive(ctx, str(tmp_path / "bad"))

@@ -1,0 +1,116 @@
+"""Host-side integrity code of libbfrs.so (no GPU): BLAKE3, Merkle root and the
+manifest format, checked against the reference's KATs, the BLAKE3 spec
+vectors and the oracle.
+
+  * blake3_hash_bytes — src/utils.rs:22-28 (KAT: src/utils.rs:17-18)
+  * MerkleTree::from_hashes / build_tree — src/merkle_tree/mod.rs:56-100
+  * manifest.json — src/chunker/io.rs:126-202 (json! -> serde_json BTreeMap:
+    compact, keys sorted) and ManifestFile::validate, src/merkle_tree/manifest.rs:55-88
+"""
+import json
+
+import numpy as np
+import pytest
+
+from test_oracle import BLAKE3_SPEC
+
+H = lambda c: c * 64  # a syntactically valid 64-hex digest
+
+
+def test_blake3_reference_kat(bfrs):
+    assert bfrs.blake3_hex(b"blockframe") == \
+        "c41e3ccb398783c24211ecea54ac84c2029d012165392c9deabbef3a597b8fb7"
+
+
+@pytest.mark.parametrize("n", sorted(BLAKE3_SPEC))
+def test_blake3_spec_vectors(bfrs, n):
+    d = (np.arange(n) % 251).astype(np.uint8)
+    assert bfrs.blake3_hex(d) == BLAKE3_SPEC[n]
+
+
+@pytest.mark.parametrize("n", [0, 1, 63, 64, 65, 1023, 1024, 1025, 2047, 2048, 2049, 3072,
+                               4097, 65536, 65537, 1 << 20, (1 << 20) + 4097])
+def test_blake3_matches_oracle(bfrs, oracle, n):
+    d = np.random.default_rng(n).integers(0, 256, size=n, dtype=np.uint8)
+    assert bfrs.blake3_hex(d) == oracle.blake3_hex(d.tobytes())
+
+
+@pytest.mark.parametrize("n", [64 * 1024 + 1, 5 * (1 << 20) + 333, 24 << 20])
+def test_blake3_threaded_subtrees(bfrs, oracle, n):
+    # the threaded split follows the BLAKE3 tree (left subtree = largest power
+    # of two chunks < n), so any thread count gives the same digest
+    d = np.random.default_rng(7).integers(0, 256, size=n, dtype=np.uint8)
+    want = oracle.blake3_hex(d.tobytes())
+    for t in (1, 2, 3, 8, 16):
+        assert bfrs.blake3_hex(d, threads=t) == want
+
+
+@pytest.mark.parametrize("n", list(range(1, 18)) + [30, 33, 64])
+def test_merkle_root_matches_oracle(bfrs, oracle, n):
+    leaves = [oracle.blake3_hex(str(i).encode()) for i in range(n)]
+    assert bfrs.merkle_root_hex(leaves) == oracle.merkle_root_hex(leaves)
+
+
+def test_merkle_rejects_bad_leaves(bfrs):
+    with pytest.raises(ValueError):
+        bfrs.merkle_root_hex(["abc"])
+    with pytest.raises(bfrs.BfrsError):
+        bfrs.merkle_root_hex([])
+
+
+def _canon(obj) -> str:
+    # serde_json::Value (BTreeMap) to_string: compact, keys in byte order
+    return json.dumps(obj, sort_keys=True, separators=(",", ":"))
+
+
+def _manifest(tier):
+    mt = {"leaves": {}, "root": H("a"), "segments": {}, "blocks": {}}
+    if tier == 1:
+        mt = {"leaves": {str(i): H("0123456789abcdef"[i]) for i in range(4)}, "root": H("a")}
+    elif tier == 2:
+        mt["segments"] = {str(i): {"data": H("b"), "parity": [H("c"), H("d"), H("e")]}
+                          for i in range(12)}
+    else:
+        mt["blocks"] = {str(b): {"segments": [H("1")] * (30 if b < 10 else 7),
+                                 "parity": [H("2"), H("3"), H("4")]} for b in range(11)}
+    return {"original_hash": H("f"), "name": "file name \"q\".bin", "size": 1234567890123,
+            "time_of_creation": "2026-01-02 03:04:05.123456789 UTC",
+            "erasure_coding": {"type": "reed-solomon", "data_shards": 30 if tier == 3 else 6,
+                               "parity_shards": 3},
+            "merkle_tree": mt, "tier": tier, "segment_size": 33554432}
+
+
+@pytest.mark.parametrize("tier", [1, 2, 3])
+def test_manifest_canonical_roundtrip(bfrs, tier):
+    obj = _manifest(tier)
+    text = _canon(obj)
+    valid, canon = bfrs.manifest_check(text)
+    assert valid
+    assert canon == text  # byte-identical to the reference's serde layout
+    # pretty-printed / unsorted input normalises to the same bytes
+    valid2, canon2 = bfrs.manifest_check(json.dumps(obj, indent=2))
+    assert valid2 and canon2 == text
+    if tier == 3:  # "10" sorts before "2" (BTreeMap<String, _>)
+        keys = list(json.loads(canon)["merkle_tree"]["blocks"])
+        assert keys[:3] == ["0", "1", "10"]
+
+
+def test_manifest_validate_rules(bfrs):
+    ok = _manifest(1)
+    assert bfrs.manifest_check(_canon(ok))[0]
+    bad_root = _manifest(1)
+    bad_root["merkle_tree"]["root"] = "xyz"
+    assert not bfrs.manifest_check(_canon(bad_root))[0]
+    gap = _manifest(1)
+    del gap["merkle_tree"]["leaves"]["1"]
+    assert not bfrs.manifest_check(_canon(gap))[0]
+    empty = _manifest(3)
+    empty["merkle_tree"]["blocks"] = {}
+    assert not bfrs.manifest_check(_canon(empty))[0]
+
+
+@pytest.mark.parametrize("text", ["", "{", "[1,2]", '{"tier": 3}', "{} x"])
+def test_manifest_parse_errors(bfrs, text):
+    with pytest.raises(bfrs.BfrsError) as e:
+        bfrs.manifest_check(text)
+    assert e.value.code == bfrs.E_WRAPPER
