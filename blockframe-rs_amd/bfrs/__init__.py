@@ -52,7 +52,7 @@ EXPORTS = (
     "bfrs_encode_batch_dev", "bfrs_decode_batch_dev", "bfrs_encode_host_batch",
     "bfrs_decode_host_batch", "bfrs_generate_parity",
     "bfrs_generate_parity_segmented", "bfrs_recover_segment_rs13", "bfrs_recover_segment_rs30_3",
-    "bfrs_blake3_hex", "bfrs_merkle_root_hex", "bfrs_manifest_check", "bfrs_commit", "bfrs_repair", "bfrs_archive_open",
+    "bfrs_blake3_hex", "bfrs_blake3_batch_dev", "bfrs_blake3_combine", "bfrs_merkle_root_hex", "bfrs_manifest_check", "bfrs_commit", "bfrs_repair", "bfrs_archive_open",
     "bfrs_archive_size", "bfrs_archive_read", "bfrs_archive_stats_get", "bfrs_archive_close",
 )
 
@@ -143,6 +143,9 @@ def lib() -> ctypes.CDLL:
                                              ctypes.POINTER(_sz), _sz, _sz, _vp,
                                              ctypes.POINTER(_sz)], ctypes.c_int),
             "bfrs_blake3_hex": ([_vp, _sz, ctypes.c_int, ctypes.c_char_p], ctypes.c_int),
+            "bfrs_blake3_batch_dev": ([_vp, _sz, _pp, ctypes.POINTER(_sz), _vp, _vp, _vp],
+                                      ctypes.c_int),
+            "bfrs_blake3_combine": ([_vp, _sz, ctypes.c_char_p], ctypes.c_int),
             "bfrs_merkle_root_hex": ([ctypes.c_char_p, _sz, ctypes.c_char_p], ctypes.c_int),
             "bfrs_manifest_check": ([ctypes.c_char_p, _sz, ctypes.POINTER(ctypes.c_int),
                                      ctypes.c_char_p, _sz, ctypes.POINTER(_sz)], ctypes.c_int),
@@ -304,6 +307,27 @@ class Context:
         def call(stream_handle=None, _keep=(ks, ko, kr, kd)):
             _check(fn(h, n, ks, recovery_count, shard_bytes, po, pr, pd, stream_handle))
         return call
+
+    def blake3_batch_dev(self, d_msgs, lens=None, stream=None, with_cvs=False):
+        """BLAKE3 of device messages (torch uint8 tensors or (address, len)
+        pairs via `lens`).  Returns hex digests, plus 32-byte subtree CVs if
+        with_cvs."""
+        import numpy as np
+        n = len(d_msgs)
+        if lens is None:
+            lens = [t.numel() for t in d_msgs]
+        pm, km = _ptr_array([self._addr(t) if l else None for t, l in zip(d_msgs, lens)])
+        ls = (_sz * max(1, n))(*lens)
+        dig = np.zeros(max(1, n) * 32, np.uint8)
+        cvs = np.zeros(max(1, n) * 32, np.uint8) if with_cvs else None
+        _check(lib().bfrs_blake3_batch_dev(self.handle, n, pm, ls, dig.ctypes.data,
+                                           cvs.ctypes.data if with_cvs else None,
+                                           _stream_handle(stream, [t for t in d_msgs
+                                                                   if not isinstance(t, int)])))
+        hexes = [dig[32 * i:32 * i + 32].tobytes().hex() for i in range(n)]
+        if with_cvs:
+            return hexes, [cvs[32 * i:32 * i + 32].tobytes() for i in range(n)]
+        return hexes
 
     # ---- host-memory batch API (host buffers: numpy arrays or CPU torch tensors)
     @staticmethod
@@ -510,6 +534,14 @@ def blake3_hex(data, threads: int = 1) -> str:
     a = _as_np(data)
     out = ctypes.create_string_buffer(65)
     _check(lib().bfrs_blake3_hex(a.ctypes.data if a.size else None, a.size, threads, out))
+    return out.value.decode()
+
+
+def blake3_combine(cvs) -> str:
+    """Digest of a message from the subtree CVs (32 bytes each) of its parts."""
+    raw = b"".join(bytes(c) for c in cvs)
+    out = ctypes.create_string_buffer(65)
+    _check(lib().bfrs_blake3_combine(raw, len(raw) // 32, out))
     return out.value.decode()
 
 

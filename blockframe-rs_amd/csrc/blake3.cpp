@@ -175,6 +175,29 @@ void blake3_hash(const uint8_t *data, size_t len, uint8_t out[32], int threads) 
   }
 }
 
+std::string blake3_combine_cvs_hex(const uint8_t *cvs, size_t n) {
+  std::vector<Words8> level(n);
+  for (size_t i = 0; i < n; ++i)
+    for (int w = 0; w < 8; ++w)
+      level[i][w] = uint32_t(cvs[32 * i + 4 * w]) | uint32_t(cvs[32 * i + 4 * w + 1]) << 8 |
+                    uint32_t(cvs[32 * i + 4 * w + 2]) << 16 | uint32_t(cvs[32 * i + 4 * w + 3]) << 24;
+  // level-wise pairing, odd last node carried: BLAKE3's left-complete tree
+  while (level.size() > 2) {
+    std::vector<Words8> next;
+    for (size_t i = 0; i + 1 < level.size(); i += 2)
+      next.push_back(parent_node(level[i], level[i + 1]).chaining());
+    if (level.size() % 2) next.push_back(level.back());
+    level.swap(next);
+  }
+  Pending root = parent_node(level[0], level[1]);
+  uint32_t o[16];
+  compress(root.cv, root.m, root.counter, root.len, root.flags | kRoot, o);
+  uint8_t d[32];
+  for (int i = 0; i < 8; ++i)
+    for (int b = 0; b < 4; ++b) d[4 * i + b] = uint8_t(o[i] >> (8 * b));
+  return to_hex(d, 32);
+}
+
 std::string to_hex(const uint8_t *d, size_t n) {
   static const char *digits = "0123456789abcdef";
   std::string s(2 * n, '0');

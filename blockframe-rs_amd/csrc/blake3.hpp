@@ -22,6 +22,12 @@ void blake3_hash(const uint8_t *data, size_t len, uint8_t out[32], int threads =
 std::string blake3_hex(const uint8_t *data, size_t len, int threads = 1);
 std::string to_hex(const uint8_t *d, size_t n);
 
+// Digest of a message from the subtree chaining values of its consecutive
+// parts (n >= 2): every part but the last holds the same power-of-two number
+// of 1 KiB chunks, so each part is one node of the message's tree (e.g. the
+// 32 MiB segments of a file).  CVs are 32 bytes each, little-endian words.
+std::string blake3_combine_cvs_hex(const uint8_t *cvs, size_t n);
+
 // src/merkle_tree/mod.rs:56-100 (from_hashes + build_tree): parents hash the
 // ASCII concatenation of the two lowercase-hex children; an odd node pairs
 // with itself.  Single leaf -> the leaf itself.

@@ -1,0 +1,159 @@
+// hash_gpu.cpp — host side of the device BLAKE3 (blake3_kernels.hip):
+// splits messages into 256 KiB groups, plans the CV reduction levels, and
+// exposes bfrs_blake3_batch_dev / bfrs_blake3_combine.
+#include <cstring>
+#include <vector>
+
+#include "blake3.hpp"
+#include "hash_kernels.hpp"
+#include "runtime.hpp"
+
+namespace bfrs {
+
+namespace {
+size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+}  // namespace
+
+int Context::blake3_dev(size_t n, const uint8_t *const *d_msgs, const size_t *lens,
+                        uint8_t *digests, uint8_t *cvs, hipStream_t s) {
+  if (n == 0) return BFRS_OK;
+  if (!d_msgs || !lens || !digests)
+    return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_blake3_batch_dev: NULL argument");
+  if (n > (1u << 30)) return set_error(BFRS_E_INVALID_ARGUMENT, "too many messages");
+  HIP_TRY(hipSetDevice(device));
+
+  // kernel-1 groups (messages in order, groups of a message contiguous)
+  std::vector<HashGroup> groups;
+  std::vector<uint32_t> g_first(n), g_count(n);
+  for (size_t i = 0; i < n; ++i) {
+    if (lens[i] && !d_msgs[i])
+      return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_blake3_batch_dev: NULL message");
+    if (reinterpret_cast<uintptr_t>(d_msgs[i]) % 16)
+      return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_blake3_batch_dev: message not 16-byte aligned");
+    const size_t ng = lens[i] == 0 ? 1 : (lens[i] + kGroupBytes - 1) / kGroupBytes;
+    g_first[i] = uint32_t(groups.size());
+    g_count[i] = uint32_t(ng);
+    for (size_t g = 0; g < ng; ++g) {
+      HashGroup h{};
+      h.addr = reinterpret_cast<uint64_t>(d_msgs[i]) + uint64_t(g) * kGroupBytes;
+      h.chunk0 = uint64_t(g) * kGroupChunks;
+      const size_t rem = lens[i] - g * size_t(kGroupBytes);
+      h.nbytes = uint32_t(lens[i] == 0 ? 0 : (rem < kGroupBytes ? rem : kGroupBytes));
+      h.msg = uint32_t(i);
+      h.single = ng == 1;
+      groups.push_back(h);
+    }
+  }
+  // reduction levels: level L's nodes of message i are cur[off[i], off[i]+cnt[i])
+  std::vector<std::vector<HashReduce>> levels;
+  std::vector<uint32_t> cnt(g_count), off(g_first);
+  for (;;) {
+    std::vector<HashReduce> jobs;
+    uint32_t next = 0;
+    bool more = false;
+    for (size_t i = 0; i < n; ++i) {
+      if (cnt[i] <= 1) continue;  // finished (or finalised by kernel 1)
+      if (cnt[i] <= kReduceFanIn) {
+        jobs.push_back({off[i], cnt[i], 0, 1, uint32_t(i), {0, 0, 0}});
+        cnt[i] = 0;
+        continue;
+      }
+      const uint32_t runs = (cnt[i] + kReduceFanIn - 1) / kReduceFanIn;
+      for (uint32_t r = 0; r < runs; ++r) {
+        const uint32_t nn = cnt[i] - r * kReduceFanIn < kReduceFanIn ? cnt[i] - r * kReduceFanIn
+                                                                      : kReduceFanIn;
+        jobs.push_back({off[i] + r * kReduceFanIn, nn, next + r, 0, uint32_t(i), {0, 0, 0}});
+      }
+      off[i] = next;
+      cnt[i] = runs;
+      next += runs;
+      more = true;
+    }
+    if (jobs.empty()) break;
+    levels.push_back(std::move(jobs));
+    if (!more) break;
+  }
+
+  // device layout: groups | jobs (all levels) | cvA | cvB | msg_cvs | digests
+  size_t njobs = 0;
+  for (auto &l : levels) njobs += l.size();
+  const size_t b_groups = align_up(groups.size() * sizeof(HashGroup), 256);
+  const size_t b_jobs = align_up(njobs * sizeof(HashReduce) + 16, 256);
+  const size_t b_cv = align_up(groups.size() * 32, 256);
+  const size_t b_out = align_up(n * 32, 256);
+  const size_t need = b_groups + b_jobs + 2 * b_cv + 2 * b_out;
+  const size_t h_need = b_groups + b_jobs + 2 * b_out;
+  if (need > d_hash_cap) {
+    if (d_hash) {
+      HIP_TRY(hipDeviceSynchronize());
+      HIP_TRY(hipFree(d_hash));
+      d_hash = nullptr;
+      d_hash_cap = 0;
+    }
+    HIP_TRY(hipMalloc(&d_hash, need));
+    d_hash_cap = need;
+  }
+  if (h_need > h_hash_cap) {
+    if (h_hash) {
+      HIP_TRY(hipDeviceSynchronize());
+      HIP_TRY(hipHostFree(h_hash));
+      h_hash = nullptr;
+      h_hash_cap = 0;
+    }
+    HIP_TRY(hipHostMalloc(&h_hash, h_need, hipHostMallocDefault));
+    h_hash_cap = h_need;
+  }
+  uint8_t *d = static_cast<uint8_t *>(d_hash);
+  uint8_t *h = static_cast<uint8_t *>(h_hash);
+  auto *d_groups = reinterpret_cast<HashGroup *>(d);
+  auto *d_jobs = reinterpret_cast<HashReduce *>(d + b_groups);
+  auto *d_cv0 = reinterpret_cast<uint32_t *>(d + b_groups + b_jobs);
+  auto *d_cv1 = reinterpret_cast<uint32_t *>(d + b_groups + b_jobs + b_cv);
+  auto *d_msg_cvs = reinterpret_cast<uint32_t *>(d + b_groups + b_jobs + 2 * b_cv);
+  auto *d_digests = reinterpret_cast<uint32_t *>(d + b_groups + b_jobs + 2 * b_cv + b_out);
+  // descriptors through pinned memory (one async copy)
+  std::memcpy(h, groups.data(), groups.size() * sizeof(HashGroup));
+  size_t jo = 0;
+  for (auto &l : levels) {
+    std::memcpy(h + b_groups + jo * sizeof(HashReduce), l.data(), l.size() * sizeof(HashReduce));
+    jo += l.size();
+  }
+  HIP_TRY(hipMemcpyAsync(d, h, b_groups + b_jobs, hipMemcpyHostToDevice, s));
+  HIP_TRY(launch_blake3_groups(d_groups, uint32_t(groups.size()), d_cv0, d_msg_cvs, d_digests, s));
+  uint32_t *cur = d_cv0, *nxt = d_cv1;
+  jo = 0;
+  for (auto &l : levels) {
+    HIP_TRY(launch_blake3_reduce(d_jobs + jo, uint32_t(l.size()), cur, nxt, d_msg_cvs, d_digests, s));
+    jo += l.size();
+    std::swap(cur, nxt);
+  }
+  uint8_t *h_digests = h + b_groups + b_jobs;
+  uint8_t *h_cvs = h_digests + b_out;
+  HIP_TRY(hipMemcpyAsync(h_digests, d_digests, n * 32, hipMemcpyDeviceToHost, s));
+  if (cvs) HIP_TRY(hipMemcpyAsync(h_cvs, d_msg_cvs, n * 32, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  std::memcpy(digests, h_digests, n * 32);
+  if (cvs) std::memcpy(cvs, h_cvs, n * 32);
+  return BFRS_OK;
+}
+
+}  // namespace bfrs
+
+extern "C" {
+
+int bfrs_blake3_batch_dev(bfrs_ctx *ctx, size_t n, const uint8_t *const *d_msgs, const size_t *lens,
+                          uint8_t *digests_out, uint8_t *cvs_out, void *hip_stream) {
+  if (!ctx) return bfrs::set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_blake3_batch_dev: NULL context");
+  return ctx->impl.blake3_dev(n, d_msgs, lens, digests_out, cvs_out,
+                              static_cast<hipStream_t>(hip_stream));
+}
+
+int bfrs_blake3_combine(const uint8_t *cvs, size_t n, char *out65) {
+  if (!cvs || !out65 || n < 2)
+    return bfrs::set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_blake3_combine: need >= 2 CVs");
+  const std::string h = bfrs::blake3_combine_cvs_hex(cvs, n);
+  std::memcpy(out65, h.c_str(), 65);
+  return BFRS_OK;
+}
+
+}  // extern "C"

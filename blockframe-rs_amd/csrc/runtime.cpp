@@ -36,11 +36,6 @@ int hip_error(hipError_t e, const char *what) {
   return set_error(BFRS_E_HIP, os.str());
 }
 
-#define HIP_TRY(expr)                                 \
-  do {                                                \
-    hipError_t e_ = (expr);                           \
-    if (e_ != hipSuccess) return hip_error(e_, #expr); \
-  } while (0)
 
 int check_shape(size_t k, size_t m, size_t shard_bytes) {
   if (shard_bytes == 0 || (shard_bytes & 1)) {
@@ -107,6 +102,8 @@ Context::~Context() {
       (void)hipStreamDestroy(ps);
     }
   if (pipe_buf) (void)hipFree(pipe_buf);
+  if (d_hash) (void)hipFree(d_hash);
+  if (h_hash) (void)hipHostFree(h_hash);
   if (stream) (void)hipStreamDestroy(stream);
 }
 

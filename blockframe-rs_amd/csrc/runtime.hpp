@@ -21,6 +21,12 @@ namespace bfrs {
 int set_error(int code, const std::string &msg);
 int hip_error(hipError_t e, const char *what);
 
+#define HIP_TRY(expr)                                   \
+  do {                                                  \
+    hipError_t e_ = (expr);                             \
+    if (e_ != hipSuccess) return bfrs::hip_error(e_, #expr); \
+  } while (0)
+
 // One kernel pass of a plan: outputs [r0, r1) x inputs [c0, c1) with its
 // nibble tables resident on the device.
 struct PlanPass {
@@ -61,8 +67,18 @@ struct Context {
   void *pipe_buf = nullptr;
   size_t pipe_cap = 0;  // bytes per slot
 
+  // BLAKE3 (hash_gpu.cpp): device work area + pinned descriptor/result area.
+  void *d_hash = nullptr;
+  size_t d_hash_cap = 0;
+  void *h_hash = nullptr;
+  size_t h_hash_cap = 0;
+
   ~Context();
   int init(int dev);
+  // BLAKE3 of n device messages; digests (and subtree CVs if cvs != NULL)
+  // land in host memory, n * 32 bytes each.  Synchronises `stream`.
+  int blake3_dev(size_t n, const uint8_t *const *d_msgs, const size_t *lens, uint8_t *digests,
+                 uint8_t *cvs, hipStream_t stream);
   int get_encode_plan(size_t k, size_t m, const Plan **out);
   int get_decode_plan(size_t k, size_t m, const std::vector<uint8_t> &orig_present,
                       const std::vector<uint8_t> &rec_present, const Plan **out);

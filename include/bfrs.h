@@ -189,6 +189,18 @@ int bfrs_recover_segment_rs30_3(bfrs_ctx *ctx, const uint8_t *const *segments,
 /* blake3_hash_bytes (src/utils.rs:22-28): lowercase hex digest + NUL into
  * out65.  threads > 1 hashes independent chunk subtrees in parallel. */
 int bfrs_blake3_hex(const uint8_t *data, size_t len, int threads, char *out65);
+/* BLAKE3 of n device-resident messages on the GPU (blake3_kernels.hip).
+ * d_msgs[i] must be 16-byte aligned (NULL allowed when lens[i] == 0).
+ * digests_out: host, n * 32 bytes.  cvs_out (may be NULL): host, n * 32
+ * bytes, each message's subtree chaining value, for bfrs_blake3_combine.
+ * Work is queued on hip_stream (NULL = HIP default) and waited for. */
+int bfrs_blake3_batch_dev(bfrs_ctx *ctx, size_t n, const uint8_t *const *d_msgs,
+                          const size_t *lens, uint8_t *digests_out, uint8_t *cvs_out,
+                          void *hip_stream);
+/* Digest of a whole message from the CVs of its n >= 2 consecutive parts,
+ * where every part but the last has the same power-of-two number of KiB (the
+ * file hash of commit.rs:478 from per-segment CVs of 32 MiB segments). */
+int bfrs_blake3_combine(const uint8_t *cvs, size_t n, char *out65);
 /* MerkleTree::from_hashes(..).get_root (src/merkle_tree/mod.rs:56-100):
  * `leaves` is n concatenated 64-char hex digests (no separators). */
 int bfrs_merkle_root_hex(const char *leaves, size_t n, char *out65);

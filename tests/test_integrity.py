@@ -114,3 +114,17 @@ def test_manifest_parse_errors(bfrs, text):
     with pytest.raises(bfrs.BfrsError) as e:
         bfrs.manifest_check(text)
     assert e.value.code == bfrs.E_WRAPPER
+
+
+@pytest.mark.parametrize("part_kib,nparts,tail", [(1, 2, 0), (2, 3, 700), (4, 5, 1), (1, 7, 1024),
+                                                  (8, 2, 5000)])
+def test_blake3_combine_from_part_cvs(bfrs, oracle, part_kib, nparts, tail):
+    # a file's digest from the subtree CVs of equal power-of-two-KiB parts
+    # (how a tier-3 file hash follows from per-segment CVs, commit.rs:478)
+    import b3py
+    P = part_kib * 1024
+    data = np.random.default_rng(P + tail).integers(0, 256, size=nparts * P + tail,
+                                                    dtype=np.uint8).tobytes()
+    parts = [data[i:i + P] for i in range(0, len(data), P)]
+    cvs = [b3py.subtree_cv(p, i * part_kib) for i, p in enumerate(parts)]
+    assert bfrs.blake3_combine(cvs) == oracle.blake3_hex(data)
