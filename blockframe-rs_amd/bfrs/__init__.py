@@ -81,7 +81,7 @@ class RepairReport(ctypes.Structure):
 class ArchiveStats(ctypes.Structure):
     """bfrs_archive_stats (include/bfrs.h)."""
     _fields_ = [(n, ctypes.c_uint64) for n in ("hits", "misses", "verified", "recoveries",
-                                               "recovered_segments", "bytes_served")]
+                                               "recovered_segments", "bytes_served", "prefetched")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}
@@ -143,7 +143,7 @@ def lib() -> ctypes.CDLL:
                                              ctypes.POINTER(_sz), _sz, _sz, _vp,
                                              ctypes.POINTER(_sz)], ctypes.c_int),
             "bfrs_blake3_hex": ([_vp, _sz, ctypes.c_int, ctypes.c_char_p], ctypes.c_int),
-            "bfrs_blake3_batch_dev": ([_vp, _sz, _pp, ctypes.POINTER(_sz), _vp, _vp, _vp],
+            "bfrs_blake3_batch_dev": ([_vp, _sz, _pp, ctypes.POINTER(_sz), _vp, _vp, _vp, _vp],
                                       ctypes.c_int),
             "bfrs_blake3_combine": ([_vp, _sz, ctypes.c_char_p], ctypes.c_int),
             "bfrs_merkle_root_hex": ([ctypes.c_char_p, _sz, ctypes.c_char_p], ctypes.c_int),
@@ -308,10 +308,11 @@ class Context:
             _check(fn(h, n, ks, recovery_count, shard_bytes, po, pr, pd, stream_handle))
         return call
 
-    def blake3_batch_dev(self, d_msgs, lens=None, stream=None, with_cvs=False):
-        """BLAKE3 of device messages (torch uint8 tensors or (address, len)
-        pairs via `lens`).  Returns hex digests, plus 32-byte subtree CVs if
-        with_cvs."""
+    def blake3_batch_dev(self, d_msgs, lens=None, stream=None, with_cvs=False,
+                         chunk_offsets=None):
+        """BLAKE3 of device messages (torch uint8 tensors, or addresses with
+        `lens`).  Returns hex digests, plus 32-byte subtree CVs if with_cvs;
+        chunk_offsets places each message inside an enclosing one (CVs)."""
         import numpy as np
         n = len(d_msgs)
         if lens is None:
@@ -320,7 +321,8 @@ class Context:
         ls = (_sz * max(1, n))(*lens)
         dig = np.zeros(max(1, n) * 32, np.uint8)
         cvs = np.zeros(max(1, n) * 32, np.uint8) if with_cvs else None
-        _check(lib().bfrs_blake3_batch_dev(self.handle, n, pm, ls, dig.ctypes.data,
+        offs = None if chunk_offsets is None else (ctypes.c_uint64 * max(1, n))(*chunk_offsets)
+        _check(lib().bfrs_blake3_batch_dev(self.handle, n, pm, ls, offs, dig.ctypes.data,
                                            cvs.ctypes.data if with_cvs else None,
                                            _stream_handle(stream, [t for t in d_msgs
                                                                    if not isinstance(t, int)])))

@@ -1,32 +1,25 @@
-// archive.cpp — BlockFrame's host pipeline around the RS codec, restated in
-// C++ over the HIP path: commit (tiers 1-3), repair, and the read-path core
-// that the FUSE mount uses.  On-disk layout and manifest are the reference's
-// (SURVEY.md Appendix B):
-//
-//   {root}/{name}_{blake3}/manifest.json
-//   tier 1: data.dat, parity_{0,1,2}.dat                          (commit.rs:25-118)
-//   tier 2: segments/segment_{i}.dat, parity/segment_{i}_parity_{p}.dat (commit.rs:124-309)
-//   tier 3: blocks/block_{b}/segments/segment_{s}.dat,
-//           blocks/block_{b}/parity/block_parity_{p}.dat          (commit.rs:314-536)
+// archive.cpp — BlockFrame's host pipeline around the RS codec: commit
+// (tiers 1-3), repair, and the read-path core of the FUSE mount, with the RS
+// arithmetic and (tier 3) the BLAKE3 verification on the GPU.  Layout and
+// manifest: archive_io.hpp.
 //
 // Repair and read follow the reference's *intended* semantics, not its bugs
 // (SURVEY §0.5): every missing or corrupt (BLAKE3 mismatch) segment of a
 // tier-3 block is restored with one RS(k,3) decode of that block and written
 // back to its in-block index; reads map offsets with `%`, not `&`
-// (filesystem_unix.rs:216), and tier-3 recovery decodes RS(30,3), not RS(1,3)
+// (filesystem_unix.rs:216), and tier-3 recovery decodes RS(k,3), not RS(1,3)
 // (:112-113).
-#include <dirent.h>
 #include <fcntl.h>
-#include <ftw.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
-#include <cerrno>
+#include <cctype>
+#include <condition_variable>
 #include <cstring>
-#include <functional>
 #include <list>
 #include <memory>
 #include <mutex>
@@ -34,7 +27,9 @@
 #include <thread>
 #include <unordered_map>
 
+#include "archive_io.hpp"
 #include "blake3.hpp"
+#include "gpu_block.hpp"
 #include "manifest.hpp"
 #include "runtime.hpp"
 
@@ -42,93 +37,16 @@ using namespace bfrs;
 
 namespace {
 
-constexpr uint64_t kTier1Limit = 25000000;    // commit.rs:596
-constexpr uint64_t kTier2Limit = 1000000000;  // commit.rs:597
-constexpr size_t kBlockSegments = 30;         // commit.rs:359,402
-constexpr size_t kParity = 3;
+constexpr uint64_t kTier1Limit = 25000000;     // commit.rs:596
+constexpr uint64_t kTier2Limit = 1000000000;   // commit.rs:597
 constexpr size_t kDefaultSegment = 32u << 20;  // utils.rs:68 on any real host
-
-int io_error(const std::string &what) {
-  return set_error(BFRS_E_WRAPPER, what + ": " + std::strerror(errno));
-}
-
-int hw_threads() {
-  const unsigned n = std::thread::hardware_concurrency();
-  return int(std::max(1u, std::min(16u, n ? n : 4u)));
-}
-
-// Runs f(i) for i in [0, n) on up to `threads` threads.
-void parallel_for(size_t n, int threads, const std::function<void(size_t)> &f) {
-  if (n == 0) return;
-  std::atomic<size_t> next{0};
-  auto worker = [&] {
-    for (size_t i; (i = next.fetch_add(1)) < n;) f(i);
-  };
-  std::vector<std::thread> ts;
-  const int t = int(std::min<size_t>(n, size_t(std::max(1, threads))));
-  for (int k = 1; k < t; ++k) ts.emplace_back(worker);
-  worker();
-  for (auto &th : ts) th.join();
-}
-
-bool mkdirs(const std::string &path) {
-  std::string cur;
-  std::stringstream ss(path);
-  std::string part;
-  if (!path.empty() && path[0] == '/') cur = "/";
-  while (std::getline(ss, part, '/')) {
-    if (part.empty()) continue;
-    cur += part + "/";
-    if (mkdir(cur.c_str(), 0755) != 0 && errno != EEXIST) return false;
-  }
-  return true;
-}
-
-int rm_cb(const char *p, const struct stat *, int, struct FTW *) { return remove(p); }
-bool rmtree(const std::string &p) { return nftw(p.c_str(), rm_cb, 32, FTW_DEPTH | FTW_PHYS) == 0; }
-
-bool write_file(const std::string &path, const uint8_t *data, size_t n) {
-  const int fd = open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
-  if (fd < 0) return false;
-  size_t done = 0;
-  while (done < n) {
-    const ssize_t w = write(fd, data + done, n - done);
-    if (w <= 0) {
-      close(fd);
-      return false;
-    }
-    done += size_t(w);
-  }
-  return close(fd) == 0;
-}
-
-// Whole file into `out`; false if absent/unreadable.
-bool read_file(const std::string &path, std::vector<uint8_t> *out) {
-  const int fd = open(path.c_str(), O_RDONLY);
-  if (fd < 0) return false;
-  struct stat st;
-  if (fstat(fd, &st) != 0) {
-    close(fd);
-    return false;
-  }
-  out->resize(size_t(st.st_size));
-  size_t done = 0;
-  while (done < out->size()) {
-    const ssize_t r = read(fd, out->data() + done, out->size() - done);
-    if (r <= 0) {
-      close(fd);
-      return false;
-    }
-    done += size_t(r);
-  }
-  close(fd);
-  return true;
-}
 
 std::string basename_of(const std::string &p) {
   const size_t s = p.find_last_of('/');
   return s == std::string::npos ? p : p.substr(s + 1);
 }
+
+bool pow2_kib(uint64_t s) { return s >= 1024 && s % 1024 == 0 && ((s / 1024) & (s / 1024 - 1)) == 0; }
 
 struct Mapped {
   int fd = -1;
@@ -140,24 +58,9 @@ struct Mapped {
   }
 };
 
-std::string t3_seg(const std::string &dir, size_t b, size_t s) {
-  return dir + "/blocks/block_" + std::to_string(b) + "/segments/segment_" + std::to_string(s) +
-         ".dat";
-}
-std::string t3_par(const std::string &dir, size_t b, size_t p) {
-  return dir + "/blocks/block_" + std::to_string(b) + "/parity/block_parity_" + std::to_string(p) +
-         ".dat";
-}
-std::string t2_seg(const std::string &dir, size_t i) {
-  return dir + "/segments/segment_" + std::to_string(i) + ".dat";
-}
-std::string t2_par(const std::string &dir, size_t i, size_t p) {
-  return dir + "/parity/segment_" + std::to_string(i) + "_parity_" + std::to_string(p) + ".dat";
-}
-
-// RS(k,3) encode of `blocks` (each a list of k host shards of shard_bytes) on the GPU.
-int gpu_encode(bfrs_ctx *ctx, const std::vector<std::vector<const uint8_t *>> &blocks,
-               size_t shard_bytes, std::vector<std::vector<std::vector<uint8_t>>> *parity) {
+// RS(k,3) encode of host blocks via the pipelined host-memory API.
+int host_encode(bfrs_ctx *ctx, const std::vector<std::vector<const uint8_t *>> &blocks,
+                size_t shard_bytes, std::vector<std::vector<std::vector<uint8_t>>> *parity) {
   std::vector<uint32_t> ks;
   std::vector<const uint8_t *> in;
   std::vector<uint8_t *> out;
@@ -174,7 +77,7 @@ int gpu_encode(bfrs_ctx *ctx, const std::vector<std::vector<const uint8_t *>> &b
 
 struct Commit {
   bfrs_ctx *ctx;
-  std::string root, name, path;
+  std::string root, name;
   size_t S;
   Mapped m;
   int threads = hw_threads();
@@ -189,7 +92,7 @@ struct Commit {
 int Commit::finish(const std::string &computing, const std::string &file_hash, Manifest &mf,
                    std::string *out_dir) {
   const std::string final_dir = root + "/" + name + "_" + file_hash;
-  if (computing != final_dir) {
+  if (computing != final_dir) {  // commit.rs:266,487
     struct stat st;
     if (stat(final_dir.c_str(), &st) == 0 && !rmtree(final_dir))  // duplicate commit overwrites
       return io_error("remove existing " + final_dir);
@@ -213,7 +116,7 @@ int Commit::tier1(std::string *out_dir) {
   std::vector<uint8_t> buf(padded, 0);
   std::memcpy(buf.data(), m.p, m.n);
   std::vector<std::vector<std::vector<uint8_t>>> par;
-  int rc = gpu_encode(ctx, {{buf.data()}}, padded, &par);
+  int rc = host_encode(ctx, {{buf.data()}}, padded, &par);
   if (rc) return rc;
   const std::string file_hash = blake3_hex(m.p, m.n, threads);
   const std::string dir = root + "/" + name + "_" + file_hash;
@@ -246,7 +149,7 @@ int Commit::tier2(std::string *out_dir) {
   mf.parity_shards = 3;
   mf.segment_size = S;
   std::vector<std::string> seg_roots(nseg);
-  // full segments in one GPU batch, the (padded) tail segment on its own
+  // full segments in GPU batches, the (padded) tail segment on its own
   const size_t full = m.n / S;
   for (size_t first = 0; first < nseg;) {
     const size_t len = std::min(S, m.n - first * S);
@@ -264,9 +167,10 @@ int Commit::tier2(std::string *out_dir) {
       blocks.push_back({src});
     }
     std::vector<std::vector<std::vector<uint8_t>>> par;
-    int rc = gpu_encode(ctx, blocks, padded, &par);
+    int rc = host_encode(ctx, blocks, padded, &par);
     if (rc) return rc;
     std::vector<SegmentHashes> hs(count);
+    for (auto &h : hs) h.parity.resize(kParity);
     std::atomic<bool> ok{true};
     parallel_for(count * 4, threads, [&](size_t t) {
       const size_t i = t / 4, what = t % 4;
@@ -278,12 +182,11 @@ int Commit::tier2(std::string *out_dir) {
       } else {
         const auto &p = par[i][what - 1];
         if (!write_file(t2_par(dir, seg, what - 1), p.data(), p.size())) ok = false;
+        hs[i].parity[what - 1] = blake3_hex(p.data(), p.size());
       }
     });
     if (!ok) return io_error("write tier-2 shards");
     for (size_t i = 0; i < count; ++i) {
-      for (size_t p = 0; p < kParity; ++p)
-        hs[i].parity.push_back(blake3_hex(par[i][p].data(), par[i][p].size()));
       std::vector<std::string> leaves{hs[i].data};
       leaves.insert(leaves.end(), hs[i].parity.begin(), hs[i].parity.end());
       seg_roots[first + i] = merkle_root_hex(leaves);
@@ -295,8 +198,14 @@ int Commit::tier2(std::string *out_dir) {
   return finish(dir, blake3_hex(m.p, m.n, threads), mf, out_dir);
 }
 
-// commit_blocked (commit.rs:314-536): blocks of <= 30 segments, RS(k,3) each,
-// block Merkle over segment+parity hashes, root over block roots.
+// commit_blocked (commit.rs:314-536), GPU-pipelined.  Per block of k <= 30
+// segments: host threads copy the segments from the mmap into a pinned
+// arena (zero-padding a short last segment, generate.rs:75-82), one H2D
+// copy, RS(k,3) encode, device BLAKE3 of all k+3 shards (commit.rs:429,451)
+// plus a second pass at file chunk offsets for the whole-file hash
+// (commit.rs:478, combined from the segment CVs), D2H of the parity.  Two
+// arenas alternate: the next block is filled while the GPU works, and the
+// previous block's files are written by a writer thread.
 int Commit::tier3(std::string *out_dir) {
   const std::string dir = root + "/" + name + "_computing";
   const size_t nseg = (m.n + S - 1) / S;
@@ -310,169 +219,131 @@ int Commit::tier3(std::string *out_dir) {
   mf.data_shards = 30;
   mf.parity_shards = 3;
   mf.segment_size = S;
+  const bool cv_hash = pow2_kib(S) && nseg >= 2;
+  std::vector<uint8_t> seg_cvs(cv_hash ? nseg * 32 : 0);
   std::vector<std::string> block_roots(nblocks);
-  // GPU batches of up to 8 full blocks (bounded host parity memory).
-  for (size_t b0 = 0; b0 < nblocks;) {
-    std::vector<std::vector<const uint8_t *>> blocks;
-    std::vector<uint8_t> tail_pad;
-    size_t shard_bytes = 0;
-    size_t b1 = b0;
-    for (; b1 < nblocks && b1 - b0 < 8; ++b1) {
-      const size_t s0 = b1 * kBlockSegments, s1 = std::min(nseg, s0 + kBlockSegments);
-      const size_t blk_max = std::min(S, m.n - s0 * S);  // first segment is the longest
-      if (b1 > b0 && blk_max != shard_bytes) break;      // one shard size per batch
-      shard_bytes = blk_max;
-      std::vector<const uint8_t *> segs;
-      for (size_t s = s0; s < s1; ++s) {
-        const size_t len = std::min(S, m.n - s * S);
-        if (len < shard_bytes) {  // generate.rs:75-82: zero-pad to the block's max length
-          tail_pad.assign(shard_bytes, 0);
-          std::memcpy(tail_pad.data(), m.p + s * S, len);
-          segs.push_back(tail_pad.data());
-        } else {
-          segs.push_back(m.p + s * S);
-        }
-      }
-      blocks.push_back(segs);
-    }
-    std::vector<std::vector<std::vector<uint8_t>>> par;
-    int rc = gpu_encode(ctx, blocks, shard_bytes, &par);
+  Arena arena[2];
+  for (auto &a : arena) {
+    int rc = a.reserve(S, kBlockSegments + kParity);
     if (rc) return rc;
-    // segment + parity files and hashes, in parallel
-    for (size_t b = b0; b < b1; ++b) {
-      const size_t s0 = b * kBlockSegments, s1 = std::min(nseg, s0 + kBlockSegments);
-      BlockHashes bh;
-      bh.segments.resize(s1 - s0);
-      bh.parity.resize(kParity);
-      std::atomic<bool> ok{true};
-      const auto &bp = par[b - b0];
-      parallel_for((s1 - s0) + kParity, threads, [&](size_t t) {
-        if (t < s1 - s0) {
-          const size_t s = s0 + t, len = std::min(S, m.n - s * S);
-          if (!write_file(t3_seg(dir, b, t), m.p + s * S, len)) ok = false;
-          bh.segments[t] = blake3_hex(m.p + s * S, len);
-        } else {
-          const size_t p = t - (s1 - s0);
-          if (!write_file(t3_par(dir, b, p), bp[p].data(), bp[p].size())) ok = false;
-          bh.parity[p] = blake3_hex(bp[p].data(), bp[p].size());
-        }
-      });
-      if (!ok) return io_error("write tier-3 shards");
-      std::vector<std::string> leaves = bh.segments;
-      leaves.insert(leaves.end(), bh.parity.begin(), bh.parity.end());
-      block_roots[b] = merkle_root_hex(leaves);
-      mf.blocks[int64_t(b)] = bh;
-    }
-    b0 = b1;
   }
+  auto geom = [&](size_t b, size_t *s0, size_t *k, size_t *shard) {
+    *s0 = b * kBlockSegments;
+    *k = std::min(kBlockSegments, nseg - *s0);
+    *shard = std::min(S, m.n - *s0 * S);  // the block's first segment is its longest
+  };
+  auto fill = [&](size_t b) {
+    size_t s0, k, shard;
+    geom(b, &s0, &k, &shard);
+    Arena &a = arena[b % 2];
+    parallel_for(k, threads, [&](size_t s) {
+      const size_t len = std::min(S, m.n - (s0 + s) * S);
+      std::memcpy(a.hs(s), m.p + (s0 + s) * S, len);
+      if (len < shard) std::memset(a.hs(s) + len, 0, shard - len);
+    });
+  };
+  Arena pbuf[2];  // pinned parity of the block being written (device side unused)
+  for (auto &a : pbuf) {
+    int rc = a.reserve(S, kParity);
+    if (rc) return rc;
+  }
+  std::atomic<bool> write_ok{true};
+  std::thread writer[2];
+  auto write_block = [&](size_t b) {  // segments from the mmap, parity from pbuf
+    size_t s0, k, shard;
+    geom(b, &s0, &k, &shard);
+    const Arena &pb = pbuf[b % 2];
+    parallel_for(k + kParity, threads, [&](size_t i) {
+      bool ok;
+      if (i < k)
+        ok = write_file(t3_seg(dir, b, i), m.p + (s0 + i) * S, std::min(S, m.n - (s0 + i) * S));
+      else
+        ok = write_file(t3_par(dir, b, i - k), pb.hs(i - k), shard);
+      if (!ok) write_ok = false;
+    });
+  };
+  // one block on the GPU: H2D, encode, hashes, D2H parity into pbuf[b % 2]
+  auto gpu_block = [&](size_t b) -> int {
+    size_t s0, k, shard;
+    geom(b, &s0, &k, &shard);
+    Arena &a = arena[b % 2];
+    Context &c = ctx->impl;
+    if (hipSetDevice(c.device) != hipSuccess ||
+        hipMemcpyAsync(a.d, a.h, a.slot * k, hipMemcpyHostToDevice, c.stream) != hipSuccess)
+      return set_error(BFRS_E_HIP, "commit: H2D copy failed");
+    std::vector<const uint8_t *> orig(k);
+    std::vector<uint8_t *> rec(kParity);
+    for (size_t s = 0; s < k; ++s) orig[s] = a.ds(s);
+    for (size_t p = 0; p < kParity; ++p) rec[p] = a.ds(k + p);
+    const uint32_t kk = uint32_t(k);
+    int rc = encode_batch_on(ctx, 1, &kk, kParity, shard, orig.data(), rec.data(), c.stream);
+    if (rc) return rc;
+    std::vector<const uint8_t *> msgs;
+    std::vector<size_t> lens;
+    for (size_t s = 0; s < k; ++s) {
+      msgs.push_back(a.ds(s));
+      lens.push_back(std::min(S, m.n - (s0 + s) * S));
+    }
+    for (size_t p = 0; p < kParity; ++p) {
+      msgs.push_back(a.ds(k + p));
+      lens.push_back(shard);
+    }
+    std::vector<std::string> hex;
+    if ((rc = gpu_hash_hex(ctx, msgs, lens, &hex))) return rc;
+    if (cv_hash) {  // the segments as nodes of the file's BLAKE3 tree
+      std::vector<const uint8_t *> sm(msgs.begin(), msgs.begin() + k);
+      std::vector<size_t> sl(lens.begin(), lens.begin() + k);
+      std::vector<uint64_t> offs(k);
+      for (size_t s = 0; s < k; ++s) offs[s] = uint64_t(s0 + s) * (S / 1024);
+      std::vector<std::string> unused;
+      std::vector<uint8_t> cvs;
+      if ((rc = gpu_hash_hex(ctx, sm, sl, &unused, offs.data(), &cvs))) return rc;
+      std::memcpy(seg_cvs.data() + s0 * 32, cvs.data(), k * 32);
+    }
+    if (writer[b % 2].joinable()) writer[b % 2].join();  // block b-2 still writing pbuf
+    Arena &pb = pbuf[b % 2];
+    for (size_t p = 0; p < kParity; ++p)
+      if (hipMemcpyAsync(pb.hs(p), a.ds(k + p), shard, hipMemcpyDeviceToHost, c.stream) !=
+          hipSuccess)
+        return set_error(BFRS_E_HIP, "commit: D2H copy failed");
+    if (hipStreamSynchronize(c.stream) != hipSuccess)
+      return set_error(BFRS_E_HIP, "commit: stream synchronize failed");
+    BlockHashes bh;
+    bh.segments.assign(hex.begin(), hex.begin() + k);
+    bh.parity.assign(hex.begin() + k, hex.end());
+    std::vector<std::string> leaves = bh.segments;
+    leaves.insert(leaves.end(), bh.parity.begin(), bh.parity.end());
+    block_roots[b] = merkle_root_hex(leaves);
+    mf.blocks[int64_t(b)] = bh;
+    return BFRS_OK;
+  };
+  int rc = BFRS_OK;
+  fill(0);
+  for (size_t b = 0; b < nblocks && rc == BFRS_OK; ++b) {
+    // arena[(b+1) % 2] was last used by block b-1's GPU work, which is done
+    std::thread filler;
+    if (b + 1 < nblocks) filler = std::thread(fill, b + 1);
+    rc = gpu_block(b);
+    if (filler.joinable()) filler.join();
+    if (rc == BFRS_OK) writer[b % 2] = std::thread(write_block, b);
+  }
+  for (auto &w : writer)
+    if (w.joinable()) w.join();
+  if (rc) return rc;
+  if (!write_ok) return io_error("write tier-3 shards");
   mf.root = merkle_root_hex(block_roots);
-  return finish(dir, blake3_hex(m.p, m.n, threads), mf, out_dir);
+  const std::string file_hash = cv_hash ? blake3_combine_cvs_hex(seg_cvs.data(), nseg)
+                                        : nseg == 1 ? mf.blocks[0].segments[0]
+                                                    : blake3_hex(m.p, m.n, threads);
+  return finish(dir, file_hash, mf, out_dir);
 }
 
 // ---------------------------------------------------------------------------
-// Archive geometry shared by repair and read.
-struct Geometry {
-  Manifest mf;
-  std::string dir;
-  uint64_t S = 0;
-  size_t nseg = 0;
-  size_t seg_len(size_t g) const { return size_t(std::min<uint64_t>(S, uint64_t(mf.size) - g * S)); }
-};
-
-int load_geometry(const std::string &dir, Geometry *g) {
-  std::vector<uint8_t> text;
-  if (!read_file(dir + "/manifest.json", &text)) return io_error("read manifest " + dir);
-  std::string err;
-  if (!Manifest::from_json(std::string(text.begin(), text.end()), &g->mf, &err))
-    return set_error(BFRS_E_WRAPPER, err);
-  g->dir = dir;
-  g->S = g->mf.tier == 1 ? uint64_t(std::max<int64_t>(g->mf.size, 1)) : g->mf.segment_size;
-  if (g->S == 0) return set_error(BFRS_E_WRAPPER, "manifest: segment_size is 0");
-  g->nseg = g->mf.tier == 1 ? 1 : size_t((uint64_t(g->mf.size) + g->S - 1) / g->S);
-  return BFRS_OK;
-}
-
-// Verified bytes of one stored shard (false = missing or hash mismatch).
-// threads > 1 splits the hash over chunk subtrees (callers already running in
-// a parallel_for pass 1).
+// Verified bytes of one stored shard, CPU hash (tiers 1/2; small files).
 bool load_verified(const std::string &path, const std::string &want_hex, std::vector<uint8_t> *out,
                    int threads = 1) {
   if (!read_file(path, out)) return false;
   return blake3_hex(out->data(), out->size(), threads) == want_hex;
-}
-
-// Tier-3 block recovery: restores every missing/corrupt segment of block b.
-// present[s]/data[s] in, restored data out (unpadded lengths).  Returns the
-// number of restored segments, or <0 (error) / BFRS_E_NOT_ENOUGH_SHARDS.
-int recover_block(bfrs_ctx *ctx, const Geometry &g, size_t b,
-                  std::vector<std::vector<uint8_t>> &data, std::vector<uint8_t> &ok,
-                  int *parity_bad) {
-  const BlockHashes &bh = g.mf.blocks.at(int64_t(b));
-  const size_t k = bh.segments.size();
-  const size_t g0 = b * kBlockSegments;
-  const size_t shard = g.seg_len(g0);  // the block's longest segment = padded shard size
-  std::vector<std::vector<uint8_t>> par(kParity);
-  std::vector<uint8_t> par_ok(kParity, 0);
-  int nbad = 0;
-  parallel_for(std::min(kParity, bh.parity.size()), int(kParity), [&](size_t p) {
-    par_ok[p] = load_verified(t3_par(g.dir, b, p), bh.parity[p], &par[p], hw_threads() / 3) &&
-                par[p].size() == shard;
-  });
-  for (size_t p = 0; p < kParity; ++p) nbad += !par_ok[p];
-  if (parity_bad) *parity_bad = nbad;
-  size_t erased = 0;
-  for (size_t s = 0; s < k; ++s) erased += !ok[s];
-  if (erased == 0) return 0;
-  size_t present = 0;
-  for (uint8_t v : par_ok) present += v;
-  if (erased > present) {
-    std::ostringstream os;
-    os << "block " << b << ": " << erased << " damaged segments but only " << present
-       << " valid parity shards - unrecoverable";
-    return set_error(BFRS_E_NOT_ENOUGH_SHARDS, os.str());
-  }
-  std::vector<std::vector<uint8_t>> padded(k);
-  std::vector<const uint8_t *> orig(k, nullptr), rec(kParity, nullptr);
-  std::vector<uint8_t *> out(k, nullptr);
-  for (size_t s = 0; s < k; ++s) {
-    if (ok[s]) {
-      if (data[s].size() < shard) {
-        padded[s].assign(shard, 0);
-        std::memcpy(padded[s].data(), data[s].data(), data[s].size());
-        orig[s] = padded[s].data();
-      } else {
-        orig[s] = data[s].data();
-      }
-    } else {
-      padded[s].assign(shard, 0);
-      out[s] = padded[s].data();
-    }
-  }
-  for (size_t p = 0; p < kParity; ++p)
-    if (par_ok[p]) rec[p] = par[p].data();
-  const uint32_t kk = uint32_t(k);
-  int rc = bfrs_decode_host_batch(ctx, 1, &kk, kParity, shard, orig.data(), rec.data(), out.data());
-  if (rc) return rc;
-  std::vector<size_t> todo;
-  for (size_t s = 0; s < k; ++s)
-    if (!ok[s]) todo.push_back(s);
-  std::vector<uint8_t> good(todo.size(), 0);
-  parallel_for(todo.size(), int(todo.size()), [&](size_t i) {
-    const size_t s = todo[i], len = g.seg_len(g0 + s);
-    padded[s].resize(len);
-    data[s] = std::move(padded[s]);
-    // src/merkle_tree re-verify of the reconstructed bytes
-    good[i] = blake3_hex(data[s].data(), len, hw_threads() / int(todo.size())) == bh.segments[s];
-  });
-  for (size_t i = 0; i < todo.size(); ++i) {
-    if (!good[i]) {
-      std::ostringstream os;
-      os << "block " << b << " segment " << todo[i] << ": restored bytes fail the manifest hash";
-      return set_error(BFRS_E_WRAPPER, os.str());
-    }
-    ok[todo[i]] = 1;
-  }
-  return int(todo.size());
 }
 
 // RS(1,3) recovery (tiers 1/2): decode from the valid parity shards.
@@ -501,121 +372,237 @@ int recover_rs13(bfrs_ctx *ctx, const std::vector<std::string> &paths,
   return BFRS_OK;
 }
 
+// Fixed-size pinned buffers backing the read cache (pinned so a segment
+// goes to HBM for verification without a staging copy).
+struct PinnedPool {
+  size_t slot;
+  std::mutex mu;
+  std::vector<uint8_t *> free_, all_;
+  explicit PinnedPool(size_t s) : slot(std::max<size_t>(256, (s + 255) / 256 * 256)) {}
+  ~PinnedPool() {
+    for (uint8_t *p : all_) (void)hipHostFree(p);
+  }
+  uint8_t *get() {
+    {
+      std::lock_guard<std::mutex> g(mu);
+      if (!free_.empty()) {
+        uint8_t *p = free_.back();
+        free_.pop_back();
+        return p;
+      }
+    }
+    void *p = nullptr;
+    if (hipHostMalloc(&p, slot, hipHostMallocDefault) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> g(mu);
+    all_.push_back(static_cast<uint8_t *>(p));
+    return static_cast<uint8_t *>(p);
+  }
+  void put(uint8_t *p) {
+    std::lock_guard<std::mutex> g(mu);
+    free_.push_back(p);
+  }
+};
+
+struct Seg {
+  uint8_t *p = nullptr;
+  size_t n = 0;
+  std::shared_ptr<PinnedPool> pool;
+  Seg(std::shared_ptr<PinnedPool> pl, uint8_t *buf, size_t len) : p(buf), n(len), pool(std::move(pl)) {}
+  ~Seg() {
+    if (p) pool->put(p);
+  }
+};
+using SegPtr = std::shared_ptr<Seg>;
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
-// Archive read handle (src/mount/filesystem_unix.rs:176-305 + cache.rs)
+// Archive read handle (src/mount/filesystem_unix.rs:176-305 + cache.rs).
+// Segments are cached in pinned buffers (LRU); a miss reads the file,
+// verifies it on the GPU and, if it is missing or corrupt, reconstructs it
+// (tier 3: RS(k,3) decode of its block on the GPU, device re-verify).  A
+// prefetch thread loads and verifies the next segment when reads move to a
+// new one, so sequential reads overlap disk/PCIe/hash with serving.
 struct bfrs_archive {
-  bfrs_ctx *ctx;
+  bfrs_ctx *ctx = nullptr;
   Geometry g;
-  size_t cap;
-  bool write_back;
-  std::mutex mu;
-  std::list<size_t> lru;
-  std::unordered_map<size_t, std::pair<std::shared_ptr<std::vector<uint8_t>>,
-                                       std::list<size_t>::iterator>>
-      cache;
-  bfrs_archive_stats st{};
+  size_t cap = 1;
+  bool write_back = false;
+  bool prefetch = true;
+  std::shared_ptr<PinnedPool> pool;
 
-  void put(size_t g_idx, std::shared_ptr<std::vector<uint8_t>> v) {
-    auto it = cache.find(g_idx);
+  std::mutex mu;  // cache, stats, prefetch state
+  std::condition_variable cv;
+  std::list<size_t> lru;
+  std::unordered_map<size_t, std::pair<SegPtr, std::list<size_t>::iterator>> cache;
+  bfrs_archive_stats st{};
+  long long want = -1, inflight = -1, last_gi = -1;
+  bool stop = false;
+  std::thread worker;
+
+  std::mutex gpu_mu;  // the context and the arena (one user at a time)
+  Arena arena;
+
+  ~bfrs_archive() {
+    {
+      std::lock_guard<std::mutex> l(mu);
+      stop = true;
+    }
+    cv.notify_all();
+    if (worker.joinable()) worker.join();
+    cache.clear();
+  }
+
+  SegPtr lookup(size_t gi) {  // under mu
+    auto it = cache.find(gi);
+    if (it == cache.end()) return nullptr;
+    lru.splice(lru.begin(), lru, it->second.second);
+    return it->second.first;
+  }
+  void put(size_t gi, SegPtr v) {  // under mu
+    auto it = cache.find(gi);
     if (it != cache.end()) {
       lru.erase(it->second.second);
       cache.erase(it);
     }
-    lru.push_front(g_idx);
-    cache[g_idx] = {std::move(v), lru.begin()};
+    lru.push_front(gi);
+    cache[gi] = {std::move(v), lru.begin()};
     while (cache.size() > cap) {
       cache.erase(lru.back());
       lru.pop_back();
     }
   }
-  int segment(size_t gi, std::shared_ptr<std::vector<uint8_t>> *out);
+  std::string expected_hash(size_t gi) const;
+  std::string seg_path(size_t gi) const;
+  int load_clean(size_t gi, SegPtr *out, bool *ok);  // no locks held
+  int recover(size_t gi, SegPtr *out);              // no locks held
+  void prefetch_loop();
 };
 
-int bfrs_archive::segment(size_t gi, std::shared_ptr<std::vector<uint8_t>> *out) {
-  auto it = cache.find(gi);
-  if (it != cache.end()) {
-    lru.splice(lru.begin(), lru, it->second.second);
-    ++st.hits;
-    *out = it->second.first;
-    return BFRS_OK;
-  }
-  ++st.misses;
+std::string bfrs_archive::expected_hash(size_t gi) const {
   const Manifest &mf = g.mf;
-  auto v = std::make_shared<std::vector<uint8_t>>();
+  if (mf.tier == 3) return mf.blocks.at(int64_t(gi / kBlockSegments)).segments[gi % kBlockSegments];
+  if (mf.tier == 2) return mf.segments.at(int64_t(gi)).data;
+  return mf.leaves.at(0);
+}
+
+std::string bfrs_archive::seg_path(size_t gi) const {
+  if (g.mf.tier == 3) return t3_seg(g.dir, gi / kBlockSegments, gi % kBlockSegments);
+  if (g.mf.tier == 2) return t2_seg(g.dir, gi);
+  return g.dir + "/data.dat";
+}
+
+// Reads segment gi into a pinned buffer and verifies it with the device
+// BLAKE3; *ok = false if it is missing, short or fails the manifest hash.
+int bfrs_archive::load_clean(size_t gi, SegPtr *out, bool *ok) {
+  *ok = false;
+  const size_t len = g.seg_len(gi);
+  uint8_t *buf = pool->get();
+  if (!buf) return set_error(BFRS_E_NOMEM, "pinned segment buffer allocation failed");
+  auto seg = std::make_shared<Seg>(pool, buf, len);
+  if (read_file_into(seg_path(gi), buf, pool->slot) != (long long)len) return BFRS_OK;
+  std::lock_guard<std::mutex> lg(gpu_mu);
+  int rc = arena.reserve(pool->slot, kBlockSegments + kParity);
+  if (rc) return rc;
+  Context &c = ctx->impl;
+  HIP_TRY(hipSetDevice(c.device));
+  HIP_TRY(hipMemcpyAsync(arena.ds(0), buf, len, hipMemcpyHostToDevice, c.stream));
+  std::vector<std::string> hex;
+  if ((rc = gpu_hash_hex(ctx, {arena.ds(0)}, {len}, &hex))) return rc;
+  if (hex[0] == expected_hash(gi)) {
+    *ok = true;
+    *out = std::move(seg);
+  }
+  return BFRS_OK;
+}
+
+// Reconstructs segment gi (and, tier 3, every other damaged segment of its
+// block, which is cached too).
+int bfrs_archive::recover(size_t gi, SegPtr *out) {
+  const Manifest &mf = g.mf;
   if (mf.tier == 3) {
-    const size_t b = gi / kBlockSegments, s = gi % kBlockSegments;
-    auto bit = mf.blocks.find(int64_t(b));
-    if (bit == mf.blocks.end() || s >= bit->second.segments.size())
-      return set_error(BFRS_E_WRAPPER, "manifest has no hash for segment " + std::to_string(gi));
-    if (load_verified(t3_seg(g.dir, b, s), bit->second.segments[s], v.get(), hw_threads())) {
-      ++st.verified;
-      put(gi, v);
-      *out = v;
-      return BFRS_OK;
-    }
-    // hash mismatch or missing: restore the whole block in one GPU decode
-    const size_t k = bit->second.segments.size();
-    std::vector<std::vector<uint8_t>> data(k);
-    std::vector<uint8_t> ok(k, 0);
-    parallel_for(k, hw_threads(), [&](size_t t) {
-      auto c = cache.find(b * kBlockSegments + t);  // read-only lookups under a.mu
-      if (c != cache.end()) {
-        data[t] = *c->second.first;
-        ok[t] = 1;
-      } else if (t != s) {
-        ok[t] = load_verified(t3_seg(g.dir, b, t), bit->second.segments[t], &data[t]);
-      }
-    });
-    std::vector<uint8_t> was_ok = ok;
-    int rc = recover_block(ctx, g, b, data, ok, nullptr);
-    if (rc < 0) return rc;
-    ++st.recoveries;
-    for (size_t t = 0; t < k; ++t) {
-      if (was_ok[t]) continue;
-      ++st.recovered_segments;
-      if (write_back && !write_file(t3_seg(g.dir, b, t), data[t].data(), data[t].size()))
-        return io_error("write back segment");
-      if (t != s) put(b * kBlockSegments + t, std::make_shared<std::vector<uint8_t>>(data[t]));
-    }
-    *v = std::move(data[s]);
-  } else if (mf.tier == 2) {
-    auto sit = mf.segments.find(int64_t(gi));
-    if (sit == mf.segments.end()) return set_error(BFRS_E_WRAPPER, "manifest has no segment");
-    if (load_verified(t2_seg(g.dir, gi), sit->second.data, v.get(), hw_threads())) {
-      ++st.verified;
-    } else {
-      std::vector<std::string> paths;
-      for (size_t p = 0; p < kParity; ++p) paths.push_back(t2_par(g.dir, gi, p));
-      int rc = recover_rs13(ctx, paths, sit->second.parity, g.seg_len(gi), sit->second.data, v.get());
+    std::vector<std::pair<size_t, SegPtr>> restored;
+    {
+      std::lock_guard<std::mutex> lg(gpu_mu);
+      const size_t b = gi / kBlockSegments;
+      BlockState bs;
+      int rc = load_block(ctx, g, b, arena, &bs);
       if (rc) return rc;
+      const std::vector<uint8_t> was_ok = bs.seg_ok;
+      rc = restore_block(ctx, g, arena, bs);
+      if (rc < 0) return rc;
+      for (size_t s = 0; s < bs.k; ++s) {
+        const bool need = !was_ok[s] || b * kBlockSegments + s == gi;
+        if (!need) continue;
+        uint8_t *buf = pool->get();
+        if (!buf) return set_error(BFRS_E_NOMEM, "pinned segment buffer allocation failed");
+        std::memcpy(buf, arena.hs(s), bs.lens[s]);
+        if (!was_ok[s] && write_back && !write_file(t3_seg(g.dir, b, s), buf, bs.lens[s]))
+          return io_error("write back segment");
+        restored.emplace_back(b * kBlockSegments + s, std::make_shared<Seg>(pool, buf, bs.lens[s]));
+      }
+      std::lock_guard<std::mutex> l(mu);
       ++st.recoveries;
-      ++st.recovered_segments;
-      if (write_back && !write_file(t2_seg(g.dir, gi), v->data(), v->size()))
-        return io_error("write back segment");
+      for (size_t s = 0; s < bs.k; ++s) st.recovered_segments += !was_ok[s];
+      for (auto &r : restored)
+        if (r.first != gi) put(r.first, r.second);
     }
+    for (auto &r : restored)
+      if (r.first == gi) *out = r.second;
+    return *out ? BFRS_OK : set_error(BFRS_E_WRAPPER, "segment not restored");
+  }
+  std::vector<uint8_t> v;
+  int rc;
+  if (mf.tier == 2) {
+    const auto &sh = mf.segments.at(int64_t(gi));
+    std::vector<std::string> paths;
+    for (size_t p = 0; p < kParity; ++p) paths.push_back(t2_par(g.dir, gi, p));
+    std::lock_guard<std::mutex> lg(gpu_mu);
+    rc = recover_rs13(ctx, paths, sh.parity, g.seg_len(gi), sh.data, &v);
   } else {
     if (mf.leaves.size() < 4) return set_error(BFRS_E_WRAPPER, "tier-1 manifest needs 4 leaves");
-    if (load_verified(g.dir + "/data.dat", mf.leaves.at(0), v.get(), hw_threads())) {
-      ++st.verified;
-    } else {
-      std::vector<std::string> paths, hashes;
-      for (size_t p = 0; p < kParity; ++p) {
-        paths.push_back(g.dir + "/parity_" + std::to_string(p) + ".dat");
-        hashes.push_back(mf.leaves.at(int64_t(p + 1)));
-      }
-      int rc = recover_rs13(ctx, paths, hashes, size_t(mf.size), mf.leaves.at(0), v.get());
-      if (rc) return rc;
-      ++st.recoveries;
-      ++st.recovered_segments;
-      if (write_back && !write_file(g.dir + "/data.dat", v->data(), v->size()))
-        return io_error("write back data.dat");
+    std::vector<std::string> paths, hashes;
+    for (size_t p = 0; p < kParity; ++p) {
+      paths.push_back(g.dir + "/parity_" + std::to_string(p) + ".dat");
+      hashes.push_back(mf.leaves.at(int64_t(p + 1)));
     }
+    std::lock_guard<std::mutex> lg(gpu_mu);
+    rc = recover_rs13(ctx, paths, hashes, size_t(mf.size), mf.leaves.at(0), &v);
   }
-  put(gi, v);
-  *out = v;
+  if (rc) return rc;
+  if (write_back && !write_file(seg_path(gi), v.data(), v.size())) return io_error("write back segment");
+  uint8_t *buf = pool->get();
+  if (!buf) return set_error(BFRS_E_NOMEM, "pinned segment buffer allocation failed");
+  std::memcpy(buf, v.data(), v.size());
+  *out = std::make_shared<Seg>(pool, buf, v.size());
+  std::lock_guard<std::mutex> l(mu);
+  ++st.recoveries;
+  ++st.recovered_segments;
   return BFRS_OK;
+}
+
+void bfrs_archive::prefetch_loop() {
+  std::unique_lock<std::mutex> l(mu);
+  for (;;) {
+    cv.wait(l, [&] { return stop || want >= 0; });
+    if (stop) return;
+    const size_t gi = size_t(want);
+    want = -1;
+    if (cache.count(gi)) continue;
+    inflight = (long long)gi;
+    l.unlock();
+    SegPtr seg;
+    bool ok = false;
+    const int rc = load_clean(gi, &seg, &ok);  // damaged segments are left to the reader
+    l.lock();
+    if (rc == BFRS_OK && ok) {
+      put(gi, seg);
+      ++st.verified;
+      ++st.prefetched;
+    }
+    inflight = -1;
+    cv.notify_all();
+  }
 }
 
 extern "C" {
@@ -643,7 +630,8 @@ int bfrs_manifest_check(const char *text, size_t len, int *valid, char *canonica
   std::string err;
   if (!Manifest::from_json(std::string(text, len), &mf, &err)) return set_error(BFRS_E_WRAPPER, err);
   auto hex64 = [](const std::string &h) {
-    return h.size() == 64 && std::all_of(h.begin(), h.end(), [](char c) { return std::isxdigit(uint8_t(c)); });
+    return h.size() == 64 &&
+           std::all_of(h.begin(), h.end(), [](char c) { return std::isxdigit(uint8_t(c)) != 0; });
   };
   // ManifestFile::validate (src/merkle_tree/manifest.rs:55-88)
   bool ok = hex64(mf.root) && !(mf.leaves.empty() && mf.segments.empty() && mf.blocks.empty());
@@ -664,8 +652,7 @@ int bfrs_commit(bfrs_ctx *ctx, const char *file_path, const char *archive_root,
                 size_t segment_size, int tier, char *out_dir, size_t out_cap) {
   if (!ctx || !file_path || !archive_root)
     return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_commit: NULL argument");
-  Commit c{ctx, archive_root, basename_of(file_path), file_path,
-           segment_size ? segment_size : kDefaultSegment};
+  Commit c{ctx, archive_root, basename_of(file_path), segment_size ? segment_size : kDefaultSegment};
   c.m.fd = open(file_path, O_RDONLY);
   if (c.m.fd < 0) return io_error(std::string("open ") + file_path);
   struct stat st;
@@ -695,72 +682,60 @@ int bfrs_repair(bfrs_ctx *ctx, const char *archive_dir, bfrs_repair_report *repo
   Geometry g;
   int rc = load_geometry(archive_dir, &g);
   if (rc) return rc;
-  const Manifest &mf = g.mf;
-  if (mf.tier == 3) {
-    for (const auto &kv : mf.blocks) {
-      const size_t b = size_t(kv.first), k = kv.second.segments.size();
+  if (g.mf.tier == 3) {  // repair_blocked (health.rs:642-765), intended semantics
+    Arena a;
+    for (const auto &kv : g.mf.blocks) {
+      const size_t b = size_t(kv.first);
+      BlockState bs;
+      if ((rc = load_block(ctx, g, b, a, &bs))) return rc;
       ++report->blocks_checked;
-      std::vector<std::vector<uint8_t>> data(k);
-      std::vector<uint8_t> ok(k, 0);
-      parallel_for(k, hw_threads(), [&](size_t s) {
-        ok[s] = load_verified(t3_seg(g.dir, b, s), kv.second.segments[s], &data[s]);
-      });
-      report->segments_checked += k;
-      std::vector<uint8_t> was_ok = ok;
-      int parity_bad = 0;
-      const int restored = recover_block(ctx, g, b, data, ok, &parity_bad);
-      if (restored < 0) {
-        if (restored != BFRS_E_NOT_ENOUGH_SHARDS) return restored;
+      report->segments_checked += bs.k;
+      const std::vector<uint8_t> was_ok = bs.seg_ok;
+      const size_t parity_bad = kParity - bs.valid_parity();
+      const int restored = restore_block(ctx, g, a, bs);
+      if (restored == BFRS_E_NOT_ENOUGH_SHARDS) {
         ++report->unrecoverable_blocks;
         continue;
       }
-      for (size_t s = 0; s < k; ++s)
+      if (restored < 0) return restored;
+      for (size_t s = 0; s < bs.k; ++s)
         if (!was_ok[s]) {
-          if (!write_file(t3_seg(g.dir, b, s), data[s].data(), data[s].size()))
+          if (!write_file(t3_seg(g.dir, b, s), a.hs(s), bs.lens[s]))
             return io_error("write restored segment");
           ++report->segments_repaired;
         }
-      if (parity_bad) {  // data is whole now: re-encode and rewrite the parity
-        const size_t shard = g.seg_len(b * kBlockSegments);
-        std::vector<std::vector<uint8_t>> padded(k);
-        std::vector<const uint8_t *> segs(k);
-        for (size_t s = 0; s < k; ++s) {
-          if (data[s].size() < shard) {
-            padded[s].assign(shard, 0);
-            std::memcpy(padded[s].data(), data[s].data(), data[s].size());
-            segs[s] = padded[s].data();
-          } else {
-            segs[s] = data[s].data();
-          }
-        }
-        std::vector<std::vector<std::vector<uint8_t>>> par;
-        if ((rc = gpu_encode(ctx, {segs}, shard, &par))) return rc;
-        for (size_t p = 0; p < kParity; ++p) {
-          if (blake3_hex(par[0][p].data(), shard) != kv.second.parity[p])
-            return set_error(BFRS_E_WRAPPER, "re-encoded parity fails the manifest hash");
-          if (!write_file(t3_par(g.dir, b, p), par[0][p].data(), shard))
+      if (parity_bad) {
+        const std::vector<uint8_t> par_was = bs.par_ok;
+        if ((rc = reencode_parity(ctx, g, a, bs))) return rc;
+        for (size_t p = 0; p < kParity; ++p)
+          if (!par_was[p] && !write_file(t3_par(g.dir, b, p), a.hs(bs.k + p), bs.shard))
             return io_error("write parity");
-        }
-        report->parity_repaired += uint64_t(parity_bad);
+        report->parity_repaired += parity_bad;
       }
     }
     return BFRS_OK;
   }
-  // tiers 1/2: per-segment RS(1,3)
-  bfrs_archive a{ctx, g, 1, true};
+  // tiers 1/2 (repair_tiny :497, repair_segment :542): per-segment RS(1,3)
+  bfrs_archive a;
+  a.ctx = ctx;
+  a.g = g;
+  a.write_back = true;
+  a.pool = std::make_shared<PinnedPool>(g.S);
   for (size_t i = 0; i < g.nseg; ++i) {
-    std::shared_ptr<std::vector<uint8_t>> v;
     ++report->segments_checked;
-    const uint64_t before = a.st.recovered_segments;
-    rc = a.segment(i, &v);
+    ++report->blocks_checked;
+    SegPtr v;
+    bool ok = false;
+    if ((rc = a.load_clean(i, &v, &ok))) return rc;
+    if (ok) continue;
+    rc = a.recover(i, &v);
     if (rc == BFRS_E_NOT_ENOUGH_SHARDS) {
       ++report->unrecoverable_blocks;
       continue;
     }
     if (rc) return rc;
-    report->segments_repaired += a.st.recovered_segments - before;
+    ++report->segments_repaired;
   }
-  report->blocks_checked = g.nseg;
   return BFRS_OK;
 }
 
@@ -769,15 +744,17 @@ int bfrs_archive_open(bfrs_ctx *ctx, const char *archive_dir, size_t cache_segme
   if (!ctx || !archive_dir || !out)
     return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_archive_open: NULL argument");
   *out = nullptr;
-  auto *a = new (std::nothrow) bfrs_archive{ctx, {}, std::max<size_t>(1, cache_segments),
-                                            write_back != 0};
+  std::unique_ptr<bfrs_archive> a(new (std::nothrow) bfrs_archive);
   if (!a) return set_error(BFRS_E_NOMEM, "archive allocation failed");
+  a->ctx = ctx;
+  a->cap = std::max<size_t>(1, cache_segments);
+  a->write_back = write_back != 0;
   int rc = load_geometry(archive_dir, &a->g);
-  if (rc) {
-    delete a;
-    return rc;
-  }
-  *out = a;
+  if (rc) return rc;
+  a->pool = std::make_shared<PinnedPool>(a->g.S);
+  a->prefetch = a->g.nseg > 1;
+  if (a->prefetch) a->worker = std::thread(&bfrs_archive::prefetch_loop, a.get());
+  *out = a.release();
   return BFRS_OK;
 }
 
@@ -789,22 +766,44 @@ int bfrs_archive_size(bfrs_archive *a, uint64_t *size) {
 
 int bfrs_archive_read(bfrs_archive *a, uint64_t offset, size_t len, uint8_t *out, size_t *nread) {
   if (!a || (!out && len) || !nread) return set_error(BFRS_E_INVALID_ARGUMENT, "NULL argument");
-  std::lock_guard<std::mutex> g(a->mu);
   *nread = 0;
   const uint64_t size = uint64_t(a->g.mf.size);
   if (offset >= size) return BFRS_OK;
   len = size_t(std::min<uint64_t>(len, size - offset));
   const uint64_t S = a->g.S;
+  std::unique_lock<std::mutex> l(a->mu);
   while (*nread < len) {
     const uint64_t pos = offset + *nread;
     const size_t gi = size_t(pos / S);
     const size_t in_seg = size_t(pos % S);  // filesystem_unix.rs:216 uses '&' (bug)
-    std::shared_ptr<std::vector<uint8_t>> seg;
-    int rc = a->segment(gi, &seg);
-    if (rc) return rc;
-    if (in_seg >= seg->size()) return set_error(BFRS_E_WRAPPER, "segment shorter than manifest size");
-    const size_t n = std::min(len - *nread, seg->size() - in_seg);
-    std::memcpy(out + *nread, seg->data() + in_seg, n);
+    SegPtr seg = a->lookup(gi);
+    if (seg) {
+      ++a->st.hits;
+    } else if (a->inflight == (long long)gi) {  // the prefetcher is loading it
+      a->cv.wait(l, [&] { return a->inflight != (long long)gi; });
+      continue;
+    } else {
+      ++a->st.misses;
+      l.unlock();
+      bool ok = false;
+      int rc = a->load_clean(gi, &seg, &ok);
+      if (rc == BFRS_OK && !ok) rc = a->recover(gi, &seg);
+      l.lock();
+      if (rc) return rc;
+      if (ok) ++a->st.verified;
+      a->put(gi, seg);
+    }
+    if (a->prefetch && (long long)gi != a->last_gi) {  // moved to a new segment
+      a->last_gi = (long long)gi;
+      const size_t nx = gi + 1;
+      if (nx < a->g.nseg && !a->cache.count(nx) && a->inflight != (long long)nx) {
+        a->want = (long long)nx;
+        a->cv.notify_all();
+      }
+    }
+    if (in_seg >= seg->n) return set_error(BFRS_E_WRAPPER, "segment shorter than manifest size");
+    const size_t n = std::min(len - *nread, seg->n - in_seg);
+    std::memcpy(out + *nread, seg->p + in_seg, n);
     *nread += n;
   }
   a->st.bytes_served += *nread;

@@ -1,0 +1,165 @@
+// archive_io.cpp — see archive_io.hpp.
+#include "archive_io.hpp"
+
+#include <fcntl.h>
+#include <ftw.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cerrno>
+#include <cstring>
+#include <sstream>
+#include <thread>
+
+#include "runtime.hpp"
+
+namespace bfrs {
+
+int io_error(const std::string &what) {
+  return set_error(BFRS_E_WRAPPER, what + ": " + std::strerror(errno));
+}
+
+int hw_threads() {
+  const unsigned n = std::thread::hardware_concurrency();
+  return int(std::max(1u, std::min(16u, n ? n : 4u)));
+}
+
+void parallel_for(size_t n, int threads, const std::function<void(size_t)> &f) {
+  if (n == 0) return;
+  std::atomic<size_t> next{0};
+  auto worker = [&] {
+    for (size_t i; (i = next.fetch_add(1)) < n;) f(i);
+  };
+  std::vector<std::thread> ts;
+  const int t = int(std::min<size_t>(n, size_t(std::max(1, threads))));
+  for (int k = 1; k < t; ++k) ts.emplace_back(worker);
+  worker();
+  for (auto &th : ts) th.join();
+}
+
+bool mkdirs(const std::string &path) {
+  std::string cur;
+  std::stringstream ss(path);
+  std::string part;
+  if (!path.empty() && path[0] == '/') cur = "/";
+  while (std::getline(ss, part, '/')) {
+    if (part.empty()) continue;
+    cur += part + "/";
+    if (mkdir(cur.c_str(), 0755) != 0 && errno != EEXIST) return false;
+  }
+  return true;
+}
+
+namespace {
+int rm_cb(const char *p, const struct stat *, int, struct FTW *) { return remove(p); }
+}  // namespace
+
+bool rmtree(const std::string &p) { return nftw(p.c_str(), rm_cb, 32, FTW_DEPTH | FTW_PHYS) == 0; }
+
+bool write_file(const std::string &path, const uint8_t *data, size_t n) {
+  const int fd = open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+  if (fd < 0) return false;
+  size_t done = 0;
+  while (done < n) {
+    const ssize_t w = write(fd, data + done, n - done);
+    if (w <= 0) {
+      close(fd);
+      return false;
+    }
+    done += size_t(w);
+  }
+  return close(fd) == 0;
+}
+
+bool read_file(const std::string &path, std::vector<uint8_t> *out) {
+  const int fd = open(path.c_str(), O_RDONLY);
+  if (fd < 0) return false;
+  struct stat st;
+  if (fstat(fd, &st) != 0) {
+    close(fd);
+    return false;
+  }
+  out->resize(size_t(st.st_size));
+  size_t done = 0;
+  while (done < out->size()) {
+    const ssize_t r = read(fd, out->data() + done, out->size() - done);
+    if (r <= 0) {
+      close(fd);
+      return false;
+    }
+    done += size_t(r);
+  }
+  close(fd);
+  return true;
+}
+
+long long read_file_into(const std::string &path, uint8_t *dst, size_t cap) {
+  const int fd = open(path.c_str(), O_RDONLY);
+  if (fd < 0) return -1;
+  struct stat st;
+  if (fstat(fd, &st) != 0 || size_t(st.st_size) > cap) {
+    close(fd);
+    return -1;
+  }
+  const size_t n = size_t(st.st_size);
+  size_t done = 0;
+  while (done < n) {
+    const ssize_t r = read(fd, dst + done, n - done);
+    if (r <= 0) {
+      close(fd);
+      return -1;
+    }
+    done += size_t(r);
+  }
+  close(fd);
+  return (long long)n;
+}
+
+std::string t3_seg(const std::string &dir, size_t b, size_t s) {
+  return dir + "/blocks/block_" + std::to_string(b) + "/segments/segment_" + std::to_string(s) +
+         ".dat";
+}
+std::string t3_par(const std::string &dir, size_t b, size_t p) {
+  return dir + "/blocks/block_" + std::to_string(b) + "/parity/block_parity_" + std::to_string(p) +
+         ".dat";
+}
+std::string t2_seg(const std::string &dir, size_t i) {
+  return dir + "/segments/segment_" + std::to_string(i) + ".dat";
+}
+std::string t2_par(const std::string &dir, size_t i, size_t p) {
+  return dir + "/parity/segment_" + std::to_string(i) + "_parity_" + std::to_string(p) + ".dat";
+}
+
+size_t Geometry::block_k(size_t b) const {
+  auto it = mf.blocks.find(int64_t(b));
+  return it == mf.blocks.end() ? 0 : it->second.segments.size();
+}
+
+int load_geometry(const std::string &dir, Geometry *g) {
+  std::vector<uint8_t> text;
+  if (!read_file(dir + "/manifest.json", &text)) return io_error("read manifest " + dir);
+  std::string err;
+  if (!Manifest::from_json(std::string(text.begin(), text.end()), &g->mf, &err))
+    return set_error(BFRS_E_WRAPPER, err);
+  g->dir = dir;
+  g->S = g->mf.tier == 1 ? uint64_t(std::max<int64_t>(g->mf.size, 1)) : g->mf.segment_size;
+  if (g->S == 0) return set_error(BFRS_E_WRAPPER, "manifest: segment_size is 0");
+  if (g->mf.size < 0) return set_error(BFRS_E_WRAPPER, "manifest: negative size");
+  g->nseg = g->mf.tier == 1 ? 1 : size_t((uint64_t(g->mf.size) + g->S - 1) / g->S);
+  if (g->mf.tier == 3) {  // blocks must cover the segments in order (commit.rs:359-402)
+    const size_t nblocks = (g->nseg + kBlockSegments - 1) / kBlockSegments;
+    if (g->mf.blocks.size() != nblocks) return set_error(BFRS_E_WRAPPER, "manifest: block count");
+    for (size_t b = 0; b < nblocks; ++b) {
+      auto it = g->mf.blocks.find(int64_t(b));
+      const size_t want = std::min(kBlockSegments, g->nseg - b * kBlockSegments);
+      if (it == g->mf.blocks.end() || it->second.segments.size() != want ||
+          it->second.parity.size() != kParity)
+        return set_error(BFRS_E_WRAPPER, "manifest: block " + std::to_string(b) + " shape");
+    }
+  }
+  return BFRS_OK;
+}
+
+}  // namespace bfrs

@@ -1,0 +1,182 @@
+// gpu_block.cpp — see gpu_block.hpp.
+#include "gpu_block.hpp"
+
+#include "blake3.hpp"
+
+#include <algorithm>
+#include <cstring>
+#include <sstream>
+
+namespace bfrs {
+
+Arena::~Arena() {
+  if (h) (void)hipHostFree(h);
+  if (d) (void)hipFree(d);
+}
+
+int Arena::reserve(size_t slot_bytes, size_t n) {
+  slot_bytes = std::max<size_t>(256, (slot_bytes + 255) / 256 * 256);
+  n = std::max<size_t>(1, n);
+  if (h && slot_bytes <= slot && n <= nslots) return BFRS_OK;
+  if (h) {
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipHostFree(h));
+    h = nullptr;
+  }
+  if (d) {
+    HIP_TRY(hipFree(d));
+    d = nullptr;
+  }
+  slot = std::max(slot, slot_bytes);
+  nslots = std::max(nslots, n);
+  HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&h), slot * nslots, hipHostMallocDefault));
+  HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d), slot * nslots));
+  return BFRS_OK;
+}
+
+int gpu_hash_hex(bfrs_ctx *ctx, const std::vector<const uint8_t *> &d_msgs,
+                 const std::vector<size_t> &lens, std::vector<std::string> *hex,
+                 const uint64_t *chunk_offsets, std::vector<uint8_t> *cvs) {
+  const size_t n = d_msgs.size();
+  std::vector<uint8_t> dig(n * 32);
+  if (cvs) cvs->assign(n * 32, 0);
+  int rc = ctx->impl.blake3_dev(n, d_msgs.data(), lens.data(), chunk_offsets, dig.data(),
+                                cvs ? cvs->data() : nullptr, ctx->impl.stream);
+  if (rc) return rc;
+  hex->resize(n);
+  for (size_t i = 0; i < n; ++i) (*hex)[i] = to_hex(dig.data() + 32 * i, 32);
+  return BFRS_OK;
+}
+
+size_t BlockState::damaged_segments() const {
+  size_t n = 0;
+  for (uint8_t v : seg_ok) n += !v;
+  return n;
+}
+
+size_t BlockState::valid_parity() const {
+  size_t n = 0;
+  for (uint8_t v : par_ok) n += v;
+  return n;
+}
+
+int load_block(bfrs_ctx *ctx, const Geometry &g, size_t b, Arena &a, BlockState *st) {
+  auto it = g.mf.blocks.find(int64_t(b));
+  if (it == g.mf.blocks.end()) return set_error(BFRS_E_WRAPPER, "manifest has no block " + std::to_string(b));
+  const BlockHashes &bh = it->second;
+  st->b = b;
+  st->k = bh.segments.size();
+  st->shard = g.block_shard(b);
+  const size_t k = st->k, shard = st->shard;
+  st->lens.resize(k);
+  for (size_t s = 0; s < k; ++s) st->lens[s] = g.seg_len(b * kBlockSegments + s);
+  int rc = a.reserve(shard, k + kParity);
+  if (rc) return rc;
+  std::vector<uint8_t> readable(k + kParity, 0);
+  parallel_for(k + kParity, hw_threads(), [&](size_t i) {
+    if (i < k) {
+      const long long n = read_file_into(t3_seg(g.dir, b, i), a.hs(i), a.slot);
+      readable[i] = n == (long long)st->lens[i];
+      if (readable[i] && st->lens[i] < shard)  // generate.rs:75-82 zero padding
+        std::memset(a.hs(i) + st->lens[i], 0, shard - st->lens[i]);
+    } else {
+      readable[i] = read_file_into(t3_par(g.dir, b, i - k), a.hs(i), a.slot) == (long long)shard;
+    }
+  });
+  Context &c = ctx->impl;
+  HIP_TRY(hipSetDevice(c.device));
+  HIP_TRY(hipMemcpyAsync(a.d, a.h, a.slot * (k + kParity), hipMemcpyHostToDevice, c.stream));
+  std::vector<const uint8_t *> msgs;
+  std::vector<size_t> lens, idx;
+  for (size_t i = 0; i < k + kParity; ++i)
+    if (readable[i]) {
+      msgs.push_back(a.ds(i));
+      lens.push_back(i < k ? st->lens[i] : shard);
+      idx.push_back(i);
+    }
+  std::vector<std::string> hex;
+  if ((rc = gpu_hash_hex(ctx, msgs, lens, &hex))) return rc;
+  st->seg_ok.assign(k, 0);
+  st->par_ok.assign(kParity, 0);
+  for (size_t j = 0; j < idx.size(); ++j) {
+    const size_t i = idx[j];
+    if (i < k)
+      st->seg_ok[i] = hex[j] == bh.segments[i];
+    else
+      st->par_ok[i - k] = hex[j] == bh.parity[i - k];
+  }
+  return BFRS_OK;
+}
+
+int restore_block(bfrs_ctx *ctx, const Geometry &g, Arena &a, BlockState &st) {
+  const size_t k = st.k, erased = st.damaged_segments(), present = st.valid_parity();
+  if (erased == 0) return 0;
+  if (erased > present) {
+    std::ostringstream os;
+    os << "block " << st.b << ": " << erased << " damaged segments but only " << present
+       << " valid parity shards - unrecoverable";
+    return set_error(BFRS_E_NOT_ENOUGH_SHARDS, os.str());
+  }
+  std::vector<const uint8_t *> orig(k), rec(kParity);
+  std::vector<uint8_t *> out(k);
+  for (size_t s = 0; s < k; ++s) {
+    orig[s] = st.seg_ok[s] ? a.ds(s) : nullptr;
+    out[s] = a.ds(s);  // written only where erased: the restored segment lands in its own slot
+  }
+  for (size_t p = 0; p < kParity; ++p) rec[p] = st.par_ok[p] ? a.ds(k + p) : nullptr;
+  Context &c = ctx->impl;
+  const uint32_t kk = uint32_t(k);
+  int rc = decode_batch_on(ctx, 1, &kk, kParity, st.shard, orig.data(), rec.data(), out.data(),
+                           c.stream);
+  if (rc) return rc;
+  // src/merkle_tree re-verify of the reconstructed bytes, on the device
+  std::vector<const uint8_t *> msgs;
+  std::vector<size_t> lens, idx;
+  for (size_t s = 0; s < k; ++s)
+    if (!st.seg_ok[s]) {
+      msgs.push_back(a.ds(s));
+      lens.push_back(st.lens[s]);
+      idx.push_back(s);
+    }
+  std::vector<std::string> hex;
+  if ((rc = gpu_hash_hex(ctx, msgs, lens, &hex))) return rc;
+  const BlockHashes &bh = g.mf.blocks.at(int64_t(st.b));
+  for (size_t j = 0; j < idx.size(); ++j)
+    if (hex[j] != bh.segments[idx[j]]) {
+      std::ostringstream os;
+      os << "block " << st.b << " segment " << idx[j] << ": restored bytes fail the manifest hash";
+      return set_error(BFRS_E_WRAPPER, os.str());
+    }
+  for (size_t s : idx)
+    HIP_TRY(hipMemcpyAsync(a.hs(s), a.ds(s), st.shard, hipMemcpyDeviceToHost, c.stream));
+  HIP_TRY(hipStreamSynchronize(c.stream));
+  for (size_t s : idx) st.seg_ok[s] = 1;
+  return int(idx.size());
+}
+
+int reencode_parity(bfrs_ctx *ctx, const Geometry &g, Arena &a, BlockState &st) {
+  const size_t k = st.k;
+  if (st.damaged_segments()) return set_error(BFRS_E_WRAPPER, "re-encode needs whole data");
+  std::vector<const uint8_t *> orig(k);
+  std::vector<uint8_t *> rec(kParity);
+  for (size_t s = 0; s < k; ++s) orig[s] = a.ds(s);
+  for (size_t p = 0; p < kParity; ++p) rec[p] = a.ds(k + p);
+  Context &c = ctx->impl;
+  const uint32_t kk = uint32_t(k);
+  int rc = encode_batch_on(ctx, 1, &kk, kParity, st.shard, orig.data(), rec.data(), c.stream);
+  if (rc) return rc;
+  std::vector<const uint8_t *> msgs(rec.begin(), rec.end());
+  std::vector<size_t> lens(kParity, st.shard);
+  std::vector<std::string> hex;
+  if ((rc = gpu_hash_hex(ctx, msgs, lens, &hex))) return rc;
+  const BlockHashes &bh = g.mf.blocks.at(int64_t(st.b));
+  for (size_t p = 0; p < kParity; ++p)
+    if (hex[p] != bh.parity[p])
+      return set_error(BFRS_E_WRAPPER, "re-encoded parity fails the manifest hash");
+  HIP_TRY(hipMemcpyAsync(a.hs(k), a.ds(k), a.slot * kParity, hipMemcpyDeviceToHost, c.stream));
+  HIP_TRY(hipStreamSynchronize(c.stream));
+  for (size_t p = 0; p < kParity; ++p) st.par_ok[p] = 1;
+  return BFRS_OK;
+}
+
+}  // namespace bfrs

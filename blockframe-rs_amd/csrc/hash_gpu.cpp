@@ -15,7 +15,8 @@ size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 }  // namespace
 
 int Context::blake3_dev(size_t n, const uint8_t *const *d_msgs, const size_t *lens,
-                        uint8_t *digests, uint8_t *cvs, hipStream_t s) {
+                        const uint64_t *chunk_offsets, uint8_t *digests, uint8_t *cvs,
+                        hipStream_t s) {
   if (n == 0) return BFRS_OK;
   if (!d_msgs || !lens || !digests)
     return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_blake3_batch_dev: NULL argument");
@@ -36,7 +37,7 @@ int Context::blake3_dev(size_t n, const uint8_t *const *d_msgs, const size_t *le
     for (size_t g = 0; g < ng; ++g) {
       HashGroup h{};
       h.addr = reinterpret_cast<uint64_t>(d_msgs[i]) + uint64_t(g) * kGroupBytes;
-      h.chunk0 = uint64_t(g) * kGroupChunks;
+      h.chunk0 = (chunk_offsets ? chunk_offsets[i] : 0) + uint64_t(g) * kGroupChunks;
       const size_t rem = lens[i] - g * size_t(kGroupBytes);
       h.nbytes = uint32_t(lens[i] == 0 ? 0 : (rem < kGroupBytes ? rem : kGroupBytes));
       h.msg = uint32_t(i);
@@ -142,9 +143,10 @@ int Context::blake3_dev(size_t n, const uint8_t *const *d_msgs, const size_t *le
 extern "C" {
 
 int bfrs_blake3_batch_dev(bfrs_ctx *ctx, size_t n, const uint8_t *const *d_msgs, const size_t *lens,
-                          uint8_t *digests_out, uint8_t *cvs_out, void *hip_stream) {
+                          const uint64_t *chunk_offsets, uint8_t *digests_out, uint8_t *cvs_out,
+                          void *hip_stream) {
   if (!ctx) return bfrs::set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_blake3_batch_dev: NULL context");
-  return ctx->impl.blake3_dev(n, d_msgs, lens, digests_out, cvs_out,
+  return ctx->impl.blake3_dev(n, d_msgs, lens, chunk_offsets, digests_out, cvs_out,
                               static_cast<hipStream_t>(hip_stream));
 }
 

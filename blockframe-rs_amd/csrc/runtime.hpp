@@ -76,9 +76,12 @@ struct Context {
   ~Context();
   int init(int dev);
   // BLAKE3 of n device messages; digests (and subtree CVs if cvs != NULL)
-  // land in host memory, n * 32 bytes each.  Synchronises `stream`.
-  int blake3_dev(size_t n, const uint8_t *const *d_msgs, const size_t *lens, uint8_t *digests,
-                 uint8_t *cvs, hipStream_t stream);
+  // land in host memory, n * 32 bytes each.  chunk_offsets (may be NULL)
+  // shifts each message's chunk counters (its position in an enclosing
+  // message, for CVs).  Synchronises `stream`.
+  int blake3_dev(size_t n, const uint8_t *const *d_msgs, const size_t *lens,
+                 const uint64_t *chunk_offsets, uint8_t *digests, uint8_t *cvs,
+                 hipStream_t stream);
   int get_encode_plan(size_t k, size_t m, const Plan **out);
   int get_decode_plan(size_t k, size_t m, const std::vector<uint8_t> &orig_present,
                       const std::vector<uint8_t> &rec_present, const Plan **out);

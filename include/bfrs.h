@@ -193,10 +193,14 @@ int bfrs_blake3_hex(const uint8_t *data, size_t len, int threads, char *out65);
  * d_msgs[i] must be 16-byte aligned (NULL allowed when lens[i] == 0).
  * digests_out: host, n * 32 bytes.  cvs_out (may be NULL): host, n * 32
  * bytes, each message's subtree chaining value, for bfrs_blake3_combine.
+ * chunk_offsets (may be NULL = all 0): message i's first BLAKE3 chunk
+ * counter.  A part of a larger message hashed at its chunk offset yields the
+ * CV of its node in that message's tree (digests_out is then meaningless);
+ * at offset 0 it yields the part's own digest.
  * Work is queued on hip_stream (NULL = HIP default) and waited for. */
 int bfrs_blake3_batch_dev(bfrs_ctx *ctx, size_t n, const uint8_t *const *d_msgs,
-                          const size_t *lens, uint8_t *digests_out, uint8_t *cvs_out,
-                          void *hip_stream);
+                          const size_t *lens, const uint64_t *chunk_offsets, uint8_t *digests_out,
+                          uint8_t *cvs_out, void *hip_stream);
 /* Digest of a whole message from the CVs of its n >= 2 consecutive parts,
  * where every part but the last has the same power-of-two number of KiB (the
  * file hash of commit.rs:478 from per-segment CVs of 32 MiB segments). */
@@ -245,10 +249,11 @@ int bfrs_repair(bfrs_ctx *ctx, const char *archive_dir, bfrs_repair_report *repo
 typedef struct bfrs_archive bfrs_archive;
 typedef struct {
   uint64_t hits, misses;
-  uint64_t verified;            /* misses served from a segment that hashed clean */
+  uint64_t verified;            /* segments loaded that hashed clean (GPU BLAKE3) */
   uint64_t recoveries;          /* decode calls */
   uint64_t recovered_segments;  /* segments restored by those calls */
   uint64_t bytes_served;
+  uint64_t prefetched;          /* segments loaded + verified ahead of the reader */
 } bfrs_archive_stats;
 int bfrs_archive_open(bfrs_ctx *ctx, const char *archive_dir, size_t cache_segments,
                       int write_back, bfrs_archive **out);

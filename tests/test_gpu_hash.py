@@ -60,8 +60,12 @@ def test_gpu_file_hash_from_segment_cvs(ctx, bfrs, oracle, part, nparts, tail):
                                                        dtype=np.uint8)
     d = _dev(data)
     segs = [d[i:i + part] for i in range(0, data.size, part)]
-    _, cvs = ctx.blake3_batch_dev(segs, with_cvs=True)
+    offs = [i * (part // K) for i in range(len(segs))]
+    _, cvs = ctx.blake3_batch_dev(segs, with_cvs=True, chunk_offsets=offs)
     assert bfrs.blake3_combine(cvs) == oracle.blake3_hex(data)
+    # at offset 0 the same call gives each segment's own digest
+    assert ctx.blake3_batch_dev(segs) == [oracle.blake3_hex(data[i:i + part])
+                                          for i in range(0, data.size, part)]
 
 
 def test_gpu_blake3_errors(ctx, bfrs):
