@@ -36,6 +36,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--settle-ms", type=float, default=1000.0,
+                    help="untimed steps until this much wall time has passed, before the W "
+                         "warmup steps: the GPU's clocks ramp over the first ~30 launches "
+                         "(rocprof trace: 1.33 ms -> 0.92 ms per launch)")
     ap.add_argument("--segments", type=int, default=128, help="segments per GPU (C2: 128)")
     ap.add_argument("--segment-bytes", type=int, default=32 * 1024 * 1024)
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
@@ -195,6 +199,13 @@ def main():
         encode(sh)
         decode(sh)
 
+    settle_steps = 0
+    t_settle = time.perf_counter()
+    while (time.perf_counter() - t_settle) * 1e3 < args.settle_ms:
+        step()
+        settle_steps += 1
+        if settle_steps % 16 == 0:
+            torch.cuda.synchronize()
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -271,6 +282,8 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "settle": {"ms": args.settle_ms, "steps": settle_steps,
+                   "note": "untimed clock-settle steps before the warmup"},
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True,
         "scaling": scaling,

@@ -8,9 +8,9 @@ OUT=gpurun_out
 TAG=${TAG:-r01}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-CMD="python3 bench.py --steps ${STEPS:-10} --warmup 3 --cpu-baseline off"
+CMD="python3 bench.py --steps ${STEPS:-50} --warmup 30 --cpu-baseline off --pcie off"
 
-timeout -k 10 600 python3 bench.py --steps 20 --warmup 5 ${BENCH_EXTRA:-} > "$OUT/bench_$TAG.log" 2>&1
+timeout -k 10 600 python3 bench.py ${BENCH_EXTRA:-} > "$OUT/bench_$TAG.log" 2>&1
 rc=$?; echo "bench rc=$rc"; tail -1 "$OUT/bench_$TAG.log"; [ $rc -eq 0 ] || exit $rc
 
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
