@@ -209,12 +209,8 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    # correctness guard on the measured buffers (cheap: compare on device)
-    seg = 0
-    for b, k in enumerate(shapes):
-        for t, i in enumerate(erased[b]):
-            assert torch.equal(restored[3 * b + t], data[seg + i]), "decode mismatch"
-        seg += k
+    # (the correctness guard runs after the timed region: host work here would
+    # idle the GPU and the timed region would start on ramping clocks again)
 
     # Timed region: K steps between a barrier + synchronize on both sides.
     # HIP events on the launch stream bracket the same region: every launch
@@ -245,6 +241,12 @@ def main():
         torch.cuda.synchronize()
         return a.elapsed_time(b) / n
     enc_ms, dec_ms = per_launch(encode), per_launch(decode)
+    # correctness guard on the measured buffers (compare on device)
+    seg = 0
+    for b, k in enumerate(shapes):
+        for t, i in enumerate(erased[b]):
+            assert torch.equal(restored[3 * b + t], data[seg + i]), "decode mismatch"
+        seg += k
     data_bytes = sum(shapes) * S                     # original data per direction (this rank)
     alg_bytes = sum(k + 3 for k in shapes) * S        # HBM bytes per launch (both directions)
     scaling = "strong" if args.strong else "weak"
