@@ -1,0 +1,59 @@
+"""Static ISA check of the product's HIP kernels (CPU: hipcc cross-compiles).
+
+The RS kernel issues its global loads/stores from inline asm with a scalar
+base (saddr).  gfx9-family hardware needs 5 wait states between a VALU write
+of an SGPR (v_readfirstlane, v_readlane, ...) and a VMEM instruction reading
+that SGPR; the compiler's hazard recognizer inserts them for its own
+instructions but not inside inline asm.  A stale base is an illegal address,
+i.e. a GPU fault.  This test keeps every saddr fed by SMEM/SALU only.
+"""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "blockframe-rs_amd", "csrc")
+HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+
+
+def _isa(src, tmp_path):
+    out = tmp_path / (os.path.basename(src) + ".s")
+    subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "--cuda-device-only",
+                    "-S", "-I", CSRC, "-o", str(out), src], check=True, capture_output=True)
+    return out.read_text().split("\n")
+
+
+def _hazards(lines, window=6):
+    hits = []
+    for i, l in enumerate(lines):
+        m = re.search(r"global_(load|store)_dwordx\d+ .*?, s\[(\d+):(\d+)\]", l)
+        if not m:
+            continue
+        lo, hi = int(m.group(2)), int(m.group(3))
+        prev = [x for x in lines[max(0, i - 3 * window):i]
+                if x.strip() and not x.strip().startswith((";", "."))][-window:]
+        for w in prev:
+            mm = re.match(r"\s*v_\w+\s+s(\d+),", w) or re.match(r"\s*v_\w+\s+s\[(\d+):\d+\]", w)
+            if mm and lo <= int(mm.group(1)) <= hi and "s_nop" not in "".join(prev):
+                hits.append((i, w.strip(), l.strip()))
+    return hits
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+@pytest.mark.parametrize("src", ["rs_kernels.hip", "blake3_kernels.hip"])
+def test_no_valu_sgpr_to_vmem_hazard(src, tmp_path):
+    lines = _isa(os.path.join(CSRC, src), tmp_path)
+    assert any("global_" in l for l in lines)
+    assert _hazards(lines) == []
+
+
+def test_hazard_detector_flags_the_pattern():
+    bad = ["\tv_readfirstlane_b32 s15, v33", "\tv_readfirstlane_b32 s14, v32",
+           "\t;;#ASMSTART", "\tglobal_load_dwordx4 v[36:39], v40, s[14:15]"]
+    assert len(_hazards(bad)) == 2
+    ok = ["\ts_load_dwordx2 s[14:15], s[6:7], 0x0", "\ts_waitcnt lgkmcnt(0)",
+          "\tglobal_load_dwordx4 v[36:39], v40, s[14:15]"]
+    assert _hazards(ok) == []

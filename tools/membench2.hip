@@ -30,23 +30,21 @@
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+// Shard addresses travel in the kernarg segment (as in the product kernel):
+// the compiler fetches them with s_load (SMEM), never through a VALU write of
+// an SGPR.  A v_readfirstlane-produced SGPR used as the saddr of the next
+// inline-asm VMEM instruction is a hazard (5 wait states) the compiler does
+// not see inside asm: the first version of this probe did that and faulted.
 struct Args {
-  const uint64_t *in;   // K * B shard addresses
-  const uint64_t *out;  // 3 * B
+  uint64_t in[120];  // K * B shard addresses
+  uint64_t out[12];  // 3 * B
   uint32_t K, B;
   uint32_t tiles_per_block;  // S / 8 KiB
   uint32_t total_tiles;      // tiles_per_block * B
 };
 
-__device__ __forceinline__ uint64_t sgpr64(uint64_t x) {
-  const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(x));
-  const uint32_t hi = __builtin_amdgcn_readfirstlane(uint32_t(x >> 32));
-  return (uint64_t(hi) << 32) | lo;
-}
-
 template <int LPOL>
-__device__ __forceinline__ void gload2(u32x4 &L, u32x4 &H, uint64_t base_v, uint32_t voff) {
-  const uint64_t base = sgpr64(base_v);
+__device__ __forceinline__ void gload2(u32x4 &L, u32x4 &H, uint64_t base, uint32_t voff) {
   if constexpr (LPOL == 0)
     asm volatile("global_load_dwordx4 %0, %2, %3\n\tglobal_load_dwordx4 %1, %2, %3 offset:32"
                  : "=&v"(L), "=&v"(H) : "v"(voff), "s"(base) : "memory");
@@ -64,8 +62,7 @@ __device__ __forceinline__ void vm_wait(u32x4 &L, u32x4 &H) {
 }
 
 template <int SPOL>
-__device__ __forceinline__ void gstore(uint64_t base_v, uint32_t voff, const u32x4 &v) {
-  const uint64_t base = sgpr64(base_v);
+__device__ __forceinline__ void gstore(uint64_t base, uint32_t voff, const u32x4 &v) {
   if constexpr (SPOL == 0)
     asm volatile("global_store_dwordx4 %0, %1, %2" ::"v"(voff), "v"(v), "s"(base) : "memory");
   else if constexpr (SPOL == 1)
@@ -79,7 +76,7 @@ __device__ __forceinline__ void do_tile(const Args &a, uint32_t t, uint32_t wave
   const uint32_t b = t / a.tiles_per_block, tile = t - b * a.tiles_per_block;
   const uint64_t hc = uint64_t(tile) * 256 + threadIdx.x;
   const uint32_t voff = uint32_t((hc >> 1) * 64 + (hc & 1) * 16);
-  const uint64_t *in = a.in + uint64_t(b) * a.K;
+  const uint64_t *in = a.in + b * a.K;
   const uint32_t K = a.K;
   const uint32_t rot = (tile * 4 + wave) % K;
   auto idx = [&](uint32_t x) -> uint32_t {
@@ -110,7 +107,7 @@ __device__ __forceinline__ void do_tile(const Args &a, uint32_t t, uint32_t wave
   }
   vm_wait<0>(LA, HA);
   if constexpr (WRITES) {
-    const uint64_t *out = a.out + uint64_t(b) * 3;
+    const uint64_t *out = a.out + b * 3;
 #pragma unroll
     for (int o = 0; o < 3; ++o) {
       gstore<SPOL>(out[o], voff, accL + u32x4{uint32_t(o), 0, 0, 0});
@@ -122,7 +119,7 @@ __device__ __forceinline__ void do_tile(const Args &a, uint32_t t, uint32_t wave
 }
 
 template <int GRID, int LPOL, int SPOL, int WRITES>
-__global__ __launch_bounds__(256) void rs_probe(Args a) {
+__global__ __launch_bounds__(256) void rs_probe(const Args a) {
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if constexpr (GRID == 0) {
     do_tile<LPOL, SPOL, WRITES>(a, blockIdx.x, wave);
@@ -187,16 +184,14 @@ int main(int argc, char **argv) {
   CHECK(hipMalloc(&par, S * 3 * B));
   CHECK(hipMemset(data, 0x5a, S * K * B));
   CHECK(hipMemset(par, 0, S * 3 * B));
-  std::vector<uint64_t> hin(K * B), hout(3 * B);
-  for (uint32_t i = 0; i < K * B; ++i) hin[i] = uint64_t(data) + S * i;
-  for (uint32_t i = 0; i < 3 * B; ++i) hout[i] = uint64_t(par) + S * i;
-  uint64_t *din, *dout;
-  CHECK(hipMalloc(&din, 8 * K * B));
-  CHECK(hipMalloc(&dout, 8 * 3 * B));
-  CHECK(hipMemcpy(din, hin.data(), 8 * K * B, hipMemcpyHostToDevice));
-  CHECK(hipMemcpy(dout, hout.data(), 8 * 3 * B, hipMemcpyHostToDevice));
   const uint32_t tpb = uint32_t(S / 8192);
-  Args a{din, dout, K, B, tpb, tpb * B};
+  Args a{};
+  for (uint32_t i = 0; i < K * B; ++i) a.in[i] = uint64_t(data) + S * i;
+  for (uint32_t i = 0; i < 3 * B; ++i) a.out[i] = uint64_t(par) + S * i;
+  a.K = K;
+  a.B = B;
+  a.tiles_per_block = tpb;
+  a.total_tiles = tpb * B;
   const double rs_bytes = double(S) * (K + 3) * B, rd_bytes = double(S) * K * B;
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
@@ -208,8 +203,11 @@ int main(int argc, char **argv) {
       hipLaunchKernelGGL((read_u<4, 0>), dim3(2048), dim3(256), 0, 0, (const u32x4 *)data,
                          (u32x4 *)par, n);
     CHECK(hipDeviceSynchronize());
+    printf("{\"settle\": \"ok\"}\n");
+    fflush(stdout);
   }
   auto time = [&](const char *name, auto launch, double nbytes) {
+    fprintf(stderr, "start %s\n", name);
     for (int i = 0; i < 3; ++i) launch();
     CHECK(hipDeviceSynchronize());
     const int iters = 20;
