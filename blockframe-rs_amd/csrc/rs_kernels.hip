@@ -129,14 +129,28 @@ __device__ __forceinline__ void store16_nt(uint64_t a, const u32x4 &v) {
 
 // Inline-asm streaming loads (see the pipeline comment in gf_apply_kernel).
 // saddr form: 64-bit wave-uniform shard base in SGPRs + 32-bit lane offset.
+// LPOL 1: non-temporal (streaming) cache policy on the loads.
+template <int LPOL = 0>
 __device__ __forceinline__ void gload_half_chunk(u32x4 &L, u32x4 &H, uint64_t base,
                                                  uint32_t voff) {
-  asm volatile(
-      "global_load_dwordx4 %0, %2, %3\n\t"
-      "global_load_dwordx4 %1, %2, %3 offset:32"
-      : "=&v"(L), "=&v"(H)
-      : "v"(voff), "s"(base)
-      : "memory");
+  if constexpr (LPOL == 1)
+    asm volatile(
+        "global_load_dwordx4 %0, %2, %3 nt\n\t"
+        "global_load_dwordx4 %1, %2, %3 offset:32 nt"
+        : "=&v"(L), "=&v"(H)
+        : "v"(voff), "s"(base)
+        : "memory");
+  else
+    asm volatile(
+        "global_load_dwordx4 %0, %2, %3\n\t"
+        "global_load_dwordx4 %1, %2, %3 offset:32"
+        : "=&v"(L), "=&v"(H)
+        : "v"(voff), "s"(base)
+        : "memory");
+}
+
+__device__ __forceinline__ void store16(uint64_t a, const u32x4 &v) {
+  *(AS_GLOBAL u32x4 *)(uintptr_t)a = v;
 }
 // Wait until at most N vector-memory ops are outstanding; L/H are in/out
 // operands so no consumer can be scheduled above the wait.
@@ -276,7 +290,7 @@ __global__ __launch_bounds__(256, VARIANT == 3 ? 7 : (VARIANT == 4 ? 8 : 1)) voi
 // after every input, so no input padding is needed; past the last input the
 // prefetch re-reads the last processed input (a cache hit, never consumed).
 // ---------------------------------------------------------------------------
-template <int NB>
+template <int NB, int LPOL = 0, int SPOL = 1>
 __global__ __launch_bounds__(256) void gf_apply_ring_kernel(const KernArgs args) {
   extern __shared__ __attribute__((aligned(16))) uint2 lds_table[];
   const PassDesc *passes = args.passes;
@@ -340,21 +354,21 @@ __global__ __launch_bounds__(256) void gf_apply_ring_kernel(const KernArgs args)
     // 4-buffer ring, 3 inputs in flight; n_in is even (host pads), exits
     // every 2 inputs keep the register allocation flat.
     u32x4 LA, HA, LB, HB, LC, HC, LD, HD;
-    gload_half_chunk(LA, HA, in[idx(0)], voff);
-    gload_half_chunk(LB, HB, in[idx(1)], voff);
-    gload_half_chunk(LC, HC, in[idx(2)], voff);
+    gload_half_chunk<LPOL>(LA, HA, in[idx(0)], voff);
+    gload_half_chunk<LPOL>(LB, HB, in[idx(1)], voff);
+    gload_half_chunk<LPOL>(LC, HC, in[idx(2)], voff);
     for (uint32_t i = 0;; i += 4) {
-      gload_half_chunk(LD, HD, in[idx(i + 3)], voff);
+      gload_half_chunk<LPOL>(LD, HD, in[idx(i + 3)], voff);
       vm_wait<6>(LA, HA);
       mac(LA, HA, i);
-      gload_half_chunk(LA, HA, in[idx(i + 4)], voff);
+      gload_half_chunk<LPOL>(LA, HA, in[idx(i + 4)], voff);
       vm_wait<6>(LB, HB);
       mac(LB, HB, i + 1);
       if (i + 2 >= n_in) break;
-      gload_half_chunk(LB, HB, in[idx(i + 5)], voff);
+      gload_half_chunk<LPOL>(LB, HB, in[idx(i + 5)], voff);
       vm_wait<6>(LC, HC);
       mac(LC, HC, i + 2);
-      gload_half_chunk(LC, HC, in[idx(i + 6)], voff);
+      gload_half_chunk<LPOL>(LC, HC, in[idx(i + 6)], voff);
       vm_wait<6>(LD, HD);
       mac(LD, HD, i + 3);
       if (i + 4 >= n_in) break;
@@ -374,8 +388,13 @@ __global__ __launch_bounds__(256) void gf_apply_ring_kernel(const KernArgs args)
         ol.x ^= pl.x; ol.y ^= pl.y; ol.z ^= pl.z; ol.w ^= pl.w;
         oh.x ^= ph.x; oh.y ^= ph.y; oh.z ^= ph.z; oh.w ^= ph.w;
       }
-      store16_nt(dst, u32x4{ol.x, ol.y, ol.z, ol.w});
-      store16_nt(dst + 32, u32x4{oh.x, oh.y, oh.z, oh.w});
+      if constexpr (SPOL == 1) {
+        store16_nt(dst, u32x4{ol.x, ol.y, ol.z, ol.w});
+        store16_nt(dst + 32, u32x4{oh.x, oh.y, oh.z, oh.w});
+      } else {
+        store16(dst, u32x4{ol.x, ol.y, ol.z, ol.w});
+        store16(dst + 32, u32x4{oh.x, oh.y, oh.z, oh.w});
+      }
     }
   }
 }
@@ -577,7 +596,8 @@ int kernel_variant() {
 // flight per wave); 1 = ping-pong (1 in flight); 0 = naive indexing;
 // 2 = contiguous-load layout; 3/4 = occupancy-bounded builds of 1; 7 = 1 with
 // an XCD-aware grid remap; 9 = traffic-only probe (refused unless
-// BFRS_ALLOW_PROBE=1).  Results of each: DESIGN.md §9.
+// BFRS_ALLOW_PROBE=1); 10/11/12 = 5 with nt loads / nt loads + plain stores /
+// plain stores.  Results of each: DESIGN.md §9.
 uint32_t tile_bytes() { return kernel_variant() == 2 ? kV2TileBytes : kTileHalfChunks * 32; }
 
 hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in,
@@ -605,6 +625,15 @@ hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in
       break;
     case 7:
       hipLaunchKernelGGL(gf_apply_kernel<7>, dim3(n_wgs), dim3(256), lds, stream, args);
+      break;
+    case 10:
+      hipLaunchKernelGGL((gf_apply_ring_kernel<3, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
+      break;
+    case 11:
+      hipLaunchKernelGGL((gf_apply_ring_kernel<3, 1, 0>), dim3(n_wgs), dim3(256), lds, stream, args);
+      break;
+    case 12:
+      hipLaunchKernelGGL((gf_apply_ring_kernel<3, 0, 0>), dim3(n_wgs), dim3(256), lds, stream, args);
       break;
 
     default:
