@@ -52,7 +52,7 @@ EXPORTS = (
     "bfrs_encode_batch_dev", "bfrs_decode_batch_dev", "bfrs_encode_host_batch",
     "bfrs_decode_host_batch", "bfrs_generate_parity",
     "bfrs_generate_parity_segmented", "bfrs_recover_segment_rs13", "bfrs_recover_segment_rs30_3",
-    "bfrs_blake3_hex", "bfrs_blake3_batch_dev", "bfrs_blake3_combine", "bfrs_merkle_root_hex", "bfrs_manifest_check", "bfrs_commit", "bfrs_repair", "bfrs_archive_open",
+    "bfrs_blake3_hex", "bfrs_blake3_batch_dev", "bfrs_blake3_combine", "bfrs_merkle_root_hex", "bfrs_manifest_check", "bfrs_commit", "bfrs_repair", "bfrs_health_check", "bfrs_archive_open",
     "bfrs_archive_size", "bfrs_archive_read", "bfrs_archive_stats_get", "bfrs_archive_close",
 )
 
@@ -152,6 +152,8 @@ def lib() -> ctypes.CDLL:
             "bfrs_commit": ([_vp, ctypes.c_char_p, ctypes.c_char_p, _sz, ctypes.c_int,
                              ctypes.c_char_p, _sz],
                             ctypes.c_int),
+            "bfrs_health_check": ([_vp, ctypes.c_char_p, ctypes.c_char_p, _sz, ctypes.POINTER(_sz)],
+                                  ctypes.c_int),
             "bfrs_repair": ([_vp, ctypes.c_char_p, ctypes.POINTER(RepairReport)], ctypes.c_int),
             "bfrs_archive_open": ([_vp, ctypes.c_char_p, _sz, ctypes.c_int, ctypes.POINTER(_vp)],
                                   ctypes.c_int),
@@ -585,6 +587,18 @@ def repair(ctx: Context, archive_dir: str) -> dict:
     rep = RepairReport()
     _check(lib().bfrs_repair(ctx.handle, os.fsencode(archive_dir), ctypes.byref(rep)))
     return rep.as_dict()
+
+
+def health_check(ctx: Context, archive_dir: str) -> dict:
+    """FileStore::health_check (src/filestore/health.rs:111-438), intended semantics."""
+    import json
+    need = _sz()
+    _check(lib().bfrs_health_check(ctx.handle, os.fsencode(archive_dir), None, 0,
+                                   ctypes.byref(need)))
+    out = ctypes.create_string_buffer(need.value)
+    _check(lib().bfrs_health_check(ctx.handle, os.fsencode(archive_dir), out, len(out),
+                                   ctypes.byref(need)))
+    return json.loads(out.value.decode())
 
 
 class Archive:

@@ -242,6 +242,17 @@ typedef struct {
  * errors. */
 int bfrs_repair(bfrs_ctx *ctx, const char *archive_dir, bfrs_repair_report *report);
 
+/* FileStore::health_check (src/filestore/health.rs:111-438), intended
+ * semantics: every shard is hashed against the manifest (tier 3: device
+ * BLAKE3), so corrupt counts like missing; each block (tier 3) or segment
+ * (tiers 1/2) is Healthy (all shards valid), Degraded (data valid, some
+ * parity not), Recoverable (damaged data <= valid parity) or Unrecoverable.
+ * Writes a JSON report with HealthReport's fields (src/filestore/models.rs:
+ * 67-82: status, recoverable, missing_data, missing_parity, corrupt_segments,
+ * details) plus corrupt_parity and per-unit counts; *needed = length + 1. */
+int bfrs_health_check(bfrs_ctx *ctx, const char *archive_dir, char *json_out, size_t cap,
+                      size_t *needed);
+
 /* Read-path core of the FUSE mount (src/mount/filesystem_unix.rs:176-305,
  * src/mount/cache.rs): offset->segment mapping, LRU segment cache,
  * BLAKE3 verification on every miss and GPU reconstruction of a corrupt or

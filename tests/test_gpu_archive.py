@@ -302,3 +302,48 @@ def test_archive_open_errors(ctx, bfrs, tmp_path):
     (tmp_path / "bad" / "manifest.json").write_text("{not json")
     with pytest.raises(bfrs.BfrsError):
         bfrs.Archive(ctx, str(tmp_path / "bad"))
+
+
+# ---------------------------------------------------------------- health check
+def test_health_check_tier3_states(ctx, bfrs, tmp_path):
+    adir, d = _tier3(ctx, bfrs, tmp_path)
+    h = bfrs.health_check(ctx, adir)
+    assert h["status"] == "Healthy" and h["recoverable"] and h["units"] == 3
+    b0 = os.path.join(adir, "blocks", "block_0")
+    os.remove(os.path.join(b0, "parity", "block_parity_1.dat"))
+    h = bfrs.health_check(ctx, adir)
+    assert h["status"] == "Degraded" and h["missing_parity"] == ["block_0/block_parity_1.dat"]
+    _flip(os.path.join(adir, "blocks", "block_1", "segments", "segment_7.dat"))
+    os.remove(os.path.join(adir, "blocks", "block_1", "segments", "segment_8.dat"))
+    h = bfrs.health_check(ctx, adir)
+    assert h["status"] == "Recoverable"
+    assert h["corrupt_segments"] == ["block_1/segment_7.dat"]
+    assert h["missing_data"] == ["block_1/segment_8.dat"]
+    assert (h["healthy"], h["degraded"], h["recoverable_units"]) == (1, 1, 1)
+    for s in (0, 1):  # block 0: 2 damaged segments but only 2 valid parity -> still recoverable
+        _flip(os.path.join(b0, "segments", f"segment_{s}.dat"))
+    assert bfrs.health_check(ctx, adir)["status"] == "Recoverable"
+    _flip(os.path.join(b0, "segments", "segment_2.dat"))  # 3 damaged > 2 valid parity
+    h = bfrs.health_check(ctx, adir)
+    assert h["status"] == "Unrecoverable" and not h["recoverable"]
+    assert h["unrecoverable_units"] == 1
+
+
+def test_health_check_tier1_tier2(ctx, bfrs, tmp_path):
+    path, _ = _file(tmp_path, 3000, seed=21, name="t1.bin")
+    a1 = bfrs.commit(ctx, path, str(tmp_path / "archive"))
+    assert bfrs.health_check(ctx, a1)["status"] == "Healthy"
+    _flip(os.path.join(a1, "parity_2.dat"))
+    h = bfrs.health_check(ctx, a1)
+    assert h["status"] == "Degraded" and h["corrupt_parity"] == ["parity_2.dat"]
+    _flip(os.path.join(a1, "data.dat"))
+    h = bfrs.health_check(ctx, a1)
+    assert h["status"] == "Recoverable" and h["corrupt_segments"] == ["data.dat"]
+    path, _ = _file(tmp_path, 2 * SEG + 5, seed=22, name="t2.bin")
+    a2 = bfrs.commit(ctx, path, str(tmp_path / "archive"), segment_size=SEG, tier=2)
+    os.remove(os.path.join(a2, "segments", "segment_1.dat"))
+    for p in range(3):
+        os.remove(os.path.join(a2, "parity", f"segment_1_parity_{p}.dat"))
+    h = bfrs.health_check(ctx, a2)
+    assert h["status"] == "Unrecoverable" and h["missing_data"] == ["segment_1.dat"]
+    assert len(h["missing_parity"]) == 3
