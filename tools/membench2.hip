@@ -133,6 +133,81 @@ __global__ __launch_bounds__(256) void rs_probe(const Args a) {
   }
 }
 
+// Write-only: the RS store pattern alone (3 output shards, 8 KiB tile per
+// workgroup, two 16-B stores per lane per output).
+template <int SPOL>
+__global__ __launch_bounds__(256) void ws_probe(const Args a) {
+  const uint32_t t = blockIdx.x;
+  const uint32_t b = t / a.tiles_per_block, tile = t - b * a.tiles_per_block;
+  const uint64_t hc = uint64_t(tile) * 256 + threadIdx.x;
+  const uint32_t voff = uint32_t((hc >> 1) * 64 + (hc & 1) * 16);
+  const u32x4 v = {t, threadIdx.x, 1, 2};
+  const uint64_t *out = a.out + b * 3;
+#pragma unroll
+  for (int o = 0; o < 3; ++o) {
+    gstore<SPOL>(out[o], voff, v);
+    gstore<SPOL>(out[o], voff + 32, v);
+  }
+}
+
+// Coarse bursts: a workgroup reads T consecutive tiles (keeping T tiles of
+// outputs in registers), then writes all T tiles' outputs together.
+template <int T, int SPOL>
+__global__ __launch_bounds__(256) void burst_probe(const Args a) {
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t t0 = blockIdx.x * T;
+  const uint32_t b = t0 / a.tiles_per_block;
+  const uint64_t *in = a.in + b * a.K;
+  const uint32_t K = a.K;
+  u32x4 accL[T], accH[T];
+  uint32_t voffs[T];
+#pragma unroll
+  for (int j = 0; j < T; ++j) {
+    const uint32_t tile = t0 + j - b * a.tiles_per_block;
+    const uint64_t hc = uint64_t(tile) * 256 + threadIdx.x;
+    const uint32_t voff = uint32_t((hc >> 1) * 64 + (hc & 1) * 16);
+    voffs[j] = voff;
+    const uint32_t rot = (tile * 4 + wave) % K;
+    auto idx = [&](uint32_t x) -> uint32_t {
+      if (x >= K) x = K - 1;
+      const uint32_t y = rot + x;
+      return y >= K ? y - K : y;
+    };
+    u32x4 aL = {0, 0, 0, 0}, aH = {0, 0, 0, 0};
+    u32x4 LA, HA, LB, HB, LC, HC, LD, HD;
+    gload2<0>(LA, HA, in[idx(0)], voff);
+    gload2<0>(LB, HB, in[idx(1)], voff);
+    gload2<0>(LC, HC, in[idx(2)], voff);
+    for (uint32_t i = 0;; i += 4) {
+      gload2<0>(LD, HD, in[idx(i + 3)], voff);
+      vm_wait<6>(LA, HA);
+      aL ^= LA; aH ^= HA;
+      gload2<0>(LA, HA, in[idx(i + 4)], voff);
+      vm_wait<6>(LB, HB);
+      aL ^= LB; aH ^= HB;
+      if (i + 2 >= K) break;
+      gload2<0>(LB, HB, in[idx(i + 5)], voff);
+      vm_wait<6>(LC, HC);
+      aL ^= LC; aH ^= HC;
+      gload2<0>(LC, HC, in[idx(i + 6)], voff);
+      vm_wait<6>(LD, HD);
+      aL ^= LD; aH ^= HD;
+      if (i + 4 >= K) break;
+    }
+    vm_wait<0>(LA, HA);
+    accL[j] = aL;
+    accH[j] = aH;
+  }
+  const uint64_t *out = a.out + b * 3;
+#pragma unroll
+  for (int j = 0; j < T; ++j)
+#pragma unroll
+    for (int o = 0; o < 3; ++o) {
+      gstore<SPOL>(out[o], voffs[j], accL[j] + u32x4{uint32_t(o), 0, 0, 0});
+      gstore<SPOL>(out[o], voffs[j] + 32, accH[j] + u32x4{uint32_t(o), 0, 0, 0});
+    }
+}
+
 // float4 copy with U independent 16-B loads in flight per lane per iteration.
 template <int U, int LPOL, int SPOL>
 __global__ __launch_bounds__(256) void copy_u(const u32x4 *__restrict__ s, u32x4 *__restrict__ d,
@@ -251,6 +326,14 @@ int main(int argc, char **argv) {
   RS(1, 0, 1, 1, 1024);
   RS(1, 1, 1, 0, 2048);
   RS(0, 0, 1, 1, 0);  // repeat baseline (drift check)
+
+  const double ws_bytes = double(S) * 3 * B;
+  time("write_only_s1", [&] { hipLaunchKernelGGL((ws_probe<1>), dim3(total), dim3(256), 0, 0, a); }, ws_bytes);
+  time("write_only_s0", [&] { hipLaunchKernelGGL((ws_probe<0>), dim3(total), dim3(256), 0, 0, a); }, ws_bytes);
+  time("burst_t2_s1", [&] { hipLaunchKernelGGL((burst_probe<2, 1>), dim3(total / 2), dim3(256), 0, 0, a); }, rs_bytes);
+  time("burst_t4_s1", [&] { hipLaunchKernelGGL((burst_probe<4, 1>), dim3(total / 4), dim3(256), 0, 0, a); }, rs_bytes);
+  time("burst_t4_s0", [&] { hipLaunchKernelGGL((burst_probe<4, 0>), dim3(total / 4), dim3(256), 0, 0, a); }, rs_bytes);
+  RS(0, 0, 1, 1, 0);  // baseline again
 
   const size_t n = S * K * B / 2 / 16;  // copy: first half of `data` -> second half
 #define CP(U, LP, SP, G)                                                                     \
