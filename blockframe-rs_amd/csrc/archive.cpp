@@ -608,23 +608,28 @@ void bfrs_archive::prefetch_loop() {
 extern "C" {
 
 int bfrs_blake3_hex(const uint8_t *data, size_t len, int threads, char *out65) {
+  BFRS_API_BEGIN
   if ((!data && len) || !out65) return set_error(BFRS_E_INVALID_ARGUMENT, "blake3: NULL argument");
   const std::string h = blake3_hex(data, len, threads);
   std::memcpy(out65, h.c_str(), 65);
   return BFRS_OK;
+  BFRS_API_END
 }
 
 int bfrs_merkle_root_hex(const char *leaves, size_t n, char *out65) {
+  BFRS_API_BEGIN
   if (!leaves || !out65 || n == 0) return set_error(BFRS_E_INVALID_ARGUMENT, "merkle: bad argument");
   std::vector<std::string> v;
   for (size_t i = 0; i < n; ++i) v.emplace_back(leaves + 64 * i, 64);
   const std::string r = merkle_root_hex(v);
   std::memcpy(out65, r.c_str(), 65);
   return BFRS_OK;
+  BFRS_API_END
 }
 
 int bfrs_manifest_check(const char *text, size_t len, int *valid, char *canonical, size_t cap,
                         size_t *needed) {
+  BFRS_API_BEGIN
   if (!text || !valid) return set_error(BFRS_E_INVALID_ARGUMENT, "manifest_check: NULL argument");
   Manifest mf;
   std::string err;
@@ -646,10 +651,12 @@ int bfrs_manifest_check(const char *text, size_t len, int *valid, char *canonica
     canonical[n] = 0;
   }
   return BFRS_OK;
+  BFRS_API_END
 }
 
 int bfrs_commit(bfrs_ctx *ctx, const char *file_path, const char *archive_root,
                 size_t segment_size, int tier, char *out_dir, size_t out_cap) {
+  BFRS_API_BEGIN
   if (!ctx || !file_path || !archive_root)
     return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_commit: NULL argument");
   Commit c{ctx, archive_root, basename_of(file_path), segment_size ? segment_size : kDefaultSegment};
@@ -673,9 +680,11 @@ int bfrs_commit(bfrs_ctx *ctx, const char *file_path, const char *archive_root,
     out_dir[out_cap - 1] = 0;
   }
   return BFRS_OK;
+  BFRS_API_END
 }
 
 int bfrs_repair(bfrs_ctx *ctx, const char *archive_dir, bfrs_repair_report *report) {
+  BFRS_API_BEGIN
   if (!ctx || !archive_dir || !report)
     return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_repair: NULL argument");
   *report = bfrs_repair_report{};
@@ -737,6 +746,7 @@ int bfrs_repair(bfrs_ctx *ctx, const char *archive_dir, bfrs_repair_report *repo
     ++report->segments_repaired;
   }
   return BFRS_OK;
+  BFRS_API_END
 }
 
 // FileStore::health_check (src/filestore/health.rs:111-438) with intended
@@ -747,6 +757,7 @@ int bfrs_repair(bfrs_ctx *ctx, const char *archive_dir, bfrs_repair_report *repo
 // (src/filestore/models.rs:67-82) plus per-tier counts.
 int bfrs_health_check(bfrs_ctx *ctx, const char *archive_dir, char *json_out, size_t cap,
                       size_t *needed) {
+  BFRS_API_BEGIN
   if (!ctx || !archive_dir) return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_health_check: NULL argument");
   Geometry g;
   int rc = load_geometry(archive_dir, &g);
@@ -848,10 +859,12 @@ int bfrs_health_check(bfrs_ctx *ctx, const char *archive_dir, char *json_out, si
     json_out[n] = 0;
   }
   return BFRS_OK;
+  BFRS_API_END
 }
 
 int bfrs_archive_open(bfrs_ctx *ctx, const char *archive_dir, size_t cache_segments,
                       int write_back, bfrs_archive **out) {
+  BFRS_API_BEGIN
   if (!ctx || !archive_dir || !out)
     return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_archive_open: NULL argument");
   *out = nullptr;
@@ -867,15 +880,19 @@ int bfrs_archive_open(bfrs_ctx *ctx, const char *archive_dir, size_t cache_segme
   if (a->prefetch) a->worker = std::thread(&bfrs_archive::prefetch_loop, a.get());
   *out = a.release();
   return BFRS_OK;
+  BFRS_API_END
 }
 
 int bfrs_archive_size(bfrs_archive *a, uint64_t *size) {
+  BFRS_API_BEGIN
   if (!a || !size) return set_error(BFRS_E_INVALID_ARGUMENT, "NULL argument");
   *size = uint64_t(a->g.mf.size);
   return BFRS_OK;
+  BFRS_API_END
 }
 
 int bfrs_archive_read(bfrs_archive *a, uint64_t offset, size_t len, uint8_t *out, size_t *nread) {
+  BFRS_API_BEGIN
   if (!a || (!out && len) || !nread) return set_error(BFRS_E_INVALID_ARGUMENT, "NULL argument");
   *nread = 0;
   const uint64_t size = uint64_t(a->g.mf.size);
@@ -919,13 +936,16 @@ int bfrs_archive_read(bfrs_archive *a, uint64_t offset, size_t len, uint8_t *out
   }
   a->st.bytes_served += *nread;
   return BFRS_OK;
+  BFRS_API_END
 }
 
 int bfrs_archive_stats_get(bfrs_archive *a, bfrs_archive_stats *out) {
+  BFRS_API_BEGIN
   if (!a || !out) return set_error(BFRS_E_INVALID_ARGUMENT, "NULL argument");
   std::lock_guard<std::mutex> g(a->mu);
   *out = a->st;
   return BFRS_OK;
+  BFRS_API_END
 }
 
 void bfrs_archive_close(bfrs_archive *a) { delete a; }

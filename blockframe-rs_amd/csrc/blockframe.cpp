@@ -36,6 +36,7 @@ extern "C" {
 int bfrs_generate_parity(bfrs_ctx *ctx, const uint8_t *const *segments, const size_t *seg_lens,
                          size_t n_segments, size_t data_shards, size_t parity_shards,
                          uint8_t *const *parity_out, size_t *parity_len) {
+  BFRS_API_BEGIN
   if (!ctx || (n_segments && (!segments || !seg_lens)) || !parity_len)
     return set_error(BFRS_E_INVALID_ARGUMENT, "generate_parity: NULL argument");
   // generate.rs:66-72 — max chunk size, error on empty input
@@ -68,10 +69,12 @@ int bfrs_generate_parity(bfrs_ctx *ctx, const uint8_t *const *segments, const si
     std::memcpy(parity_out[j], data, len);
   }
   return BFRS_OK;
+  BFRS_API_END
 }
 
 int bfrs_generate_parity_segmented(bfrs_ctx *ctx, const uint8_t *segment, size_t len,
                                    uint8_t *const *parity_out, size_t *parity_len) {
+  BFRS_API_BEGIN
   if (!ctx || (len && !segment) || !parity_len)
     return set_error(BFRS_E_INVALID_ARGUMENT, "generate_parity_segmented: NULL argument");
   // generate.rs:31-37 — RS(1,3) over the data padded to a multiple of 64
@@ -98,11 +101,13 @@ int bfrs_generate_parity_segmented(bfrs_ctx *ctx, const uint8_t *segment, size_t
     std::memcpy(parity_out[j], data, n);
   }
   return BFRS_OK;
+  BFRS_API_END
 }
 
 int bfrs_recover_segment_rs13(bfrs_ctx *ctx, const uint8_t *const *parity,
                               const size_t *parity_lens, size_t n_parity, size_t expected_size,
                               uint8_t *out, size_t *out_len) {
+  BFRS_API_BEGIN
   if (!ctx || !out_len || (n_parity && (!parity || !parity_lens)))
     return set_error(BFRS_E_INVALID_ARGUMENT, "recover_segment_rs13: NULL argument");
   if (n_parity != 3) return wrapper_error("Exactly 3 parity shards required for RS(1,3)");
@@ -125,6 +130,7 @@ int bfrs_recover_segment_rs13(bfrs_ctx *ctx, const uint8_t *const *parity,
   std::memcpy(out, data, len);
   *out_len = len;
   return BFRS_OK;
+  BFRS_API_END
 }
 
 int bfrs_recover_segment_rs30_3(bfrs_ctx *ctx, const uint8_t *const *segments,
@@ -132,6 +138,7 @@ int bfrs_recover_segment_rs30_3(bfrs_ctx *ctx, const uint8_t *const *segments,
                                 const uint8_t *const *block_parity, const size_t *parity_lens,
                                 size_t n_parity, size_t target_index, uint8_t *out,
                                 size_t *out_len) {
+  BFRS_API_BEGIN
   if (!ctx || !out_len || (n_slots && (!segments || !seg_lens)) ||
       (n_parity && (!block_parity || !parity_lens)))
     return set_error(BFRS_E_INVALID_ARGUMENT, "recover_segment_rs30_3: NULL argument");
@@ -172,6 +179,7 @@ int bfrs_recover_segment_rs30_3(bfrs_ctx *ctx, const uint8_t *const *segments,
   std::memcpy(out, data, len);
   *out_len = len;
   return BFRS_OK;
+  BFRS_API_END
 }
 
 }  // extern "C"

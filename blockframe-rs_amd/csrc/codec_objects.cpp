@@ -53,6 +53,7 @@ struct bfrs_decoder {
 extern "C" {
 
 int bfrs_encoder_new(bfrs_ctx *ctx, size_t k, size_t m, size_t shard_bytes, bfrs_encoder **out) {
+  BFRS_API_BEGIN
   if (!ctx || !out) return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_encoder_new: NULL argument");
   *out = nullptr;
   int rc = check_shape(k, m, shard_bytes);
@@ -67,9 +68,11 @@ int bfrs_encoder_new(bfrs_ctx *ctx, size_t k, size_t m, size_t shard_bytes, bfrs
   }
   *out = e;
   return BFRS_OK;
+  BFRS_API_END
 }
 
 int bfrs_encoder_add_original_shard(bfrs_encoder *e, const uint8_t *shard, size_t len) {
+  BFRS_API_BEGIN
   if (!e || !shard) return set_error(BFRS_E_INVALID_ARGUMENT, "add_original_shard: NULL argument");
   if (e->encoded) {  // the crate resets an encoder once its result is released
     e->encoded = false;
@@ -88,9 +91,11 @@ int bfrs_encoder_add_original_shard(bfrs_encoder *e, const uint8_t *shard, size_
   if (he != hipSuccess) return hip_error(he, "add_original_shard: hipMemcpy");
   ++e->received;
   return BFRS_OK;
+  BFRS_API_END
 }
 
 int bfrs_encoder_encode(bfrs_encoder *e) {
+  BFRS_API_BEGIN
   if (!e) return set_error(BFRS_E_INVALID_ARGUMENT, "encode: NULL encoder");
   if (e->received < e->k || e->encoded) {
     std::ostringstream os;
@@ -119,9 +124,11 @@ int bfrs_encoder_encode(bfrs_encoder *e) {
   if (he != hipSuccess) return hip_error(he, "encode: sync");
   e->encoded = true;
   return BFRS_OK;
+  BFRS_API_END
 }
 
 int bfrs_encoder_recovery(bfrs_encoder *e, size_t index, const uint8_t **data, size_t *len) {
+  BFRS_API_BEGIN
   if (!e || !data || !len) return set_error(BFRS_E_INVALID_ARGUMENT, "recovery: NULL argument");
   if (!e->encoded || index >= e->recovery.size()) {
     std::ostringstream os;
@@ -131,11 +138,13 @@ int bfrs_encoder_recovery(bfrs_encoder *e, size_t index, const uint8_t **data, s
   *data = e->recovery[index].data();
   *len = e->recovery[index].size();
   return BFRS_OK;
+  BFRS_API_END
 }
 
 void bfrs_encoder_free(bfrs_encoder *e) { delete e; }
 
 int bfrs_decoder_new(bfrs_ctx *ctx, size_t k, size_t m, size_t shard_bytes, bfrs_decoder **out) {
+  BFRS_API_BEGIN
   if (!ctx || !out) return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_decoder_new: NULL argument");
   *out = nullptr;
   int rc = check_shape(k, m, shard_bytes);
@@ -152,6 +161,7 @@ int bfrs_decoder_new(bfrs_ctx *ctx, size_t k, size_t m, size_t shard_bytes, bfrs
   }
   *out = d;
   return BFRS_OK;
+  BFRS_API_END
 }
 
 static void decoder_reset_if_done(bfrs_decoder *d) {
@@ -165,6 +175,7 @@ static void decoder_reset_if_done(bfrs_decoder *d) {
 
 int bfrs_decoder_add_original_shard(bfrs_decoder *d, size_t index, const uint8_t *shard,
                                     size_t len) {
+  BFRS_API_BEGIN
   if (!d || !shard) return set_error(BFRS_E_INVALID_ARGUMENT, "add_original_shard: NULL argument");
   decoder_reset_if_done(d);
   if (index >= d->k) {
@@ -185,10 +196,12 @@ int bfrs_decoder_add_original_shard(bfrs_decoder *d, size_t index, const uint8_t
   if (he != hipSuccess) return hip_error(he, "add_original_shard: hipMemcpy");
   d->orig_present[index] = 1;
   return BFRS_OK;
+  BFRS_API_END
 }
 
 int bfrs_decoder_add_recovery_shard(bfrs_decoder *d, size_t index, const uint8_t *shard,
                                     size_t len) {
+  BFRS_API_BEGIN
   if (!d || !shard) return set_error(BFRS_E_INVALID_ARGUMENT, "add_recovery_shard: NULL argument");
   decoder_reset_if_done(d);
   if (index >= d->m) {
@@ -209,9 +222,11 @@ int bfrs_decoder_add_recovery_shard(bfrs_decoder *d, size_t index, const uint8_t
   if (he != hipSuccess) return hip_error(he, "add_recovery_shard: hipMemcpy");
   d->rec_present[index] = 1;
   return BFRS_OK;
+  BFRS_API_END
 }
 
 int bfrs_decoder_decode(bfrs_decoder *d) {
+  BFRS_API_BEGIN
   if (!d) return set_error(BFRS_E_INVALID_ARGUMENT, "decode: NULL decoder");
   size_t orig_recv = 0, rec_recv = 0;
   for (uint8_t b : d->orig_present) orig_recv += b;
@@ -254,10 +269,12 @@ int bfrs_decoder_decode(bfrs_decoder *d) {
   hipError_t he = hipStreamSynchronize(c.stream);
   if (he != hipSuccess) return hip_error(he, "decode: sync");
   return BFRS_OK;
+  BFRS_API_END
 }
 
 int bfrs_decoder_restored_original(bfrs_decoder *d, size_t index, const uint8_t **data,
                                    size_t *len) {
+  BFRS_API_BEGIN
   if (!d || !data || !len)
     return set_error(BFRS_E_INVALID_ARGUMENT, "restored_original: NULL argument");
   *data = nullptr;
@@ -267,6 +284,7 @@ int bfrs_decoder_restored_original(bfrs_decoder *d, size_t index, const uint8_t 
   *data = d->restored[index].data();
   *len = d->restored[index].size();
   return BFRS_OK;
+  BFRS_API_END
 }
 
 void bfrs_decoder_free(bfrs_decoder *d) { delete d; }

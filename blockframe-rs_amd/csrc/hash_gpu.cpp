@@ -145,17 +145,21 @@ extern "C" {
 int bfrs_blake3_batch_dev(bfrs_ctx *ctx, size_t n, const uint8_t *const *d_msgs, const size_t *lens,
                           const uint64_t *chunk_offsets, uint8_t *digests_out, uint8_t *cvs_out,
                           void *hip_stream) {
+  BFRS_API_BEGIN
   if (!ctx) return bfrs::set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_blake3_batch_dev: NULL context");
   return ctx->impl.blake3_dev(n, d_msgs, lens, chunk_offsets, digests_out, cvs_out,
                               static_cast<hipStream_t>(hip_stream));
+  BFRS_API_END
 }
 
 int bfrs_blake3_combine(const uint8_t *cvs, size_t n, char *out65) {
+  BFRS_API_BEGIN
   if (!cvs || !out65 || n < 2)
     return bfrs::set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_blake3_combine: need >= 2 CVs");
   const std::string h = bfrs::blake3_combine_cvs_hex(cvs, n);
   std::memcpy(out65, h.c_str(), 65);
   return BFRS_OK;
+  BFRS_API_END
 }
 
 }  // extern "C"

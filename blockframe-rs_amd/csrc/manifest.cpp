@@ -282,7 +282,7 @@ std::string Manifest::to_json() const {
   j["size"] = Json::num(size);
   j["time_of_creation"] = Json::str(time_of_creation);
   Json ec = Json::obj();
-  ec["type"] = Json::str("reed-solomon");
+  ec["type"] = Json::str(ec_type);
   ec["data_shards"] = Json::num(data_shards);
   ec["parity_shards"] = Json::num(parity_shards);
   j["erasure_coding"] = ec;
@@ -315,6 +315,24 @@ std::string Manifest::to_json() const {
   return j.dump();
 }
 
+namespace {
+// Map keys of leaves/segments/blocks are decimal integers (serde's
+// HashMap<i32|usize, _> keys); anything else is a parse error, never an
+// exception across the C-ABI.
+bool parse_key(const std::string &k, int64_t *out) {
+  if (k.empty() || k.size() > 18) return false;
+  size_t i = k[0] == '-' ? 1 : 0;
+  if (i == k.size()) return false;
+  int64_t v = 0;
+  for (; i < k.size(); ++i) {
+    if (k[i] < '0' || k[i] > '9') return false;
+    v = v * 10 + (k[i] - '0');
+  }
+  *out = k[0] == '-' ? -v : v;
+  return true;
+}
+}  // namespace
+
 bool Manifest::from_json(const std::string &text, Manifest *m, std::string *err) {
   Json j;
   if (!Json::parse(text, &j, err)) return false;
@@ -342,13 +360,22 @@ bool Manifest::from_json(const std::string &text, Manifest *m, std::string *err)
   if (!need(ec, Json::kObject, "erasure_coding")) return false;
   if ((v = ec->get("data_shards")) && v->kind == Json::kInt) m->data_shards = int(v->i);
   if ((v = ec->get("parity_shards")) && v->kind == Json::kInt) m->parity_shards = int(v->i);
+  if ((v = ec->get("type")) && v->kind == Json::kString) m->ec_type = v->s;
   const Json *mt = j.get("merkle_tree");
   if (!need(mt, Json::kObject, "merkle_tree")) return false;
   if (!need(v = mt->get("root"), Json::kString, "merkle_tree.root")) return false;
   m->root = v->s;
+  auto key = [&](const std::string &k, int64_t *out) {
+    if (parse_key(k, out)) return true;
+    if (err) *err = "manifest: map key '" + k + "' is not an integer";
+    return false;
+  };
+  int64_t id;
   if ((v = mt->get("leaves")) && v->kind == Json::kObject)
-    for (const auto &kv : v->o)
-      if (kv.second.kind == Json::kString) m->leaves[std::stoll(kv.first)] = kv.second.s;
+    for (const auto &kv : v->o) {
+      if (!key(kv.first, &id)) return false;
+      if (kv.second.kind == Json::kString) m->leaves[id] = kv.second.s;
+    }
   if ((v = mt->get("segments")) && v->kind == Json::kObject)
     for (const auto &kv : v->o) {
       SegmentHashes sh;
@@ -358,7 +385,8 @@ bool Manifest::from_json(const std::string &text, Manifest *m, std::string *err)
         return false;
       }
       sh.data = d->s;
-      m->segments[std::stoll(kv.first)] = sh;
+      if (!key(kv.first, &id)) return false;
+      m->segments[id] = sh;
     }
   if ((v = mt->get("blocks")) && v->kind == Json::kObject)
     for (const auto &kv : v->o) {
@@ -368,7 +396,8 @@ bool Manifest::from_json(const std::string &text, Manifest *m, std::string *err)
         if (err) *err = "manifest: bad blocks entry";
         return false;
       }
-      m->blocks[std::stoll(kv.first)] = bh;
+      if (!key(kv.first, &id)) return false;
+      m->blocks[id] = bh;
     }
   return true;
 }

@@ -65,6 +65,7 @@ struct SegmentHashes {
 };
 struct Manifest {
   std::string original_hash, name, time_of_creation, root;
+  std::string ec_type = "reed-solomon";  // io.rs:141 writes "reed-solomon"
   int64_t size = 0;
   int tier = 0;
   uint64_t segment_size = 0;

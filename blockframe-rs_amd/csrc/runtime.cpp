@@ -355,12 +355,15 @@ const char *bfrs_strerror(int code) {
 const char *bfrs_last_error(void) { return g_last_error.c_str(); }
 
 int bfrs_device_count(void) {
+  BFRS_API_BEGIN
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
   return n;
+  BFRS_API_END
 }
 
 int bfrs_open(int device, bfrs_ctx **out) {
+  BFRS_API_BEGIN
   if (!out) return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_open: out is NULL");
   *out = nullptr;
   auto *c = new (std::nothrow) bfrs_ctx;
@@ -372,24 +375,30 @@ int bfrs_open(int device, bfrs_ctx **out) {
   }
   *out = c;
   return BFRS_OK;
+  BFRS_API_END
 }
 
 void bfrs_close(bfrs_ctx *ctx) { delete ctx; }
 
 int bfrs_synchronize(bfrs_ctx *ctx) {
+  BFRS_API_BEGIN
   if (!ctx) return set_error(BFRS_E_INVALID_ARGUMENT, "NULL context");
   HIP_TRY(hipSetDevice(ctx->impl.device));
   HIP_TRY(hipStreamSynchronize(ctx->impl.stream));
   return BFRS_OK;
+  BFRS_API_END
 }
 
 int bfrs_use_high_rate(size_t k, size_t m) {
+  BFRS_API_BEGIN
   Rate r;
   if (!choose_rate(k, m, &r)) return BFRS_E_UNSUPPORTED_SHARD_COUNT;
   return r == Rate::kHigh ? 1 : 0;
+  BFRS_API_END
 }
 
 int bfrs_encode_coefficient(size_t k, size_t m, size_t j, size_t i, uint16_t *coef_out) {
+  BFRS_API_BEGIN
   if (!coef_out) return set_error(BFRS_E_INVALID_ARGUMENT, "coef_out is NULL");
   int rc = check_shape(k, m, 2);
   if (rc) return rc;
@@ -397,10 +406,12 @@ int bfrs_encode_coefficient(size_t k, size_t m, size_t j, size_t i, uint16_t *co
   CoefMatrix c = plan_encode(k, m);
   *coef_out = c.at(j, i);
   return BFRS_OK;
+  BFRS_API_END
 }
 
 int bfrs_plan_decode(size_t k, size_t m, const uint8_t *orig_present, const uint8_t *rec_present,
                      uint16_t *coef_out, size_t cap, size_t *rows, size_t *cols) {
+  BFRS_API_BEGIN
   if (!orig_present || !rec_present || !rows || !cols)
     return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_plan_decode: NULL argument");
   int rc = check_shape(k, m, 2);
@@ -420,6 +431,7 @@ int bfrs_plan_decode(size_t k, size_t m, const uint8_t *orig_present, const uint
   *cols = c.cols;
   if (coef_out && cap >= c.c.size()) std::copy(c.c.begin(), c.c.end(), coef_out);
   return BFRS_OK;
+  BFRS_API_END
 }
 
 // ---- batch (device-resident) ------------------------------------------------
@@ -433,16 +445,20 @@ int check_dev_ptr(const void *p, const char *what) {
 int bfrs_encode_batch_dev(bfrs_ctx *ctx, size_t nblocks, const uint32_t *ks, size_t m,
                           size_t shard_bytes, const uint8_t *const *d_orig,
                           uint8_t *const *d_rec, void *hip_stream) {
+  BFRS_API_BEGIN
   return encode_batch_on(ctx, nblocks, ks, m, shard_bytes, d_orig, d_rec,
                          static_cast<hipStream_t>(hip_stream));
+  BFRS_API_END
 }
 
 int bfrs_decode_batch_dev(bfrs_ctx *ctx, size_t nblocks, const uint32_t *ks, size_t m,
                           size_t shard_bytes, const uint8_t *const *d_orig,
                           const uint8_t *const *d_rec, uint8_t *const *d_restored,
                           void *hip_stream) {
+  BFRS_API_BEGIN
   return decode_batch_on(ctx, nblocks, ks, m, shard_bytes, d_orig, d_rec, d_restored,
                          static_cast<hipStream_t>(hip_stream));
+  BFRS_API_END
 }
 
 }  // extern "C"
@@ -567,40 +583,48 @@ static int check_host_batch(bfrs_ctx *ctx, size_t nblocks, const uint32_t *ks, s
 int bfrs_encode_host_batch(bfrs_ctx *ctx, size_t nblocks, const uint32_t *ks, size_t m,
                            size_t shard_bytes, const uint8_t *const *orig,
                            uint8_t *const *rec_out) {
+  BFRS_API_BEGIN
   int rc = check_host_batch(ctx, nblocks, ks, m, shard_bytes, false, orig, nullptr, rec_out);
   if (rc) return rc;
   HIP_TRY(hipSetDevice(ctx->impl.device));
   return ctx->impl.run_host(false, nblocks, ks, m, shard_bytes, orig, nullptr, rec_out);
+  BFRS_API_END
 }
 
 int bfrs_decode_host_batch(bfrs_ctx *ctx, size_t nblocks, const uint32_t *ks, size_t m,
                            size_t shard_bytes, const uint8_t *const *orig,
                            const uint8_t *const *rec, uint8_t *const *restored_out) {
+  BFRS_API_BEGIN
   int rc = check_host_batch(ctx, nblocks, ks, m, shard_bytes, true, orig, rec, restored_out);
   if (rc) return rc;
   HIP_TRY(hipSetDevice(ctx->impl.device));
   return ctx->impl.run_host(true, nblocks, ks, m, shard_bytes, orig, rec, restored_out);
+  BFRS_API_END
 }
 
 int bfrs_encode(bfrs_ctx *ctx, size_t k, size_t m, size_t shard_bytes,
                 const uint8_t *const *originals, uint8_t *const *recovery_out) {
+  BFRS_API_BEGIN
   if (!ctx || !originals || !recovery_out)
     return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_encode: NULL argument");
   int rc = check_shape(k, m, shard_bytes);
   if (rc) return rc;
   const uint32_t kk = uint32_t(k);
   return bfrs_encode_host_batch(ctx, 1, &kk, m, shard_bytes, originals, recovery_out);
+  BFRS_API_END
 }
 
 int bfrs_decode(bfrs_ctx *ctx, size_t k, size_t m, size_t shard_bytes,
                 const uint8_t *const *originals, const uint8_t *const *recovery,
                 uint8_t *const *restored_out) {
+  BFRS_API_BEGIN
   if (!ctx || !originals || !recovery || !restored_out)
     return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_decode: NULL argument");
   int rc = check_shape(k, m, shard_bytes);
   if (rc) return rc;
   const uint32_t kk = uint32_t(k);
   return bfrs_decode_host_batch(ctx, 1, &kk, m, shard_bytes, originals, recovery, restored_out);
+  BFRS_API_END
 }
 
 }  // extern "C"

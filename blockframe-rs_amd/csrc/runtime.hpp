@@ -6,6 +6,8 @@
 #include <cstddef>
 #include <cstdint>
 #include <map>
+#include <new>
+#include <stdexcept>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -20,6 +22,22 @@ namespace bfrs {
 // Thread-local error reporting (bfrs_last_error).
 int set_error(int code, const std::string &msg);
 int hip_error(hipError_t e, const char *what);
+
+// Every int-returning C entry point runs inside BFRS_API_BEGIN/END: a C++
+// exception (allocation failure, malformed input reaching an .at()) becomes
+// an error code and never crosses the C-ABI (bfrs.h: never aborts).
+#define BFRS_API_BEGIN try {
+#define BFRS_API_END                                                             \
+  }                                                                              \
+  catch (const std::bad_alloc &) {                                               \
+    return bfrs::set_error(BFRS_E_NOMEM, "host memory allocation failed");       \
+  }                                                                              \
+  catch (const std::exception &ex_) {                                            \
+    return bfrs::set_error(BFRS_E_WRAPPER, std::string("internal error: ") + ex_.what()); \
+  }                                                                              \
+  catch (...) {                                                                  \
+    return bfrs::set_error(BFRS_E_WRAPPER, "internal error");                    \
+  }
 
 #define HIP_TRY(expr)                                   \
   do {                                                  \

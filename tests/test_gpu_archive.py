@@ -347,3 +347,56 @@ def test_health_check_tier1_tier2(ctx, bfrs, tmp_path):
     h = bfrs.health_check(ctx, a2)
     assert h["status"] == "Unrecoverable" and h["missing_data"] == ["segment_1.dat"]
     assert len(h["missing_parity"]) == 3
+
+
+# ---------------------------------------------------------------- src/chunker/tests.rs, mirrored
+def _const_file(tmp_path, name, size, byte=None):
+    # chunker/tests.rs:19-27: content = the name's first byte, repeated
+    p = tmp_path / name
+    p.write_bytes(bytes([byte if byte is not None else name.encode()[0]]) * size)
+    return str(p)
+
+
+def test_ref_tier_selection_tiny(ctx, bfrs, tmp_path):  # tests.rs:36-51
+    adir = bfrs.commit(ctx, _const_file(tmp_path, "tiny.txt", 1_000_000), str(tmp_path / "ar"))
+    m = _manifest(adir)
+    assert m["tier"] == 1
+    assert (m["erasure_coding"]["data_shards"], m["erasure_coding"]["parity_shards"]) == (6, 3)
+
+
+def test_ref_tier_selection_segmented(ctx, bfrs, oracle, tmp_path):  # tests.rs:53-73 (#[ignore] there)
+    adir = bfrs.commit(ctx, _const_file(tmp_path, "medium.txt", 50_000_000), str(tmp_path / "ar"))
+    m = _manifest(adir)
+    assert m["tier"] == 2 and len(m["merkle_tree"]["segments"]) > 0
+    assert (m["erasure_coding"]["data_shards"], m["erasure_coding"]["parity_shards"]) == (6, 3)
+    nseg = len(os.listdir(os.path.join(adir, "segments")))
+    assert nseg == len(m["merkle_tree"]["segments"]) == -(-50_000_000 // m["segment_size"])
+    assert m["original_hash"] == oracle.blake3_hex(b"m" * 50_000_000)
+
+
+def test_ref_commit_tiny_structure(ctx, bfrs, tmp_path):  # tests.rs:75-103
+    adir = bfrs.commit(ctx, _const_file(tmp_path, "test.txt", 500_000), str(tmp_path / "ar"))
+    for f in ["data.dat", "parity_0.dat", "parity_1.dat", "parity_2.dat", "manifest.json"]:
+        assert os.path.exists(os.path.join(adir, f)), f
+
+
+def test_ref_file_hash_is_deterministic(ctx, bfrs, tmp_path):  # tests.rs:132-149
+    a = bfrs.commit(ctx, _const_file(tmp_path, "file1.txt", 1_000_000, 42), str(tmp_path / "ar"))
+    b = bfrs.commit(ctx, _const_file(tmp_path, "file2.txt", 1_000_000, 42), str(tmp_path / "ar"))
+    ma, mb = _manifest(a), _manifest(b)
+    assert ma["original_hash"] == mb["original_hash"] and a != b
+    assert ma["merkle_tree"] == mb["merkle_tree"]
+
+
+def test_ref_merkle_root_and_size(ctx, bfrs, tmp_path):  # tests.rs:151-180
+    m = _manifest(bfrs.commit(ctx, _const_file(tmp_path, "merkle.txt", 2_000_000), str(tmp_path / "ar")))
+    assert len(m["merkle_tree"]["root"]) == 64
+    m = _manifest(bfrs.commit(ctx, _const_file(tmp_path, "sized.txt", 3_500_000), str(tmp_path / "ar")))
+    assert m["size"] == 3_500_000
+
+
+def test_ref_commit_nonexistent_and_empty(ctx, bfrs, tmp_path):  # tests.rs:182-205
+    with pytest.raises(bfrs.BfrsError):
+        bfrs.commit(ctx, str(tmp_path / "does_not_exist.txt"), str(tmp_path / "ar"))
+    with pytest.raises(bfrs.BfrsError, match="empty file"):
+        bfrs.commit(ctx, _const_file(tmp_path, "empty.txt", 0), str(tmp_path / "ar"))

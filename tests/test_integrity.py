@@ -128,3 +128,41 @@ def test_blake3_combine_from_part_cvs(bfrs, oracle, part_kib, nparts, tail):
     parts = [data[i:i + P] for i in range(0, len(data), P)]
     cvs = [b3py.subtree_cv(p, i * part_kib) for i, p in enumerate(parts)]
     assert bfrs.blake3_combine(cvs) == oracle.blake3_hex(data)
+
+
+# src/filestore/tests.rs:26-41: the reference's hand-written tier-1 manifest
+# fixture (pretty-printed, "reed_solomon", segment_size 0, no leaves).
+REF_FIXTURE_MANIFEST = """{
+    "name": "test.txt",
+    "original_hash": "abc123",
+    "size": 1000,
+    "tier": 1,
+    "segment_size": 0,
+    "time_of_creation": "2024-01-01T00:00:00Z",
+    "erasure_coding": {
+        "type": "reed_solomon",
+        "data_shards": 1,
+        "parity_shards": 3
+    },
+    "merkle_tree": {
+        "root": "0000000000000000000000000000000000000000000000000000000000000000",
+        "leaves": {}
+    }
+}"""
+
+
+def test_manifest_reference_fixture(bfrs):
+    valid, canon = bfrs.manifest_check(REF_FIXTURE_MANIFEST)
+    # parses like ManifestFile::new; validate() is false: no leaves/segments/blocks
+    assert not valid
+    assert json.loads(canon) == json.loads(REF_FIXTURE_MANIFEST)  # every field survives
+    assert canon == _canon(json.loads(REF_FIXTURE_MANIFEST))
+
+
+@pytest.mark.parametrize("key", ["abc", "", "1x", "99999999999999999999"])
+def test_manifest_bad_map_key_is_an_error_not_a_crash(bfrs, key):
+    m = _manifest(1)
+    m["merkle_tree"]["leaves"] = {key: H("a")}
+    with pytest.raises(bfrs.BfrsError) as e:
+        bfrs.manifest_check(_canon(m))
+    assert e.value.code == bfrs.E_WRAPPER
