@@ -290,13 +290,11 @@ __global__ __launch_bounds__(256, VARIANT == 3 ? 7 : (VARIANT == 4 ? 8 : 1)) voi
 // after every input, so no input padding is needed; past the last input the
 // prefetch re-reads the last processed input (a cache hit, never consumed).
 // ---------------------------------------------------------------------------
-template <int NB, int LPOL = 0, int SPOL = 1>
-__global__ __launch_bounds__(256) void gf_apply_ring_kernel(const KernArgs args) {
+// Stages this workgroup's pass tables in LDS; returns the pass.
+__device__ __forceinline__ const PassDesc &enter_pass(const KernArgs &args, uint32_t wg) {
   extern __shared__ __attribute__((aligned(16))) uint2 lds_table[];
   const PassDesc *passes = args.passes;
-  const uint32_t n_passes = args.n_passes, tiles_per_wg = args.tiles_per_wg;
-  const uint32_t wg = blockIdx.x;
-  uint32_t lo = 0, hi = n_passes;
+  uint32_t lo = 0, hi = args.n_passes;
   while (hi - lo > 1) {
     const uint32_t mid = (lo + hi) >> 1;
     if (passes[mid].wg_begin <= wg)
@@ -305,97 +303,217 @@ __global__ __launch_bounds__(256) void gf_apply_ring_kernel(const KernArgs args)
       hi = mid;
   }
   const PassDesc &P = passes[lo];
-  const uint32_t n_in = P.n_in, n_out = P.n_out;
-  const uint64_t *in = args.ptrs + P.in;
-  {
-    const AS_GLOBAL u32x4 *tab = (const AS_GLOBAL u32x4 *)(uintptr_t)P.table;
-    u32x4 *dst = reinterpret_cast<u32x4 *>(lds_table);
-    const uint32_t n16 = n_in * 32;
-    u32x4 v[kMaxPassInputs * 32 / 256];
+  const uint32_t n_in = P.n_in;
+  const AS_GLOBAL u32x4 *tab = (const AS_GLOBAL u32x4 *)(uintptr_t)P.table;
+  u32x4 *dst = reinterpret_cast<u32x4 *>(lds_table);
+  const uint32_t n16 = n_in * 32;
+  u32x4 v[kMaxPassInputs * 32 / 256];
 #pragma unroll
-    for (int r = 0; r < int(kMaxPassInputs * 32 / 256); ++r) {
-      const uint32_t e = threadIdx.x + 256u * r;
-      v[r] = e < n16 ? tab[e] : u32x4{0, 0, 0, 0};
-    }
+  for (int r = 0; r < int(kMaxPassInputs * 32 / 256); ++r) {
+    const uint32_t e = threadIdx.x + 256u * r;
+    v[r] = e < n16 ? tab[e] : u32x4{0, 0, 0, 0};
+  }
 #pragma unroll
-    for (int r = 0; r < int(kMaxPassInputs * 32 / 256); ++r) {
-      const uint32_t e = threadIdx.x + 256u * r;
-      if (e < n16) dst[e] = v[r];
-    }
+  for (int r = 0; r < int(kMaxPassInputs * 32 / 256); ++r) {
+    const uint32_t e = threadIdx.x + 256u * r;
+    if (e < n16) dst[e] = v[r];
   }
   __syncthreads();
+  return P;
+}
 
-  const uint64_t full_hc = P.full_chunks * 2;
-  const uint32_t t_begin = (wg - P.wg_begin) * tiles_per_wg;
-  const uint32_t t_end = min(t_begin + tiles_per_wg, P.n_tiles);
-  const uint32_t wave_id = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+template <int SPOL>
+__device__ __forceinline__ void store16_pol(uint64_t a, const u32x4 &v) {
+  if constexpr (SPOL == 1)
+    store16_nt(a, v);
+  else
+    store16(a, v);
+}
 
-  for (uint32_t tile = t_begin; tile < t_end; ++tile) {
-    const uint64_t hc = uint64_t(tile) * kTileHalfChunks + threadIdx.x;
-    if (hc >= full_hc) break;
-    const uint64_t off = (hc >> 1) * 64 + (hc & 1) * 16;
-    const uint32_t voff = uint32_t(off);
-    uint32_t acc_lo[16], acc_hi[16];
+// The 4-buffer input ring shared by both lane layouts: 3 inputs in flight per
+// wave; n_in is even (host pads), uniform exits every 2 inputs keep the
+// register allocation flat; past the last input the prefetch re-reads the
+// last processed input (a cache hit, never consumed).
+template <typename Load, typename Mac>
+__device__ __forceinline__ void input_ring(uint32_t n_in, const Load &load, const Mac &mac) {
+  u32x4 LA, HA, LB, HB, LC, HC, LD, HD;
+  load(LA, HA, 0);
+  load(LB, HB, 1);
+  load(LC, HC, 2);
+  for (uint32_t i = 0;; i += 4) {
+    load(LD, HD, i + 3);
+    vm_wait<6>(LA, HA);
+    mac(LA, HA, i);
+    load(LA, HA, i + 4);
+    vm_wait<6>(LB, HB);
+    mac(LB, HB, i + 1);
+    if (i + 2 >= n_in) break;
+    load(LB, HB, i + 5);
+    vm_wait<6>(LC, HC);
+    mac(LC, HC, i + 2);
+    load(LC, HC, i + 6);
+    vm_wait<6>(LD, HD);
+    mac(LD, HD, i + 3);
+    if (i + 4 >= n_in) break;
+  }
+  vm_wait<0>(LA, HA);
+}
+
+// LAYOUT 0 (v5): lane = one 32-byte half-chunk, 16 B at +0 (low bytes) and
+// 16 B at +32 (high bytes): every 128-B line is touched by two instructions.
+template <int LPOL, int SPOL>
+__device__ __forceinline__ void ring_tile_halfchunk(const KernArgs &args, const PassDesc &P,
+                                                    uint32_t tile, uint32_t wave_id) {
+  const uint32_t n_in = P.n_in, n_out = P.n_out;
+  const uint64_t *in = args.ptrs + P.in;
+  const uint64_t hc = uint64_t(tile) * kTileHalfChunks + threadIdx.x;
+  if (hc >= P.full_chunks * 2) return;
+  const uint64_t off = (hc >> 1) * 64 + (hc & 1) * 16;
+  const uint32_t voff = uint32_t(off);
+  uint32_t acc_lo[16], acc_hi[16];
 #pragma unroll
-    for (int s = 0; s < 16; ++s) acc_lo[s] = acc_hi[s] = 0;
-
-    // input index of step x (x >= n_in: repeat the last input -> cache hit)
-    const uint32_t rot = P.rotate ? (tile * 4 + wave_id) % n_in : 0;
-    auto idx = [&](uint32_t x) -> uint32_t {
-      if (x >= n_in) x = n_in - 1;
-      const uint32_t y = rot + x;
-      return y >= n_in ? y - n_in : y;
-    };
-    auto mac = [&](const u32x4 &Lv, const u32x4 &Hv, uint32_t x) {
-      const uint32_t r = idx(x);
-      mac_input_v1(make_uint4(Lv.x, Lv.y, Lv.z, Lv.w), make_uint4(Hv.x, Hv.y, Hv.z, Hv.w),
-                   nullptr, 2 * r, 2 * r + 1, acc_lo, acc_hi);
-    };
-    // 4-buffer ring, 3 inputs in flight; n_in is even (host pads), exits
-    // every 2 inputs keep the register allocation flat.
-    u32x4 LA, HA, LB, HB, LC, HC, LD, HD;
-    gload_half_chunk<LPOL>(LA, HA, in[idx(0)], voff);
-    gload_half_chunk<LPOL>(LB, HB, in[idx(1)], voff);
-    gload_half_chunk<LPOL>(LC, HC, in[idx(2)], voff);
-    for (uint32_t i = 0;; i += 4) {
-      gload_half_chunk<LPOL>(LD, HD, in[idx(i + 3)], voff);
-      vm_wait<6>(LA, HA);
-      mac(LA, HA, i);
-      gload_half_chunk<LPOL>(LA, HA, in[idx(i + 4)], voff);
-      vm_wait<6>(LB, HB);
-      mac(LB, HB, i + 1);
-      if (i + 2 >= n_in) break;
-      gload_half_chunk<LPOL>(LB, HB, in[idx(i + 5)], voff);
-      vm_wait<6>(LC, HC);
-      mac(LC, HC, i + 2);
-      gload_half_chunk<LPOL>(LC, HC, in[idx(i + 6)], voff);
-      vm_wait<6>(LD, HD);
-      mac(LD, HD, i + 3);
-      if (i + 4 >= n_in) break;
+  for (int s = 0; s < 16; ++s) acc_lo[s] = acc_hi[s] = 0;
+  // input index of step x (x >= n_in: repeat the last input -> cache hit)
+  const uint32_t rot = P.rotate ? (tile * 4 + wave_id) % n_in : 0;
+  auto idx = [&](uint32_t x) -> uint32_t {
+    if (x >= n_in) x = n_in - 1;
+    const uint32_t y = rot + x;
+    return y >= n_in ? y - n_in : y;
+  };
+  input_ring(
+      n_in, [&](u32x4 &L, u32x4 &H, uint32_t x) { gload_half_chunk<LPOL>(L, H, in[idx(x)], voff); },
+      [&](const u32x4 &Lv, const u32x4 &Hv, uint32_t x) {
+        const uint32_t r = idx(x);
+        mac_input_v1(make_uint4(Lv.x, Lv.y, Lv.z, Lv.w), make_uint4(Hv.x, Hv.y, Hv.z, Hv.w),
+                     nullptr, 2 * r, 2 * r + 1, acc_lo, acc_hi);
+      });
+  const uint64_t *outp = args.ptrs + P.out;
+  const bool accumulate = P.accumulate != 0;
+  for (uint32_t t = 0; t < n_out; ++t) {
+    uint4 ol = make_uint4(gather_byte(acc_lo, 0, t), gather_byte(acc_lo, 1, t),
+                          gather_byte(acc_lo, 2, t), gather_byte(acc_lo, 3, t));
+    uint4 oh = make_uint4(gather_byte(acc_hi, 0, t), gather_byte(acc_hi, 1, t),
+                          gather_byte(acc_hi, 2, t), gather_byte(acc_hi, 3, t));
+    const uint64_t dst = outp[t] + off;
+    if (accumulate) {
+      const uint4 pl = load16(dst), ph = load16(dst + 32);
+      ol.x ^= pl.x; ol.y ^= pl.y; ol.z ^= pl.z; ol.w ^= pl.w;
+      oh.x ^= ph.x; oh.y ^= ph.y; oh.z ^= ph.z; oh.w ^= ph.w;
     }
-    vm_wait<0>(LA, HA);
+    store16_pol<SPOL>(dst, u32x4{ol.x, ol.y, ol.z, ol.w});
+    store16_pol<SPOL>(dst + 32, u32x4{oh.x, oh.y, oh.z, oh.w});
+  }
+}
 
-    const uint64_t *outp = args.ptrs + P.out;
-    const bool accumulate = P.accumulate != 0;
-    for (uint32_t t = 0; t < n_out; ++t) {
-      uint4 ol = make_uint4(gather_byte(acc_lo, 0, t), gather_byte(acc_lo, 1, t),
-                            gather_byte(acc_lo, 2, t), gather_byte(acc_lo, 3, t));
-      uint4 oh = make_uint4(gather_byte(acc_hi, 0, t), gather_byte(acc_hi, 1, t),
-                            gather_byte(acc_hi, 2, t), gather_byte(acc_hi, 3, t));
-      const uint64_t dst = outp[t] + off;
-      if (accumulate) {
-        const uint4 pl = load16(dst), ph = load16(dst + 32);
-        ol.x ^= pl.x; ol.y ^= pl.y; ol.z ^= pl.z; ol.w ^= pl.w;
-        oh.x ^= ph.x; oh.y ^= ph.y; oh.z ^= ph.z; oh.w ^= ph.w;
-      }
-      if constexpr (SPOL == 1) {
-        store16_nt(dst, u32x4{ol.x, ol.y, ol.z, ol.w});
-        store16_nt(dst + 32, u32x4{oh.x, oh.y, oh.z, oh.w});
-      } else {
-        store16(dst, u32x4{ol.x, ol.y, ol.z, ol.w});
-        store16(dst + 32, u32x4{oh.x, oh.y, oh.z, oh.w});
+// Two 16-B loads per input at per-lane offsets vx, vy (contiguous layout).
+template <int LPOL>
+__device__ __forceinline__ void gload_pair(u32x4 &X, u32x4 &Y, uint64_t base, uint32_t vx,
+                                           uint32_t vy) {
+  if constexpr (LPOL == 1)
+    asm volatile(
+        "global_load_dwordx4 %0, %2, %4 nt\n\t"
+        "global_load_dwordx4 %1, %3, %4 nt"
+        : "=&v"(X), "=&v"(Y)
+        : "v"(vx), "v"(vy), "s"(base)
+        : "memory");
+  else
+    asm volatile(
+        "global_load_dwordx4 %0, %2, %4\n\t"
+        "global_load_dwordx4 %1, %3, %4"
+        : "=&v"(X), "=&v"(Y)
+        : "v"(vx), "v"(vy), "s"(base)
+        : "memory");
+}
+
+// Value of lane l^2 (DPP quad_perm [2,3,0,1]).
+__device__ __forceinline__ u32x4 quad_swap2(const u32x4 &v) {
+  u32x4 r;
+  r.x = uint32_t(__builtin_amdgcn_update_dpp(0, int(v.x), 0x4E, 0xF, 0xF, false));
+  r.y = uint32_t(__builtin_amdgcn_update_dpp(0, int(v.y), 0x4E, 0xF, 0xF, false));
+  r.z = uint32_t(__builtin_amdgcn_update_dpp(0, int(v.z), 0x4E, 0xF, 0xF, false));
+  r.w = uint32_t(__builtin_amdgcn_update_dpp(0, int(v.w), 0x4E, 0xF, 0xF, false));
+  return r;
+}
+
+// LAYOUT 1: contiguous lines.  A wave's 2 KiB column span is read as two
+// 1 KiB runs, lane l taking 16 B at +16l of each (whole 128-B lines per
+// instruction).  Lane l = 4*c4 + p then holds part p of chunk c4 (first run)
+// and of chunk 16+c4 (second run); parts 0/1 are low bytes, 2/3 high bytes
+// of 16 symbols.  Lanes p < 2 load the first run into X, lanes p >= 2 the
+// second, so one DPP quad swap of Y (lanes l <-> l^2) hands every lane the
+// other byte of its own 16 symbols: p < 2 owns chunk c4 (X = low, R = high),
+// p >= 2 owns chunk 16+c4 (X = high, R = low) and just swaps its two table
+// bases (2i <-> 2i+1).  Stores mirror it: a lane writes one of its output
+// halves at vx and swaps the other to its partner, which writes it at vy.
+// Needs all 64 lanes (DPP): only for waves whose span is all full chunks.
+template <int LPOL, int SPOL>
+__device__ __forceinline__ void ring_tile_contig(const KernArgs &args, const PassDesc &P,
+                                                 uint32_t tile, uint32_t wave_id) {
+  const uint32_t n_in = P.n_in, n_out = P.n_out;
+  const uint64_t *in = args.ptrs + P.in;
+  const uint32_t lane = threadIdx.x & 63, p = lane & 3;
+  const bool lowp = p < 2;
+  const uint32_t span = tile * (kTileHalfChunks * 32) + wave_id * 2048;
+  const uint32_t vx = span + (lowp ? 0u : 1024u) + 16 * lane;
+  const uint32_t vy = span + (lowp ? 1024u : 0u) + 16 * lane;
+  const uint32_t sw = lowp ? 0u : 1u;
+  uint32_t acc_lo[16], acc_hi[16];
+#pragma unroll
+  for (int s = 0; s < 16; ++s) acc_lo[s] = acc_hi[s] = 0;
+  const uint32_t rot = P.rotate ? (tile * 4 + wave_id) % n_in : 0;
+  auto idx = [&](uint32_t x) -> uint32_t {
+    if (x >= n_in) x = n_in - 1;
+    const uint32_t y = rot + x;
+    return y >= n_in ? y - n_in : y;
+  };
+  input_ring(
+      n_in, [&](u32x4 &X, u32x4 &Y, uint32_t x) { gload_pair<LPOL>(X, Y, in[idx(x)], vx, vy); },
+      [&](const u32x4 &X, const u32x4 &Y, uint32_t x) {
+        const uint32_t r = idx(x);
+        const u32x4 R = quad_swap2(Y);
+        mac_input_v1(make_uint4(X.x, X.y, X.z, X.w), make_uint4(R.x, R.y, R.z, R.w), nullptr,
+                     (2 * r) | sw, (2 * r + 1) ^ sw, acc_lo, acc_hi);
+      });
+  const uint64_t *outp = args.ptrs + P.out;
+  const bool accumulate = P.accumulate != 0;
+  for (uint32_t t = 0; t < n_out; ++t) {
+    const u32x4 ol = {gather_byte(acc_lo, 0, t), gather_byte(acc_lo, 1, t),
+                      gather_byte(acc_lo, 2, t), gather_byte(acc_lo, 3, t)};
+    const u32x4 oh = {gather_byte(acc_hi, 0, t), gather_byte(acc_hi, 1, t),
+                      gather_byte(acc_hi, 2, t), gather_byte(acc_hi, 3, t)};
+    u32x4 own = lowp ? ol : oh;
+    u32x4 other = quad_swap2(lowp ? oh : ol);
+    const uint64_t base = outp[t];
+    if (accumulate) {
+      const uint4 a = load16(base + vx), b = load16(base + vy);
+      own ^= u32x4{a.x, a.y, a.z, a.w};
+      other ^= u32x4{b.x, b.y, b.z, b.w};
+    }
+    store16_pol<SPOL>(base + vx, own);
+    store16_pol<SPOL>(base + vy, other);
+  }
+}
+
+// Variants 5 / 10-15: the ring kernel.  LAYOUT 0 = half-chunk lanes (v5),
+// LAYOUT 1 = contiguous lines + DPP (falls back to LAYOUT 0 for a wave whose
+// span crosses the last full chunk).
+template <int NB, int LPOL = 0, int SPOL = 1, int LAYOUT = 0>
+__global__ __launch_bounds__(256) void gf_apply_ring_kernel(const KernArgs args) {
+  static_assert(NB == 3, "4-buffer ring");
+  const uint32_t wg = blockIdx.x;
+  const PassDesc &P = enter_pass(args, wg);
+  const uint32_t t_begin = (wg - P.wg_begin) * args.tiles_per_wg;
+  const uint32_t t_end = min(t_begin + args.tiles_per_wg, P.n_tiles);
+  const uint32_t wave_id = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  for (uint32_t tile = t_begin; tile < t_end; ++tile) {
+    if constexpr (LAYOUT == 1) {
+      const uint64_t span_end = uint64_t(tile) * (kTileHalfChunks * 32) + (wave_id + 1) * 2048;
+      if (span_end <= P.full_chunks * 64) {
+        ring_tile_contig<LPOL, SPOL>(args, P, tile, wave_id);
+        continue;
       }
     }
+    ring_tile_halfchunk<LPOL, SPOL>(args, P, tile, wave_id);
   }
 }
 
@@ -597,7 +715,9 @@ int kernel_variant() {
 // 2 = contiguous-load layout; 3/4 = occupancy-bounded builds of 1; 7 = 1 with
 // an XCD-aware grid remap; 9 = traffic-only probe (refused unless
 // BFRS_ALLOW_PROBE=1); 10/11/12 = 5 with nt loads / nt loads + plain stores /
-// plain stores.  Results of each: DESIGN.md §9.
+// plain stores; 13/14/15 = contiguous-line layout (DPP quad swap) with nt
+// loads + nt stores / plain loads + nt stores / nt loads + plain stores.
+// Results of each: DESIGN.md §9.
 uint32_t tile_bytes() { return kernel_variant() == 2 ? kV2TileBytes : kTileHalfChunks * 32; }
 
 hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in,
@@ -634,6 +754,15 @@ hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in
       break;
     case 12:
       hipLaunchKernelGGL((gf_apply_ring_kernel<3, 0, 0>), dim3(n_wgs), dim3(256), lds, stream, args);
+      break;
+    case 13:
+      hipLaunchKernelGGL((gf_apply_ring_kernel<3, 1, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
+      break;
+    case 14:
+      hipLaunchKernelGGL((gf_apply_ring_kernel<3, 0, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
+      break;
+    case 15:
+      hipLaunchKernelGGL((gf_apply_ring_kernel<3, 1, 0, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
       break;
 
     default:
