@@ -16,6 +16,13 @@ constexpr uint32_t kMaxPassOutputs = 4;
 // One workgroup tile = 256 lanes x one 32-byte half-chunk = 8 KiB of columns.
 constexpr uint32_t kTileHalfChunks = 256;
 
+// Nibble-table entry (8 B) index within one input's 64 entries; q = 2*byte_hi
+// + nib_hi selects which nibble of which symbol byte is looked up.  Layout
+// [nib_hi][byte_hi][v]: a 256-B LDS row per nibble half, the low byte's table
+// at +0 and the high byte's at +128 -- disjoint banks, so lanes looking up
+// the same nibble half of different bytes never conflict.
+constexpr uint32_t tab_idx(uint32_t q, uint32_t v) { return (q & 1) * 32 + (q >> 1) * 16 + v; }
+
 // One pass: out[t] (^)= sum_i coef(t,i) * in[i] for t < n_out, over the
 // 64-byte-chunk symbol layout of reed-solomon-simd.
 struct alignas(16) PassDesc {

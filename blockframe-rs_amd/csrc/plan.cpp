@@ -5,6 +5,8 @@
 // of shard bytes.  Rows are code positions, columns are probes.
 #include "plan.hpp"
 
+#include "kernels.hpp"
+
 #include <algorithm>
 #include <array>
 
@@ -288,7 +290,7 @@ void build_tables(const CoefMatrix &m, size_t r0, size_t r1, size_t c0, size_t c
       for (unsigned q = 0; q < 4; ++q)
         for (unsigned v = 0; v < 16; ++v) {
           const uint16_t prod = f.mul(uint16_t(v << (4 * q)), coef);
-          uint32_t *e = t + (q * 16 + v) * 2;
+          uint32_t *e = t + tab_idx(q, v) * 2;
           e[0] |= uint32_t(prod & 0xFF) << shift;
           e[1] |= uint32_t(prod >> 8) << shift;
         }

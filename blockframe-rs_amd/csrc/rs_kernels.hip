@@ -19,12 +19,15 @@
 // nibble per lane is bank-conflict free.  Per symbol and input: 4 LDS lookups
 // and ~10 VALU, independent of the number of outputs (<= 4).
 //
-// LDS table layout per input i (512 B): [q][v] at i*512 + q*128 + v*8, with
-// q = 0/1 low/high nibble of the symbol's low byte, q = 2/3 of its high byte.
-// Address of a lookup: byte 0 = (q&1)*128 + 8*v, bytes 1-2 = 2i + (q>>1).
-// Byte 0 for four symbols at once comes from one shift+mask of the data dword
-// (nibble*8 per byte, bit 7 set for the high nibble); one v_perm_b32 then
-// splices byte b of it under the wave-uniform (2i + q>>1) -> 1 VALU/lookup.
+// LDS table layout per input i (512 B): entry tab_idx(q, v) (kernels.hpp) at
+// i*512 + nib_hi*256 + byte_hi*128 + v*8, q = 2*byte_hi + nib_hi (low/high
+// nibble of the symbol's low/high byte).  Address of a lookup: byte 0 =
+// byte_hi*128 + 8*v, bytes 1-2 = 2i + nib_hi.  Byte 0 for four symbols at once
+// comes from one shift+mask(+or) of the data dword (nibble*8 per byte, bit 7 =
+// byte_hi); one v_perm_b32 splices byte b of it under the wave-uniform
+// 2i + nib_hi -> 1 VALU/lookup.  The two bytes' tables for one nibble half sit
+// in disjoint banks, so lanes holding different bytes of their symbols (the
+// contiguous layout) look up conflict-free.
 #include "kernels.hpp"
 
 namespace bfrs {
@@ -57,35 +60,38 @@ __device__ __forceinline__ void mac_input_v0(const uint4 &L, const uint4 &H, con
       const int s = d * 4 + b;
       const uint32_t lb = (l[d] >> (8 * b)) & 0xFF;
       const uint32_t hb = (h[d] >> (8 * b)) & 0xFF;
-      const uint2 e0 = T[lb & 15], e1 = T[16 + (lb >> 4)], e2 = T[32 + (hb & 15)],
-                  e3 = T[48 + (hb >> 4)];
+      const uint2 e0 = T[tab_idx(0, lb & 15)], e1 = T[tab_idx(1, lb >> 4)],
+                  e2 = T[tab_idx(2, hb & 15)], e3 = T[tab_idx(3, hb >> 4)];
       acc_lo[s] ^= e0.x ^ e1.x ^ e2.x ^ e3.x;
       acc_hi[s] ^= e0.y ^ e1.y ^ e2.y ^ e3.y;
     }
   }
 }
 
-// Variant 1: v_perm addressing + 3-input XOR.  base_lo = 2i, base_hi = 2i+1.
-__device__ __forceinline__ void mac_input_v1(const uint4 &L, const uint4 &H, const char *lds,
-                                             uint32_t base_lo, uint32_t base_hi,
-                                             uint32_t (&acc_lo)[16], uint32_t (&acc_hi)[16]) {
+// Variant 1: v_perm addressing + 3-input XOR.  L/H: the two byte registers of
+// 16 symbols; flag_l/flag_h: 0x80808080 for the register holding high bytes,
+// 0 for low bytes; base_even = 2i, base_odd = 2i + 1.
+__device__ __forceinline__ void mac_input_v1(const uint4 &L, const uint4 &H, uint32_t flag_l,
+                                             uint32_t flag_h, uint32_t base_even,
+                                             uint32_t base_odd, uint32_t (&acc_lo)[16],
+                                             uint32_t (&acc_hi)[16]) {
   const uint32_t l[4] = {L.x, L.y, L.z, L.w};
   const uint32_t h[4] = {H.x, H.y, H.z, H.w};
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
-    const uint32_t ll = (l[d] << 3) & 0x78787878u;
-    const uint32_t lh = ((l[d] >> 1) & 0x78787878u) | 0x80808080u;
-    const uint32_t hl = (h[d] << 3) & 0x78787878u;
-    const uint32_t hh = ((h[d] >> 1) & 0x78787878u) | 0x80808080u;
+    const uint32_t ll = ((l[d] << 3) & 0x78787878u) | flag_l;
+    const uint32_t lh = ((l[d] >> 1) & 0x78787878u) | flag_l;
+    const uint32_t hl = ((h[d] << 3) & 0x78787878u) | flag_h;
+    const uint32_t hh = ((h[d] >> 1) & 0x78787878u) | flag_h;
     uint2 e[4][4];
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       // selector: byte0 <- byte b of the nibble word, byte1..2 <- base, byte3 <- 0
       const uint32_t sel = 0x0C050400u | uint32_t(b);
-      e[b][0] = lds_entry(lds, __builtin_amdgcn_perm(base_lo, ll, sel));
-      e[b][1] = lds_entry(lds, __builtin_amdgcn_perm(base_lo, lh, sel));
-      e[b][2] = lds_entry(lds, __builtin_amdgcn_perm(base_hi, hl, sel));
-      e[b][3] = lds_entry(lds, __builtin_amdgcn_perm(base_hi, hh, sel));
+      e[b][0] = lds_entry(nullptr, __builtin_amdgcn_perm(base_even, ll, sel));
+      e[b][1] = lds_entry(nullptr, __builtin_amdgcn_perm(base_odd, lh, sel));
+      e[b][2] = lds_entry(nullptr, __builtin_amdgcn_perm(base_even, hl, sel));
+      e[b][3] = lds_entry(nullptr, __builtin_amdgcn_perm(base_odd, hh, sel));
     }
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
@@ -169,7 +175,7 @@ __device__ __forceinline__ void mac_input(const u32x4 &Lv, const u32x4 &Hv, uint
   } else if constexpr (VARIANT == 9) {
     mac_input_stream(L, H, acc_lo, acc_hi);
   } else {  // 1, 3, 4
-    mac_input_v1(L, H, nullptr, 2 * i, 2 * i + 1, acc_lo, acc_hi);
+    mac_input_v1(L, H, 0u, 0x80808080u, 2 * i, 2 * i + 1, acc_lo, acc_hi);
   }
 }
 
@@ -385,7 +391,7 @@ __device__ __forceinline__ void ring_tile_halfchunk(const KernArgs &args, const 
       [&](const u32x4 &Lv, const u32x4 &Hv, uint32_t x) {
         const uint32_t r = idx(x);
         mac_input_v1(make_uint4(Lv.x, Lv.y, Lv.z, Lv.w), make_uint4(Hv.x, Hv.y, Hv.z, Hv.w),
-                     nullptr, 2 * r, 2 * r + 1, acc_lo, acc_hi);
+                     0u, 0x80808080u, 2 * r, 2 * r + 1, acc_lo, acc_hi);
       });
   const uint64_t *outp = args.ptrs + P.out;
   const bool accumulate = P.accumulate != 0;
@@ -442,8 +448,8 @@ __device__ __forceinline__ u32x4 quad_swap2(const u32x4 &v) {
 // of 16 symbols.  Lanes p < 2 load the first run into X, lanes p >= 2 the
 // second, so one DPP quad swap of Y (lanes l <-> l^2) hands every lane the
 // other byte of its own 16 symbols: p < 2 owns chunk c4 (X = low, R = high),
-// p >= 2 owns chunk 16+c4 (X = high, R = low) and just swaps its two table
-// bases (2i <-> 2i+1).  Stores mirror it: a lane writes one of its output
+// p >= 2 owns chunk 16+c4 (X = high, R = low) and just flips the byte_hi bit
+// of its table addresses (tab_idx layout: no bank conflicts between them).  Stores mirror it: a lane writes one of its output
 // halves at vx and swaps the other to its partner, which writes it at vy.
 // Needs all 64 lanes (DPP): only for waves whose span is all full chunks.
 template <int LPOL, int SPOL>
@@ -456,7 +462,8 @@ __device__ __forceinline__ void ring_tile_contig(const KernArgs &args, const Pas
   const uint32_t span = tile * (kTileHalfChunks * 32) + wave_id * 2048;
   const uint32_t vx = span + (lowp ? 0u : 1024u) + 16 * lane;
   const uint32_t vy = span + (lowp ? 1024u : 0u) + 16 * lane;
-  const uint32_t sw = lowp ? 0u : 1u;
+  // X holds low bytes (p < 2) or high bytes (p >= 2); R the other byte
+  const uint32_t flag_x = lowp ? 0u : 0x80808080u, flag_r = flag_x ^ 0x80808080u;
   uint32_t acc_lo[16], acc_hi[16];
 #pragma unroll
   for (int s = 0; s < 16; ++s) acc_lo[s] = acc_hi[s] = 0;
@@ -471,8 +478,8 @@ __device__ __forceinline__ void ring_tile_contig(const KernArgs &args, const Pas
       [&](const u32x4 &X, const u32x4 &Y, uint32_t x) {
         const uint32_t r = idx(x);
         const u32x4 R = quad_swap2(Y);
-        mac_input_v1(make_uint4(X.x, X.y, X.z, X.w), make_uint4(R.x, R.y, R.z, R.w), nullptr,
-                     (2 * r) | sw, (2 * r + 1) ^ sw, acc_lo, acc_hi);
+        mac_input_v1(make_uint4(X.x, X.y, X.z, X.w), make_uint4(R.x, R.y, R.z, R.w), flag_x,
+                     flag_r, 2 * r, 2 * r + 1, acc_lo, acc_hi);
       });
   const uint64_t *outp = args.ptrs + P.out;
   const bool accumulate = P.accumulate != 0;
@@ -517,155 +524,6 @@ __global__ __launch_bounds__(256) void gf_apply_ring_kernel(const KernArgs args)
   }
 }
 
-// ---------------------------------------------------------------------------
-// Variant 2 (default): contiguous streaming.
-//
-// A wave covers 1 KiB of columns per input with ONE global_load_dwordx4:
-// lane l holds bytes [16l, 16l+16), i.e. part p = l&3 of chunk l>>2 — the low
-// bytes (p = 0,1) or the high bytes (p = 2,3) of 16 symbols.  Each lane looks
-// up only the two nibble tables of the byte it holds and keeps partial sums
-// for its 16 symbols; lanes l and l^2 hold the two halves of the same symbols,
-// so one DPP quad swap + XOR per accumulator at the end of the tile combines
-// them (XOR is the field addition).  Loads are `nt` (read once), with three
-// inputs in flight (4-buffer ring, loop unrolled by 4, no register moves);
-// stores are non-temporal, 1 KiB contiguous per wave instruction.
-// ---------------------------------------------------------------------------
-constexpr uint32_t kV2TileBytes = 4096;  // 256 lanes x 16 B
-
-__device__ __forceinline__ void gload16_nt(u32x4 &v, uint64_t base, uint32_t voff) {
-  asm volatile("global_load_dwordx4 %0, %1, %2 nt" : "=&v"(v) : "v"(voff), "s"(base) : "memory");
-}
-template <int N>
-__device__ __forceinline__ void vm_wait1(u32x4 &v) {
-  asm volatile("s_waitcnt vmcnt(%1)" : "+v"(v) : "n"(N) : "memory");
-}
-
-// 16 half-symbols of one input: 2 lookups each (the byte's two nibbles).
-// base = 2*input + (lane holds high bytes).
-__device__ __forceinline__ void mac_half(const u32x4 &X, uint32_t base, uint32_t (&acc_lo)[16],
-                                         uint32_t (&acc_hi)[16]) {
-  const uint32_t x[4] = {X.x, X.y, X.z, X.w};
-#pragma unroll
-  for (int d = 0; d < 4; ++d) {
-    const uint32_t nl = (x[d] << 3) & 0x78787878u;
-    const uint32_t nh = ((x[d] >> 1) & 0x78787878u) | 0x80808080u;
-    uint2 e[4][2];
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const uint32_t sel = 0x0C050400u | uint32_t(b);
-      e[b][0] = lds_entry(nullptr, __builtin_amdgcn_perm(base, nl, sel));
-      e[b][1] = lds_entry(nullptr, __builtin_amdgcn_perm(base, nh, sel));
-    }
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const int s = d * 4 + b;
-      acc_lo[s] = xor3(acc_lo[s], e[b][0].x, e[b][1].x);
-      acc_hi[s] = xor3(acc_hi[s], e[b][0].y, e[b][1].y);
-    }
-  }
-}
-
-// Swap with lane ^2 inside each quad (quad_perm [2,3,0,1]) and XOR.
-__device__ __forceinline__ uint32_t quad_xor2(uint32_t v) {
-  return v ^ uint32_t(__builtin_amdgcn_mov_dpp(int(v), 0x4E, 0xF, 0xF, true));
-}
-
-
-__global__ __launch_bounds__(256) void gf_apply_v2_kernel(const KernArgs args) {
-  extern __shared__ __attribute__((aligned(16))) uint2 lds_table[];
-  const PassDesc *passes = args.passes;
-  const uint32_t n_passes = args.n_passes, tiles_per_wg = args.tiles_per_wg;
-
-  const uint32_t wg = blockIdx.x;
-  uint32_t lo = 0, hi = n_passes;
-  while (hi - lo > 1) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (passes[mid].wg_begin <= wg)
-      lo = mid;
-    else
-      hi = mid;
-  }
-  const PassDesc &P = passes[lo];
-  const uint32_t n_in = P.n_in, n_out = P.n_out;
-  const uint64_t *in = args.ptrs + P.in;
-
-  {  // table -> LDS (all loads before stores)
-    const AS_GLOBAL u32x4 *tab = (const AS_GLOBAL u32x4 *)(uintptr_t)P.table;
-    u32x4 *dst = reinterpret_cast<u32x4 *>(lds_table);
-    const uint32_t n16 = n_in * 32;
-    u32x4 v[kMaxPassInputs * 32 / 256];
-#pragma unroll
-    for (int r = 0; r < int(kMaxPassInputs * 32 / 256); ++r) {
-      const uint32_t e = threadIdx.x + 256u * r;
-      v[r] = e < n16 ? tab[e] : u32x4{0, 0, 0, 0};
-    }
-#pragma unroll
-    for (int r = 0; r < int(kMaxPassInputs * 32 / 256); ++r) {
-      const uint32_t e = threadIdx.x + 256u * r;
-      if (e < n16) dst[e] = v[r];
-    }
-  }
-  __syncthreads();
-
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t is_hi = (lane >> 1) & 1;
-  const uint64_t full_bytes = P.full_chunks * 64;
-  const uint32_t t_begin = (wg - P.wg_begin) * tiles_per_wg;
-  const uint32_t t_end = min(t_begin + tiles_per_wg, P.n_tiles);
-
-  for (uint32_t tile = t_begin; tile < t_end; ++tile) {
-    const uint64_t off = uint64_t(tile) * kV2TileBytes + threadIdx.x * 16u;
-    if (off >= full_bytes) break;
-    const uint32_t voff = uint32_t(off);
-
-    uint32_t acc_lo[16], acc_hi[16];
-#pragma unroll
-    for (int s = 0; s < 16; ++s) acc_lo[s] = acc_hi[s] = 0;
-
-    // Ring of 4 buffers, 3 inputs in flight.  n_in is even; the host pads
-    // the pointer list with 3 duplicates so every load is unconditional.
-    u32x4 A, B, C, D;
-    gload16_nt(A, in[0], voff);
-    gload16_nt(B, in[1], voff);
-    gload16_nt(C, in[2], voff);
-    for (uint32_t i = 0;; i += 4) {
-      gload16_nt(D, in[i + 3], voff);
-      vm_wait1<3>(A);
-      mac_half(A, 2 * i + is_hi, acc_lo, acc_hi);
-      gload16_nt(A, in[i + 4], voff);
-      vm_wait1<3>(B);
-      mac_half(B, 2 * (i + 1) + is_hi, acc_lo, acc_hi);
-      if (i + 2 >= n_in) break;
-      gload16_nt(B, in[i + 5], voff);
-      vm_wait1<3>(C);
-      mac_half(C, 2 * (i + 2) + is_hi, acc_lo, acc_hi);
-      gload16_nt(C, in[i + 6], voff);
-      vm_wait1<3>(D);
-      mac_half(D, 2 * (i + 3) + is_hi, acc_lo, acc_hi);
-      if (i + 4 >= n_in) break;
-    }
-    vm_wait1<0>(A);  // drain the prefetches past the end
-
-    // Combine the two halves of every symbol (lanes l, l^2), then each lane
-    // keeps the output bytes of the part it owns: low bytes for p = 0,1.
-#pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      const uint32_t lo_v = quad_xor2(acc_lo[s]);
-      const uint32_t hi_v = quad_xor2(acc_hi[s]);
-      acc_lo[s] = is_hi ? hi_v : lo_v;
-    }
-    const uint64_t *outp = args.ptrs + P.out;
-    const bool accumulate = P.accumulate != 0;
-    for (uint32_t t = 0; t < n_out; ++t) {
-      u32x4 o = {gather_byte(acc_lo, 0, t), gather_byte(acc_lo, 1, t), gather_byte(acc_lo, 2, t),
-                 gather_byte(acc_lo, 3, t)};
-      const uint64_t dst = outp[t] + off;
-      if (accumulate) o ^= *(const AS_GLOBAL u32x4 *)(uintptr_t)dst;
-      store16_nt(dst, o);
-    }
-  }
-}
-
 // Tail chunk (shard_bytes % 64 = tb != 0): tb/2 symbols, low bytes at
 // [base, base+tb/2), high bytes at [base+tb/2, base+tb) — the crate's tail rule.
 // One workgroup per pass, one lane per symbol; rare and tiny.
@@ -682,8 +540,8 @@ __global__ __launch_bounds__(64) void gf_tail_kernel(const KernArgs args) {
     const uint8_t *src = (const uint8_t *)(uintptr_t)in[i];
     const uint32_t lb = src[base + s], hb = src[base + half + s];
     const uint2 *T = (const uint2 *)(uintptr_t)P.table + i * 64;
-    const uint2 e0 = T[lb & 15], e1 = T[16 + (lb >> 4)], e2 = T[32 + (hb & 15)],
-                e3 = T[48 + (hb >> 4)];
+    const uint2 e0 = T[tab_idx(0, lb & 15)], e1 = T[tab_idx(1, lb >> 4)],
+                e2 = T[tab_idx(2, hb & 15)], e3 = T[tab_idx(3, hb >> 4)];
     acc_lo ^= e0.x ^ e1.x ^ e2.x ^ e3.x;
     acc_hi ^= e0.y ^ e1.y ^ e2.y ^ e3.y;
   }
@@ -712,13 +570,13 @@ int kernel_variant() {
 
 // Variants: 5 (default) = v1 arithmetic with a 4-buffer ring (3 inputs in
 // flight per wave); 1 = ping-pong (1 in flight); 0 = naive indexing;
-// 2 = contiguous-load layout; 3/4 = occupancy-bounded builds of 1; 7 = 1 with
+// 3/4 = occupancy-bounded builds of 1; 7 = 1 with
 // an XCD-aware grid remap; 9 = traffic-only probe (refused unless
 // BFRS_ALLOW_PROBE=1); 10/11/12 = 5 with nt loads / nt loads + plain stores /
 // plain stores; 13/14/15 = contiguous-line layout (DPP quad swap) with nt
 // loads + nt stores / plain loads + nt stores / nt loads + plain stores.
 // Results of each: DESIGN.md §9.
-uint32_t tile_bytes() { return kernel_variant() == 2 ? kV2TileBytes : kTileHalfChunks * 32; }
+uint32_t tile_bytes() { return kTileHalfChunks * 32; }
 
 hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in,
                            hipStream_t stream) {
@@ -739,9 +597,6 @@ hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in
       break;
     case 4:
       hipLaunchKernelGGL(gf_apply_kernel<4>, dim3(n_wgs), dim3(256), lds, stream, args);
-      break;
-    case 5:
-      hipLaunchKernelGGL(gf_apply_ring_kernel<3>, dim3(n_wgs), dim3(256), lds, stream, args);
       break;
     case 7:
       hipLaunchKernelGGL(gf_apply_kernel<7>, dim3(n_wgs), dim3(256), lds, stream, args);
@@ -764,9 +619,8 @@ hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in
     case 15:
       hipLaunchKernelGGL((gf_apply_ring_kernel<3, 1, 0, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
       break;
-
-    default:
-      hipLaunchKernelGGL(gf_apply_v2_kernel, dim3(n_wgs), dim3(256), lds, stream, args);
+    default:  // 5
+      hipLaunchKernelGGL((gf_apply_ring_kernel<3>), dim3(n_wgs), dim3(256), lds, stream, args);
   }
   return hipGetLastError();
 }
