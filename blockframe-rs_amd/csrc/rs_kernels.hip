@@ -574,7 +574,8 @@ int kernel_variant() {
 // an XCD-aware grid remap; 9 = traffic-only probe (refused unless
 // BFRS_ALLOW_PROBE=1); 10/11/12 = 5 with nt loads / nt loads + plain stores /
 // plain stores; 13/14/15 = contiguous-line layout (DPP quad swap) with nt
-// loads + nt stores / plain loads + nt stores / nt loads + plain stores.
+// loads + nt stores / plain loads + nt stores / nt loads + plain stores;
+// 16 = contiguous-line layout with plain loads + plain stores.
 // Results of each: DESIGN.md §9.
 uint32_t tile_bytes() { return kTileHalfChunks * 32; }
 
@@ -618,6 +619,9 @@ hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in
       break;
     case 15:
       hipLaunchKernelGGL((gf_apply_ring_kernel<3, 1, 0, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
+      break;
+    case 16:
+      hipLaunchKernelGGL((gf_apply_ring_kernel<3, 0, 0, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
       break;
     default:  // 5
       hipLaunchKernelGGL((gf_apply_ring_kernel<3>), dim3(n_wgs), dim3(256), lds, stream, args);
