@@ -100,3 +100,28 @@ def test_planner_decode_matrices_reproduce_oracle(bfrs, gf_tables):
                 assert a.tobytes().hex() == d["restored"][str(i)], (k, m, d["erased"])
             checked += 1
     assert checked >= 30
+
+
+def test_archive_entry_points_reject_null_arguments(bfrs):
+    """The pipeline entry points fail with BFRS_E_INVALID_ARGUMENT, never crash,
+    on NULL handles/pointers (checked before any device work)."""
+    import ctypes
+    L = bfrs.lib()
+    E = bfrs.E_INVALID_ARGUMENT
+    buf = ctypes.create_string_buffer(256)
+    rep = bfrs.RepairReport()
+    out = ctypes.c_void_p()
+    n = ctypes.c_size_t()
+    assert L.bfrs_commit(None, b"/x", b"/y", 0, 0, buf, 256) == E
+    assert L.bfrs_repair(None, b"/x", ctypes.byref(rep)) == E
+    assert L.bfrs_health_check(None, b"/x", buf, 256, ctypes.byref(n)) == E
+    assert L.bfrs_archive_open(None, b"/x", 4, 0, ctypes.byref(out)) == E
+    assert L.bfrs_archive_size(None, None) == E
+    assert L.bfrs_archive_read(None, 0, 0, None, ctypes.byref(n)) == E
+    assert L.bfrs_archive_stats_get(None, None) == E
+    assert L.bfrs_blake3_batch_dev(None, 1, None, None, None, None, None, None) == E
+    assert L.bfrs_blake3_combine(None, 2, buf) == E
+    assert L.bfrs_blake3_hex(None, 5, 1, buf) == E
+    assert L.bfrs_merkle_root_hex(None, 1, buf) == E
+    assert L.bfrs_manifest_check(None, 0, None, None, 0, None) == E
+    L.bfrs_archive_close(None)  # no-op
