@@ -23,7 +23,7 @@ if [ "${SKIP_TESTS:-0}" != 1 ]; then
 fi
 
 if [ "${READPATH:-0}" = 1 ]; then
-  timeout -k 10 600 python tools/read_path_bench.py ${READPATH_ARGS:-} > "$OUT/readpath_$TAG.log" 2>&1
+  timeout -k 10 900 python bench.py --workload c5 ${READPATH_ARGS:-} > "$OUT/readpath_$TAG.log" 2>&1
   rc=$?; echo "readpath rc=$rc"; tail -3 "$OUT/readpath_$TAG.log"; stop_if_crash $rc readpath
 fi
 
