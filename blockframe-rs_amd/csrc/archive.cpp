@@ -437,6 +437,7 @@ struct bfrs_archive {
   std::unordered_map<size_t, std::pair<SegPtr, std::list<size_t>::iterator>> cache;
   bfrs_archive_stats st{};
   long long want = -1, inflight = -1, last_gi = -1;
+  long long reader_gi = -1;  // segment a reader is loading itself (prefetch skips it)
   bool stop = false;
   std::thread worker;
 
@@ -588,7 +589,7 @@ void bfrs_archive::prefetch_loop() {
     if (stop) return;
     const size_t gi = size_t(want);
     want = -1;
-    if (cache.count(gi)) continue;
+    if (cache.count(gi) || reader_gi == (long long)gi) continue;
     inflight = (long long)gi;
     l.unlock();
     SegPtr seg;
@@ -912,11 +913,14 @@ int bfrs_archive_read(bfrs_archive *a, uint64_t offset, size_t len, uint8_t *out
       continue;
     } else {
       ++a->st.misses;
+      if (a->want == (long long)gi) a->want = -1;  // not started yet: load it here instead
+      a->reader_gi = (long long)gi;
       l.unlock();
       bool ok = false;
       int rc = a->load_clean(gi, &seg, &ok);
       if (rc == BFRS_OK && !ok) rc = a->recover(gi, &seg);
       l.lock();
+      a->reader_gi = -1;
       if (rc) return rc;
       if (ok) ++a->st.verified;
       a->put(gi, seg);
