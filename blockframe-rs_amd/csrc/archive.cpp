@@ -501,7 +501,7 @@ int bfrs_archive::load_clean(size_t gi, SegPtr *out, bool *ok) {
   uint8_t *buf = pool->get();
   if (!buf) return set_error(BFRS_E_NOMEM, "pinned segment buffer allocation failed");
   auto seg = std::make_shared<Seg>(pool, buf, len);
-  if (read_file_into(seg_path(gi), buf, pool->slot) != (long long)len) return BFRS_OK;
+  if (read_file_into(seg_path(gi), buf, pool->slot, 8) != (long long)len) return BFRS_OK;
   std::lock_guard<std::mutex> lg(gpu_mu);
   int rc = arena.reserve(pool->slot, kBlockSegments + kParity);
   if (rc) return rc;

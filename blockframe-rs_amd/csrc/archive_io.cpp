@@ -95,7 +95,7 @@ bool read_file(const std::string &path, std::vector<uint8_t> *out) {
   return true;
 }
 
-long long read_file_into(const std::string &path, uint8_t *dst, size_t cap) {
+long long read_file_into(const std::string &path, uint8_t *dst, size_t cap, int threads) {
   const int fd = open(path.c_str(), O_RDONLY);
   if (fd < 0) return -1;
   struct stat st;
@@ -104,17 +104,28 @@ long long read_file_into(const std::string &path, uint8_t *dst, size_t cap) {
     return -1;
   }
   const size_t n = size_t(st.st_size);
-  size_t done = 0;
-  while (done < n) {
-    const ssize_t r = read(fd, dst + done, n - done);
-    if (r <= 0) {
-      close(fd);
-      return -1;
+  // large files: parallel preads of >= 4 MiB pieces (page-cache copies are
+  // per-thread bandwidth bound)
+  const size_t pieces = threads > 1 ? std::min<size_t>(size_t(threads), n >> 22) : 1;
+  std::atomic<bool> ok{true};
+  auto piece = [&](size_t i) {
+    const size_t lo = n * i / std::max<size_t>(pieces, 1), hi = n * (i + 1) / std::max<size_t>(pieces, 1);
+    size_t done = lo;
+    while (done < hi) {
+      const ssize_t r = pread(fd, dst + done, hi - done, off_t(done));
+      if (r <= 0) {
+        ok = false;
+        return;
+      }
+      done += size_t(r);
     }
-    done += size_t(r);
-  }
+  };
+  if (pieces <= 1)
+    piece(0);
+  else
+    parallel_for(pieces, int(pieces), piece);
   close(fd);
-  return (long long)n;
+  return ok ? (long long)n : -1;
 }
 
 std::string t3_seg(const std::string &dir, size_t b, size_t s) {

@@ -31,8 +31,8 @@ bool rmtree(const std::string &path);
 bool write_file(const std::string &path, const uint8_t *data, size_t n);
 bool read_file(const std::string &path, std::vector<uint8_t> *out);
 // Whole file into dst[0, cap).  Returns its size, or -1 if it is missing,
-// unreadable or longer than cap.
-long long read_file_into(const std::string &path, uint8_t *dst, size_t cap);
+// unreadable or longer than cap.  threads > 1: parallel preads (>= 4 MiB each).
+long long read_file_into(const std::string &path, uint8_t *dst, size_t cap, int threads = 1);
 
 std::string t3_seg(const std::string &dir, size_t b, size_t s);
 std::string t3_par(const std::string &dir, size_t b, size_t p);
