@@ -58,23 +58,6 @@ struct Mapped {
   }
 };
 
-// RS(k,3) encode of host blocks via the pipelined host-memory API.
-int host_encode(bfrs_ctx *ctx, const std::vector<std::vector<const uint8_t *>> &blocks,
-                size_t shard_bytes, std::vector<std::vector<std::vector<uint8_t>>> *parity) {
-  std::vector<uint32_t> ks;
-  std::vector<const uint8_t *> in;
-  std::vector<uint8_t *> out;
-  parity->assign(blocks.size(), {});
-  for (size_t b = 0; b < blocks.size(); ++b) {
-    ks.push_back(uint32_t(blocks[b].size()));
-    in.insert(in.end(), blocks[b].begin(), blocks[b].end());
-    (*parity)[b].assign(kParity, std::vector<uint8_t>(shard_bytes));
-    for (auto &p : (*parity)[b]) out.push_back(p.data());
-  }
-  return bfrs_encode_host_batch(ctx, blocks.size(), ks.data(), kParity, shard_bytes, in.data(),
-                                out.data());
-}
-
 struct Commit {
   bfrs_ctx *ctx;
   std::string root, name;
@@ -85,6 +68,9 @@ struct Commit {
   int tier1(std::string *out_dir);
   int tier2(std::string *out_dir);
   int tier3(std::string *out_dir);
+  int rs13_segments(size_t nseg, bool cv_hash, std::vector<uint8_t> *seg_cvs,
+                    std::vector<struct Rs13Hashes> *hashes,
+                    const std::function<bool(size_t, const uint8_t *const *, size_t)> &write);
   int finish(const std::string &computing, const std::string &file_hash, Manifest &mf,
              std::string *out_dir);
 };
@@ -110,92 +96,205 @@ int Commit::finish(const std::string &computing, const std::string &file_hash, M
   return BFRS_OK;
 }
 
-// commit_tiny (commit.rs:25-118): RS(1,3) of the 64-padded file.
-int Commit::tier1(std::string *out_dir) {
-  const size_t padded = (m.n + 63) / 64 * 64;
-  std::vector<uint8_t> buf(padded, 0);
-  std::memcpy(buf.data(), m.p, m.n);
-  std::vector<std::vector<std::vector<uint8_t>>> par;
-  int rc = host_encode(ctx, {{buf.data()}}, padded, &par);
+// RS(1,3) segments on the GPU (tiers 1 and 2): segment j = file bytes
+// [j*S, j*S + len_j), zero-padded to 64 (generate.rs:26-57).  Rounds of up to
+// kRound segments with one padded size share an arena: host threads copy
+// them from the mmap into pinned slots (4 per segment: data + 3 parity), one
+// H2D copy each, one batched encode, device BLAKE3 of data (unpadded) and
+// parity, optionally the CV pass at file chunk offsets, D2H of the parity;
+// `write` (called on a writer thread) stores the files.  Two arenas and two
+// parity buffers alternate so filling, the GPU and writing overlap.
+struct Rs13Hashes {
+  std::string data;
+  std::string parity[3];
+};
+using Rs13Writer = std::function<bool(size_t seg, const uint8_t *const par[3], size_t shard)>;
+
+int Commit::rs13_segments(size_t nseg, bool cv_hash, std::vector<uint8_t> *seg_cvs,
+                          std::vector<Rs13Hashes> *hashes, const Rs13Writer &write) {
+  constexpr size_t kRound = 8;
+  auto seg_len = [&](size_t j) { return std::min(S, m.n - j * S); };
+  auto padded = [&](size_t j) { return (seg_len(j) + 63) / 64 * 64; };
+  // rounds: consecutive segments with the same padded size, <= kRound each
+  std::vector<std::pair<size_t, size_t>> rounds;  // [first, count)
+  for (size_t j = 0; j < nseg;) {
+    size_t c = 1;
+    while (j + c < nseg && c < kRound && padded(j + c) == padded(j)) ++c;
+    rounds.push_back({j, c});
+    j += c;
+  }
+  hashes->assign(nseg, {});
+  if (cv_hash) seg_cvs->assign(nseg * 32, 0);
+  const size_t slot = (std::min(S, m.n) + 63) / 64 * 64;
+  Arena arena[2], pbuf[2];
+  for (int i = 0; i < 2; ++i) {
+    int rc = arena[i].reserve(slot, 4 * std::min(kRound, nseg));
+    if (rc) return rc;
+    if ((rc = pbuf[i].reserve(slot, 3 * std::min(kRound, nseg)))) return rc;
+  }
+  auto fill = [&](size_t r) {
+    const size_t first = rounds[r].first, cnt = rounds[r].second;
+    Arena &a = arena[r % 2];
+    parallel_for(cnt, threads, [&](size_t j) {
+      const size_t len = seg_len(first + j), pad = padded(first + j);
+      std::memcpy(a.hs(4 * j), m.p + (first + j) * S, len);
+      if (pad > len) std::memset(a.hs(4 * j) + len, 0, pad - len);
+    });
+  };
+  std::atomic<bool> write_ok{true};
+  std::thread writer[2];
+  auto write_round = [&](size_t r) {
+    const size_t first = rounds[r].first, cnt = rounds[r].second;
+    const Arena &pb = pbuf[r % 2];
+    parallel_for(cnt, threads, [&](size_t j) {
+      const uint8_t *par[3] = {pb.hs(3 * j), pb.hs(3 * j + 1), pb.hs(3 * j + 2)};
+      if (!write(first + j, par, padded(first + j))) write_ok = false;
+    });
+  };
+  Context &c = ctx->impl;
+  auto gpu_round = [&](size_t r) -> int {
+    const size_t first = rounds[r].first, cnt = rounds[r].second;
+    const size_t shard = padded(first);
+    Arena &a = arena[r % 2];
+    if (hipSetDevice(c.device) != hipSuccess) return set_error(BFRS_E_HIP, "commit: hipSetDevice");
+    for (size_t j = 0; j < cnt; ++j)
+      if (hipMemcpyAsync(a.ds(4 * j), a.hs(4 * j), shard, hipMemcpyHostToDevice, c.stream) != hipSuccess)
+        return set_error(BFRS_E_HIP, "commit: H2D copy failed");
+    std::vector<uint32_t> ks(cnt, 1);
+    std::vector<const uint8_t *> orig(cnt);
+    std::vector<uint8_t *> rec(3 * cnt);
+    for (size_t j = 0; j < cnt; ++j) {
+      orig[j] = a.ds(4 * j);
+      for (size_t p = 0; p < kParity; ++p) rec[3 * j + p] = a.ds(4 * j + 1 + p);
+    }
+    int rc = encode_batch_on(ctx, cnt, ks.data(), kParity, shard, orig.data(), rec.data(), c.stream);
+    if (rc) return rc;
+    std::vector<const uint8_t *> msgs;
+    std::vector<size_t> lens;
+    for (size_t j = 0; j < cnt; ++j) {
+      msgs.push_back(a.ds(4 * j));
+      lens.push_back(seg_len(first + j));
+      for (size_t p = 0; p < kParity; ++p) {
+        msgs.push_back(a.ds(4 * j + 1 + p));
+        lens.push_back(shard);
+      }
+    }
+    std::vector<std::string> hex;
+    if ((rc = gpu_hash_hex(ctx, msgs, lens, &hex))) return rc;
+    for (size_t j = 0; j < cnt; ++j) {
+      Rs13Hashes &h = (*hashes)[first + j];
+      h.data = hex[4 * j];
+      for (size_t p = 0; p < kParity; ++p) h.parity[p] = hex[4 * j + 1 + p];
+    }
+    if (cv_hash) {  // the segments as nodes of the file's BLAKE3 tree
+      std::vector<const uint8_t *> sm;
+      std::vector<size_t> sl;
+      std::vector<uint64_t> offs;
+      for (size_t j = 0; j < cnt; ++j) {
+        sm.push_back(a.ds(4 * j));
+        sl.push_back(seg_len(first + j));
+        offs.push_back(uint64_t(first + j) * (S / 1024));
+      }
+      std::vector<std::string> unused;
+      std::vector<uint8_t> cvs;
+      if ((rc = gpu_hash_hex(ctx, sm, sl, &unused, offs.data(), &cvs))) return rc;
+      std::memcpy(seg_cvs->data() + first * 32, cvs.data(), cnt * 32);
+    }
+    if (writer[r % 2].joinable()) writer[r % 2].join();  // round r-2 still writing pbuf
+    Arena &pb = pbuf[r % 2];
+    for (size_t j = 0; j < cnt; ++j)
+      for (size_t p = 0; p < kParity; ++p)
+        if (hipMemcpyAsync(pb.hs(3 * j + p), a.ds(4 * j + 1 + p), shard, hipMemcpyDeviceToHost,
+                           c.stream) != hipSuccess)
+          return set_error(BFRS_E_HIP, "commit: D2H copy failed");
+    if (hipStreamSynchronize(c.stream) != hipSuccess)
+      return set_error(BFRS_E_HIP, "commit: stream synchronize failed");
+    return BFRS_OK;
+  };
+  int rc = BFRS_OK;
+  fill(0);
+  for (size_t r = 0; r < rounds.size() && rc == BFRS_OK; ++r) {
+    std::thread filler;
+    if (r + 1 < rounds.size()) filler = std::thread(fill, r + 1);
+    rc = gpu_round(r);
+    if (filler.joinable()) filler.join();
+    if (rc == BFRS_OK) writer[r % 2] = std::thread(write_round, r);
+  }
+  for (auto &w : writer)
+    if (w.joinable()) w.join();
   if (rc) return rc;
-  const std::string file_hash = blake3_hex(m.p, m.n, threads);
-  const std::string dir = root + "/" + name + "_" + file_hash;
+  return write_ok ? BFRS_OK : io_error("write RS(1,3) shards");
+}
+
+// commit_tiny (commit.rs:25-118): RS(1,3) of the 64-padded file; the file
+// digest is the data shard's (unpadded) device BLAKE3.
+int Commit::tier1(std::string *out_dir) {
+  S = m.n;  // one segment: the whole file
+  std::vector<Rs13Hashes> hs;
+  std::string dir;
+  // the directory name needs the file hash, which the GPU pass produces: hash
+  // and encode into memory first (the writer runs after the pass completes)
+  std::vector<std::vector<uint8_t>> par(kParity);
+  size_t shard = 0;
+  auto keep = [&](size_t, const uint8_t *const p[3], size_t sh) {
+    shard = sh;
+    for (size_t i = 0; i < kParity; ++i) par[i].assign(p[i], p[i] + sh);
+    return true;
+  };
+  int rc = rs13_segments(1, false, nullptr, &hs, keep);
+  if (rc) return rc;
+  const std::string file_hash = hs[0].data;
+  dir = root + "/" + name + "_" + file_hash;
   if (!mkdirs(dir)) return io_error("mkdir " + dir);
   if (!write_file(dir + "/data.dat", m.p, m.n)) return io_error("write data.dat");
+  for (size_t p = 0; p < kParity; ++p)
+    if (!write_file(dir + "/parity_" + std::to_string(p) + ".dat", par[p].data(), shard))
+      return io_error("write parity");
   Manifest mf;
   mf.tier = 1;
   mf.data_shards = 6;  // commit.rs:98 (sic)
   mf.parity_shards = 3;
-  mf.segment_size = padded;
-  std::vector<std::string> leaves{file_hash};
-  for (size_t p = 0; p < kParity; ++p) {
-    if (!write_file(dir + "/parity_" + std::to_string(p) + ".dat", par[0][p].data(), padded))
-      return io_error("write parity");
-    leaves.push_back(blake3_hex(par[0][p].data(), padded));
-  }
+  mf.segment_size = shard;
+  std::vector<std::string> leaves{file_hash, hs[0].parity[0], hs[0].parity[1], hs[0].parity[2]};
   for (size_t i = 0; i < leaves.size(); ++i) mf.leaves[int64_t(i)] = leaves[i];
   mf.root = merkle_root_hex(leaves);
   return finish(dir, file_hash, mf, out_dir);
 }
 
-// commit_segmented (commit.rs:124-309): per-segment RS(1,3).
+// commit_segmented (commit.rs:124-309): per-segment RS(1,3), all on the GPU.
 int Commit::tier2(std::string *out_dir) {
   const std::string dir = root + "/" + name + "_computing";
   if (!mkdirs(dir + "/segments") || !mkdirs(dir + "/parity")) return io_error("mkdir " + dir);
   const size_t nseg = (m.n + S - 1) / S;
+  const bool cv_hash = pow2_kib(S) && nseg >= 2;
+  std::vector<Rs13Hashes> hs;
+  std::vector<uint8_t> seg_cvs;
+  auto write = [&](size_t j, const uint8_t *const par[3], size_t shard) {
+    bool ok = write_file(t2_seg(dir, j), m.p + j * S, std::min(S, m.n - j * S));
+    for (size_t p = 0; p < kParity; ++p) ok = ok && write_file(t2_par(dir, j, p), par[p], shard);
+    return ok;
+  };
+  int rc = rs13_segments(nseg, cv_hash, &seg_cvs, &hs, write);
+  if (rc) return rc;
   Manifest mf;
   mf.tier = 2;
   mf.data_shards = 6;  // commit.rs:294 (sic)
   mf.parity_shards = 3;
   mf.segment_size = S;
   std::vector<std::string> seg_roots(nseg);
-  // full segments in GPU batches, the (padded) tail segment on its own
-  const size_t full = m.n / S;
-  for (size_t first = 0; first < nseg;) {
-    const size_t len = std::min(S, m.n - first * S);
-    const size_t padded = (len + 63) / 64 * 64;
-    const size_t count = len == S ? std::min<size_t>(full - first, 64) : 1;
-    std::vector<std::vector<uint8_t>> pads;
-    std::vector<std::vector<const uint8_t *>> blocks;
-    for (size_t i = 0; i < count; ++i) {
-      const uint8_t *src = m.p + (first + i) * S;
-      if (padded != len) {
-        pads.emplace_back(padded, 0);
-        std::memcpy(pads.back().data(), src, len);
-        src = pads.back().data();
-      }
-      blocks.push_back({src});
-    }
-    std::vector<std::vector<std::vector<uint8_t>>> par;
-    int rc = host_encode(ctx, blocks, padded, &par);
-    if (rc) return rc;
-    std::vector<SegmentHashes> hs(count);
-    for (auto &h : hs) h.parity.resize(kParity);
-    std::atomic<bool> ok{true};
-    parallel_for(count * 4, threads, [&](size_t t) {
-      const size_t i = t / 4, what = t % 4;
-      const size_t seg = first + i;
-      if (what == 0) {
-        const uint8_t *src = m.p + seg * S;
-        if (!write_file(t2_seg(dir, seg), src, len)) ok = false;
-        hs[i].data = blake3_hex(src, len);
-      } else {
-        const auto &p = par[i][what - 1];
-        if (!write_file(t2_par(dir, seg, what - 1), p.data(), p.size())) ok = false;
-        hs[i].parity[what - 1] = blake3_hex(p.data(), p.size());
-      }
-    });
-    if (!ok) return io_error("write tier-2 shards");
-    for (size_t i = 0; i < count; ++i) {
-      std::vector<std::string> leaves{hs[i].data};
-      leaves.insert(leaves.end(), hs[i].parity.begin(), hs[i].parity.end());
-      seg_roots[first + i] = merkle_root_hex(leaves);
-      mf.segments[int64_t(first + i)] = hs[i];
-    }
-    first += count;
+  for (size_t j = 0; j < nseg; ++j) {
+    SegmentHashes sh;
+    sh.data = hs[j].data;
+    sh.parity.assign(hs[j].parity, hs[j].parity + kParity);
+    std::vector<std::string> leaves{sh.data};
+    leaves.insert(leaves.end(), sh.parity.begin(), sh.parity.end());
+    seg_roots[j] = merkle_root_hex(leaves);
+    mf.segments[int64_t(j)] = sh;
   }
   mf.root = merkle_root_hex(seg_roots);
-  return finish(dir, blake3_hex(m.p, m.n, threads), mf, out_dir);
+  const std::string file_hash = cv_hash ? blake3_combine_cvs_hex(seg_cvs.data(), nseg)
+                                        : nseg == 1 ? hs[0].data : blake3_hex(m.p, m.n, threads);
+  return finish(dir, file_hash, mf, out_dir);
 }
 
 // commit_blocked (commit.rs:314-536), GPU-pipelined.  Per block of k <= 30
