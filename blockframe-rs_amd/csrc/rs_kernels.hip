@@ -30,6 +30,8 @@
 // contiguous layout) look up conflict-free.
 #include "kernels.hpp"
 
+#include <algorithm>
+
 namespace bfrs {
 namespace {
 
@@ -367,16 +369,19 @@ __device__ __forceinline__ void input_ring(uint32_t n_in, const Load &load, cons
 
 // LAYOUT 0 (v5): lane = one 32-byte half-chunk, 16 B at +0 (low bytes) and
 // 16 B at +32 (high bytes): every 128-B line is touched by two instructions.
-template <int LPOL, int SPOL>
-__device__ __forceinline__ void ring_tile_halfchunk(const KernArgs &args, const PassDesc &P,
-                                                    uint32_t tile, uint32_t wave_id) {
-  const uint32_t n_in = P.n_in, n_out = P.n_out;
+// Accumulates lane `lane` (0..255) of `tile`; false if the lane's half-chunk
+// is past the last full chunk.  `off` = the half-chunk's shard byte offset.
+template <int LPOL>
+__device__ __forceinline__ bool ring_acc_halfchunk(const KernArgs &args, const PassDesc &P,
+                                                   uint32_t tile, uint32_t wave_id, uint32_t lane,
+                                                   uint32_t (&acc_lo)[16], uint32_t (&acc_hi)[16],
+                                                   uint32_t &off) {
+  const uint32_t n_in = P.n_in;
   const uint64_t *in = args.ptrs + P.in;
-  const uint64_t hc = uint64_t(tile) * kTileHalfChunks + threadIdx.x;
-  if (hc >= P.full_chunks * 2) return;
-  const uint64_t off = (hc >> 1) * 64 + (hc & 1) * 16;
-  const uint32_t voff = uint32_t(off);
-  uint32_t acc_lo[16], acc_hi[16];
+  const uint64_t hc = uint64_t(tile) * kTileHalfChunks + lane;
+  if (hc >= P.full_chunks * 2) return false;
+  off = uint32_t((hc >> 1) * 64 + (hc & 1) * 16);
+  const uint32_t voff = off;
 #pragma unroll
   for (int s = 0; s < 16; ++s) acc_lo[s] = acc_hi[s] = 0;
   // input index of step x (x >= n_in: repeat the last input -> cache hit)
@@ -393,6 +398,15 @@ __device__ __forceinline__ void ring_tile_halfchunk(const KernArgs &args, const 
         mac_input_v1(make_uint4(Lv.x, Lv.y, Lv.z, Lv.w), make_uint4(Hv.x, Hv.y, Hv.z, Hv.w),
                      0u, 0x80808080u, 2 * r, 2 * r + 1, acc_lo, acc_hi);
       });
+  return true;
+}
+
+template <int LPOL, int SPOL>
+__device__ __forceinline__ void ring_tile_halfchunk(const KernArgs &args, const PassDesc &P,
+                                                    uint32_t tile, uint32_t wave_id) {
+  uint32_t acc_lo[16], acc_hi[16], off;
+  if (!ring_acc_halfchunk<LPOL>(args, P, tile, wave_id, threadIdx.x, acc_lo, acc_hi, off)) return;
+  const uint32_t n_out = P.n_out;
   const uint64_t *outp = args.ptrs + P.out;
   const bool accumulate = P.accumulate != 0;
   for (uint32_t t = 0; t < n_out; ++t) {
@@ -524,6 +538,349 @@ __global__ __launch_bounds__(256) void gf_apply_ring_kernel(const KernArgs args)
   }
 }
 
+// ---------------------------------------------------------------------------
+// Phased variants (17+): persistent grid, one workgroup per CU, NW waves.
+// The host cuts every pass into "super-tiles" of T consecutive 8 KiB tiles
+// (PassDesc::wg_begin counts super-tiles, tiles_per_wg = T); workgroup b
+// walks super-tiles b, b+G, b+2G, ...  Per super-tile: NW/4 groups of 4 waves
+// compute the T tiles (same lanes, ring and arithmetic as v5) into an LDS
+// image of the outputs in shard byte order, then the whole workgroup writes
+// the image out as one contiguous T x 8 KiB run per output shard.
+// Why: with 30 read streams in flight, the parity writes cost far more than
+// their bytes when every wave stores its own 2 KiB pieces as it finishes
+// (membench5/6: ~1.6 TB/s marginal); bunching a CU's writes into one burst of
+// long contiguous runs per phase recovered ~7% in the traffic-only probe
+// (membench6 "ph_*").  Output-major burst order: each output's T x 8 KiB run
+// is written by consecutive lanes, whole lines per instruction.
+// LDS: [0, n_in*512) pass tables (absolute addresses, as in v5), image at
+// args.lds_image_off: [o][j][512 x 16 B].
+// ---------------------------------------------------------------------------
+template <int NW, int T, int SPOL>
+__global__ __launch_bounds__(NW * 64) void gf_apply_phased_kernel(const KernArgs args,
+                                                                 uint32_t n_virtual) {
+  static_assert(NW % 4 == 0 && T % (NW / 4) == 0, "T tiles split evenly over NW/4 wave groups");
+  extern __shared__ __attribute__((aligned(16))) uint2 lds_table[];
+  u32x4 *img = reinterpret_cast<u32x4 *>(reinterpret_cast<char *>(lds_table) + args.lds_image_off);
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t grp = wave >> 2, w4 = wave & 3, lane = threadIdx.x & 255;
+  uint32_t cur = ~0u;
+  for (uint32_t v = blockIdx.x; v < n_virtual; v += gridDim.x) {
+    uint32_t lo = 0, hi = args.n_passes;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (args.passes[mid].wg_begin <= v)
+        lo = mid;
+      else
+        hi = mid;
+    }
+    const PassDesc &P = args.passes[lo];
+    if (lo != cur) {  // stage this pass's tables (the image barrier below fenced the old ones)
+      const AS_GLOBAL u32x4 *tab = (const AS_GLOBAL u32x4 *)(uintptr_t)P.table;
+      u32x4 *dst = reinterpret_cast<u32x4 *>(lds_table);
+      for (uint32_t e = threadIdx.x; e < P.n_in * 32; e += NW * 64) dst[e] = tab[e];
+      __syncthreads();
+      cur = lo;
+    }
+    const uint32_t n_out = P.n_out;
+    const uint32_t t0 = (v - P.wg_begin) * T;
+#pragma unroll 1
+    for (uint32_t jj = 0; jj < T / (NW / 4); ++jj) {
+      const uint32_t j = grp + jj * (NW / 4);
+      const uint32_t tile = t0 + j;
+      if (tile >= P.n_tiles) break;  // wave-uniform
+      uint32_t acc_lo[16], acc_hi[16], off;
+      if (!ring_acc_halfchunk<0>(args, P, tile, w4, lane, acc_lo, acc_hi, off)) continue;
+      const uint32_t rel = (off & (kTileHalfChunks * 32 - 1)) >> 4;  // 16-B unit within the tile
+      for (uint32_t t = 0; t < n_out; ++t) {
+        u32x4 *d = img + (t * T + j) * 512 + rel;
+        d[0] = u32x4{gather_byte(acc_lo, 0, t), gather_byte(acc_lo, 1, t),
+                     gather_byte(acc_lo, 2, t), gather_byte(acc_lo, 3, t)};
+        d[2] = u32x4{gather_byte(acc_hi, 0, t), gather_byte(acc_hi, 1, t),
+                     gather_byte(acc_hi, 2, t), gather_byte(acc_hi, 3, t)};
+      }
+    }
+    __syncthreads();  // image complete
+    {
+      const uint64_t *outp = args.ptrs + P.out;
+      const uint64_t limit = P.full_chunks * 64;
+      const uint64_t base = uint64_t(t0) * (kTileHalfChunks * 32);
+      const bool accumulate = P.accumulate != 0;
+      for (uint32_t e = threadIdx.x; e < n_out * T * 512; e += NW * 64) {
+        const uint32_t o = e / (T * 512), rem = e - o * (T * 512);
+        const uint64_t byte = base + uint64_t(rem) * 16;  // rem = j*512 + r: contiguous run
+        if (byte >= limit) continue;
+        u32x4 val = img[e];
+        const uint64_t dst = outp[o] + byte;
+        if (accumulate) {
+          const uint4 pv = load16(dst);
+          val ^= u32x4{pv.x, pv.y, pv.z, pv.w};
+        }
+        store16_pol<SPOL>(dst, val);
+      }
+    }
+    __syncthreads();  // image consumed before the next super-tile overwrites it
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Streamed variants (24-26): the phased layout (persistent grid, one
+// workgroup per CU, super-tiles of T = NC/4 tiles, LDS output image written
+// as one contiguous T x 8 KiB run per output) without the phased kernel's
+// bubbles.  NC compute waves never store and never drain their input ring:
+// it runs on across tiles, super-tiles and passes.  4 writer waves (one per
+// SIMD) burst image n out while the compute waves read super-tile n+1.
+// Two barriers per super-tile n, in every wave:
+//   B1(n): the writers are done with image n-1 (the image is free);
+//   B2(n): image n is complete (compute waves go on to n+1's arithmetic).
+// Pass tables sit in two LDS slots of 16 KiB (n_in <= 32).  When the table
+// changes between consecutive super-tiles n and n+1 of a workgroup (a new
+// "run"), the writers store n+1's table into the other slot between B1(n)
+// and B2(n): that slot's last reader finished before B1(n-1), and compute
+// waves start n+1's arithmetic only after B2(n).  The table is prefetched
+// into writer registers one super-tile earlier, so the barrier wait is short.
+// LDS: [0, 32 KiB) table slots, [32 KiB, +n_out*T*8 KiB) image [o][j][512].
+// Lookup addresses: perm base 2r + nib_hi + 64*slot -> slot*16 KiB + r*512.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kSlotBytes = 16384;
+
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// Next super-tile of this workgroup: pass and table-slot bookkeeping.
+__device__ __forceinline__ bool stream_advance(const AS_CONST KernArgs *a, uint32_t n_virtual, uint32_t &v,
+                                               uint32_t &p, uint32_t &slot) {
+  const uint64_t tab = a->passes[p].table;
+  v += gridDim.x;
+  if (v >= n_virtual) return false;
+  while (p + 1 < a->n_passes && a->passes[p + 1].wg_begin <= v) ++p;
+  if (a->passes[p].table != tab) slot ^= 1;
+  return true;
+}
+
+// Per-tile state of a compute group (wave-uniform).
+struct TileDesc {
+  uint32_t in;        // KernArgs::ptrs index of the pass inputs
+  uint32_t n_in;      // ring steps: inputs rounded up to a multiple of 4
+  uint32_t n_real;    // steps with arithmetic (the rest re-read the last input)
+  uint32_t rot;       // first input of this wave (rotation)
+  uint32_t slot;      // LDS table slot
+  uint32_t tile_off;  // tile's first shard byte
+  uint32_t max_off;   // last valid half-chunk offset (lanes past it re-read it)
+  uint32_t valid;     // tile inside the pass (else a dummy, never written)
+};
+
+__device__ __forceinline__ TileDesc stream_tile(const AS_CONST KernArgs *a, uint32_t v, uint32_t p,
+                                                uint32_t slot, uint32_t g, uint32_t w4,
+                                                uint32_t T) {
+  const AS_CONST PassDesc &P = a->passes[p];
+  TileDesc d;
+  uint32_t tile = (v - P.wg_begin) * T + g;
+  d.valid = tile < P.n_tiles;
+  if (!d.valid) tile = P.n_tiles - 1;
+  d.in = uint32_t(P.in);
+  d.n_in = (P.n_in + 3) & ~3u;  // pointer slots up to n_in + 3 hold the last input
+  d.n_real = P.n_real;
+  d.rot = P.rotate ? (tile * 4 + w4) % d.n_in : 0;
+  d.slot = slot;
+  d.tile_off = tile * (kTileHalfChunks * 32);
+  d.max_off = uint32_t(P.full_chunks * 64 - 48);  // the last chunk's second half-chunk
+  return d;
+}
+
+// Step x of the current tile; x >= n_in: step x - n_in of the next tile
+// (past the last tile: the current tile's last step again, never consumed).
+__device__ __forceinline__ void stream_load(const AS_CONST KernArgs *A, u32x4 &L, u32x4 &H,
+                                            uint32_t x, const TileDesc cur, const TileDesc nxt,
+                                            bool has_next, uint32_t lane_off) {
+  const bool in_cur = x < cur.n_in;
+  const bool use_cur = in_cur || !has_next;
+  uint32_t y = in_cur ? x : (has_next ? x - cur.n_in : cur.n_in - 1);
+  const uint32_t n_in = use_cur ? cur.n_in : nxt.n_in;
+  const uint32_t rot = use_cur ? cur.rot : nxt.rot;
+  const uint32_t in = use_cur ? cur.in : nxt.in;
+  const uint32_t tile_off = use_cur ? cur.tile_off : nxt.tile_off;
+  const uint32_t max_off = use_cur ? cur.max_off : nxt.max_off;
+  if (y >= n_in) y = n_in - 1;
+  uint32_t r = y + rot;
+  if (r >= n_in) r -= n_in;
+  const uint32_t voff = min(tile_off + lane_off, max_off);
+  gload_half_chunk<0>(L, H, A->ptrs[in + r], voff);
+}
+
+__device__ __forceinline__ void stream_mac(const u32x4 &Lv, const u32x4 &Hv, uint32_t x,
+                                           const TileDesc cur, uint32_t (&acc_lo)[16],
+                                           uint32_t (&acc_hi)[16]) {
+  uint32_t r = x + cur.rot;
+  if (r >= cur.n_in) r -= cur.n_in;
+  if (r >= cur.n_real) return;  // padding step (wave-uniform)
+  const uint32_t b = 2 * r + 64 * cur.slot;
+  mac_input_v1(make_uint4(Lv.x, Lv.y, Lv.z, Lv.w), make_uint4(Hv.x, Hv.y, Hv.z, Hv.w), 0u,
+               0x80808080u, b, b + 1, acc_lo, acc_hi);
+}
+
+// The 4-buffer input ring of one tile, entered with steps 0..2 in flight in
+// X0..X2; leaves the next tile's steps 0..2 in flight in X0..X2.  Every tile
+// has a multiple of 4 steps, so a tile always starts on the same buffer: two
+// ring entry points (buffer rotations) would make the compiler reconcile
+// register assignments with copies of registers whose loads are still in
+// flight (asm loads are invisible to it) -- a race.
+__device__ __forceinline__ void stream_ring(const AS_CONST KernArgs *A, const TileDesc cur,
+                                            const TileDesc nxt, bool has_next, uint32_t lane_off,
+                                            u32x4 &L0, u32x4 &H0, u32x4 &L1, u32x4 &H1,
+                                            u32x4 &L2, u32x4 &H2, u32x4 &L3, u32x4 &H3,
+                                            uint32_t (&acc_lo)[16], uint32_t (&acc_hi)[16]) {
+  const uint32_t n_in = cur.n_in;
+  for (uint32_t i = 0;; i += 4) {
+    stream_load(A, L3, H3, i + 3, cur, nxt, has_next, lane_off);
+    vm_wait<6>(L0, H0);
+    stream_mac(L0, H0, i, cur, acc_lo, acc_hi);
+    stream_load(A, L0, H0, i + 4, cur, nxt, has_next, lane_off);
+    vm_wait<6>(L1, H1);
+    stream_mac(L1, H1, i + 1, cur, acc_lo, acc_hi);
+    stream_load(A, L1, H1, i + 5, cur, nxt, has_next, lane_off);
+    vm_wait<6>(L2, H2);
+    stream_mac(L2, H2, i + 2, cur, acc_lo, acc_hi);
+    stream_load(A, L2, H2, i + 6, cur, nxt, has_next, lane_off);
+    vm_wait<6>(L3, H3);
+    stream_mac(L3, H3, i + 3, cur, acc_lo, acc_hi);
+    if (i + 4 >= n_in) break;
+  }
+}
+
+template <int NC, int SPOL>
+__global__ __launch_bounds__((NC + 4) * 64) void gf_apply_stream_kernel(const KernArgs args,
+                                                                       uint32_t n_virtual) {
+  static_assert(NC % 4 == 0, "whole 4-wave groups");
+  constexpr uint32_t T = NC / 4;
+  // Descriptors are read through the kernarg segment pointer (scalar loads):
+  // taking the address of the by-value parameter would copy 4 KiB to scratch.
+  const AS_CONST KernArgs *A = (const AS_CONST KernArgs *)__builtin_amdgcn_kernarg_segment_ptr();
+  extern __shared__ __attribute__((aligned(16))) uint2 lds_table[];
+  u32x4 *img = reinterpret_cast<u32x4 *>(reinterpret_cast<char *>(lds_table) + 2 * kSlotBytes);
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t v0 = blockIdx.x;
+  uint32_t p0 = 0;
+  while (p0 + 1 < A->n_passes && A->passes[p0 + 1].wg_begin <= v0) ++p0;
+  {  // first run's table -> slot 0 (every wave)
+    const AS_CONST PassDesc &P = A->passes[p0];
+    const AS_GLOBAL u32x4 *tab = (const AS_GLOBAL u32x4 *)(uintptr_t)P.table;
+    u32x4 *dst = reinterpret_cast<u32x4 *>(lds_table);
+    for (uint32_t e = threadIdx.x; e < P.n_in * 32; e += (NC + 4) * 64) dst[e] = tab[e];
+  }
+  lds_barrier();
+
+  if (wave >= NC) {
+    // ---------------- writer waves ----------------
+    const uint32_t wl = threadIdx.x - NC * 64;  // 0..255
+    uint32_t v = v0, p = p0, slot = 0;
+    // successor state (n+1) and the table prefetched for it
+    uint32_t vn = v, pn = p, slotn = slot;
+    bool has_next = stream_advance(A, n_virtual, vn, pn, slotn);
+    bool pending = has_next && slotn != slot;
+    u32x4 pre[4];
+    auto prefetch = [&](const AS_CONST PassDesc &Q) {
+      const AS_GLOBAL u32x4 *tab = (const AS_GLOBAL u32x4 *)(uintptr_t)Q.table;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const uint32_t e = wl + 256u * r;
+        pre[r] = e < Q.n_in * 32 ? tab[e] : u32x4{0, 0, 0, 0};
+      }
+    };
+    if (pending) prefetch(A->passes[pn]);
+    for (;;) {
+      asm volatile("s_barrier" ::: "memory");  // B1(n)
+      if (pending) {
+        u32x4 *dst = reinterpret_cast<u32x4 *>(reinterpret_cast<char *>(lds_table) + slotn * kSlotBytes);
+        const uint32_t n16 = A->passes[pn].n_in * 32;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const uint32_t e = wl + 256u * r;
+          if (e < n16) dst[e] = pre[r];
+        }
+      }
+      lds_barrier();  // B2(n)
+      // prefetch the table of n+2 if a new run starts there
+      uint32_t vnn = vn, pnn = pn, slotnn = slotn;
+      const bool has_nn = has_next && stream_advance(A, n_virtual, vnn, pnn, slotnn);
+      const bool pending_nn = has_nn && slotnn != slotn;
+      if (pending_nn) prefetch(A->passes[pnn]);
+      {  // burst image n: output-major, each output's T x 8 KiB run contiguous
+        const AS_CONST PassDesc &P = A->passes[p];
+        const uint32_t n_out = P.n_out;
+        const uint32_t t0 = (v - P.wg_begin) * T;
+        const AS_CONST uint64_t *outp = A->ptrs + P.out;
+        const uint64_t limit = P.full_chunks * 64;
+        const uint64_t base = uint64_t(t0) * (kTileHalfChunks * 32);
+        const bool accumulate = P.accumulate != 0;
+        for (uint32_t e = wl; e < n_out * T * 512; e += 256) {
+          const uint32_t o = e / (T * 512), rem = e - o * (T * 512);
+          const uint64_t byte = base + uint64_t(rem) * 16;
+          if (byte >= limit) continue;
+          u32x4 val = img[e];
+          const uint64_t dst = outp[o] + byte;
+          if (accumulate) {
+            const uint4 pv = load16(dst);
+            val ^= u32x4{pv.x, pv.y, pv.z, pv.w};
+          }
+          store16_pol<SPOL>(dst, val);
+        }
+      }
+      if (!has_next) break;
+      v = vn; p = pn; slot = slotn;
+      vn = vnn; pn = pnn; slotn = slotnn;
+      has_next = has_nn;
+      pending = pending_nn;
+    }
+    return;
+  }
+
+  // ---------------- compute waves ----------------
+  // One tile per super-tile per 4-wave group.  The input ring of a tile
+  // prefetches the first 3 inputs of the group's next tile, so it never
+  // drains.
+  const uint32_t g = wave >> 2, w4 = wave & 3, lane = threadIdx.x & 255;
+  const uint32_t lane_off = (lane >> 1) * 64 + (lane & 1) * 16;
+  TileDesc cur = stream_tile(A, v0, p0, 0, g, w4, T);
+  uint32_t v = v0, p = p0, slot = 0;
+  uint32_t vn = v, pn = p, slotn = slot;
+  bool has_next = stream_advance(A, n_virtual, vn, pn, slotn);
+  TileDesc nxt = has_next ? stream_tile(A, vn, pn, slotn, g, w4, T) : cur;
+  uint32_t acc_lo[16], acc_hi[16];
+#pragma unroll
+  for (int s = 0; s < 16; ++s) acc_lo[s] = acc_hi[s] = 0;
+  u32x4 LA, HA, LB, HB, LC, HC, LD, HD;
+  stream_load(A, LA, HA, 0, cur, nxt, has_next, lane_off);
+  stream_load(A, LB, HB, 1, cur, nxt, has_next, lane_off);
+  stream_load(A, LC, HC, 2, cur, nxt, has_next, lane_off);
+  for (;;) {
+    stream_ring(A, cur, nxt, has_next, lane_off, LA, HA, LB, HB, LC, HC, LD, HD, acc_lo, acc_hi);
+    asm volatile("s_barrier" ::: "memory");  // B1(n): image free
+    if (cur.valid) {
+      const AS_CONST PassDesc &P = A->passes[p];
+      if (cur.tile_off + lane_off < P.full_chunks * 64) {
+        const uint32_t rel = lane_off >> 4;  // 16-B unit within the tile
+        for (uint32_t t = 0; t < P.n_out; ++t) {
+          u32x4 *d = img + (t * T + g) * 512 + rel;
+          d[0] = u32x4{gather_byte(acc_lo, 0, t), gather_byte(acc_lo, 1, t),
+                       gather_byte(acc_lo, 2, t), gather_byte(acc_lo, 3, t)};
+          d[2] = u32x4{gather_byte(acc_hi, 0, t), gather_byte(acc_hi, 1, t),
+                       gather_byte(acc_hi, 2, t), gather_byte(acc_hi, 3, t)};
+        }
+      }
+    }
+    lds_barrier();  // B2(n): image complete
+#pragma unroll
+    for (int s = 0; s < 16; ++s) acc_lo[s] = acc_hi[s] = 0;
+    if (!has_next) break;
+    cur = nxt;
+    v = vn; p = pn; slot = slotn;
+    has_next = stream_advance(A, n_virtual, vn, pn, slotn);
+    if (has_next) nxt = stream_tile(A, vn, pn, slotn, g, w4, T);
+  }
+  vm_wait<0>(LA, HA);
+}
+
 // Tail chunk (shard_bytes % 64 = tb != 0): tb/2 symbols, low bytes at
 // [base, base+tb/2), high bytes at [base+tb/2, base+tb) — the crate's tail rule.
 // One workgroup per pass, one lane per symbol; rare and tiny.
@@ -579,11 +936,91 @@ int kernel_variant() {
 // Results of each: DESIGN.md §9.
 uint32_t tile_bytes() { return kTileHalfChunks * 32; }
 
+// Phased variants (waves x tiles per super-tile; grid = CUs x occupancy):
+// 17 = 16 x 4, 18 = 8 x 4, 19 = 16 x 4 with plain stores, 20 = 8 x 2,
+// 21 = 4 x 1, 22 = 4 x 2 (T > waves/4: the groups take several rounds).
+// Streamed (writer-wave) variants, + 4 writer waves each: 24 = 12 compute
+// waves x 3 tiles, 25 = 8 x 2, 26 = 24 with plain stores.
+static uint32_t phased_T(int v) {
+  switch (v) {
+    case 17: case 18: case 19: return 4;
+    case 20: case 22: case 25: return 2;
+    case 21: return 1;
+    case 24: case 26: return 3;
+    default: return 0;
+  }
+}
+uint32_t phased_tiles() { return phased_T(kernel_variant()); }
+
+static int device_cus() {
+  static int cus[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cus[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    cus[dev] = n;
+  }
+  return cus[dev];
+}
+
+template <int NW, int T, int SPOL>
+static hipError_t launch_phased(const KernArgs &args, uint32_t n_virtual, uint32_t max_in,
+                                uint32_t max_out, hipStream_t stream) {
+  KernArgs a = args;
+  a.lds_image_off = max_in * 64 * sizeof(uint2);
+  const size_t lds = a.lds_image_off + size_t(max_out) * T * kTileHalfChunks * 32;
+  int per_cu = 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gf_apply_phased_kernel<NW, T, SPOL>,
+                                                   NW * 64, lds) != hipSuccess || per_cu < 1)
+    per_cu = 1;
+  const uint32_t grid = std::min<uint32_t>(n_virtual, uint32_t(device_cus() * per_cu));
+  hipLaunchKernelGGL((gf_apply_phased_kernel<NW, T, SPOL>), dim3(grid), dim3(NW * 64), lds, stream,
+                     a, n_virtual);
+  return hipGetLastError();
+}
+
+template <int NC, int SPOL>
+static hipError_t launch_stream(const KernArgs &args, uint32_t n_virtual, uint32_t max_in,
+                                uint32_t max_out, hipStream_t stream) {
+  constexpr uint32_t T = NC / 4;
+  const size_t lds = 2 * kSlotBytes + size_t(max_out) * T * kTileHalfChunks * 32;
+  if (max_in > kSlotBytes / 512 || lds > 160 * 1024) {
+    // Outside the streamed layout (tables > one slot, image too large): the
+    // ring kernel reads the same descriptors (tiles_per_wg = T, one
+    // workgroup per super-tile).
+    hipLaunchKernelGGL((gf_apply_ring_kernel<3>), dim3(n_virtual), dim3(256),
+                       size_t(max_in) * 64 * sizeof(uint2), stream, args);
+    return hipGetLastError();
+  }
+  const uint32_t grid = std::min<uint32_t>(n_virtual, uint32_t(device_cus()));
+  hipLaunchKernelGGL((gf_apply_stream_kernel<NC, SPOL>), dim3(grid), dim3((NC + 4) * 64), lds,
+                     stream, args, n_virtual);
+  return hipGetLastError();
+}
+
 hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in,
                            hipStream_t stream) {
   if (n_wgs == 0) return hipSuccess;
   const size_t lds = size_t(max_in) * 64 * sizeof(uint2);
-  switch (kernel_variant()) {
+  const int variant = kernel_variant();
+  if (phased_T(variant)) {
+    uint32_t max_out = 0;
+    for (uint32_t p = 0; p < args.n_passes; ++p) max_out = std::max(max_out, args.passes[p].n_out);
+    switch (variant) {
+      case 17: return launch_phased<16, 4, 1>(args, n_wgs, max_in, max_out, stream);
+      case 18: return launch_phased<8, 4, 1>(args, n_wgs, max_in, max_out, stream);
+      case 19: return launch_phased<16, 4, 0>(args, n_wgs, max_in, max_out, stream);
+      case 20: return launch_phased<8, 2, 1>(args, n_wgs, max_in, max_out, stream);
+      case 21: return launch_phased<4, 1, 1>(args, n_wgs, max_in, max_out, stream);
+      case 22: return launch_phased<4, 2, 1>(args, n_wgs, max_in, max_out, stream);
+      case 24: return launch_stream<12, 1>(args, n_wgs, max_in, max_out, stream);
+      case 25: return launch_stream<8, 1>(args, n_wgs, max_in, max_out, stream);
+      default: return launch_stream<12, 0>(args, n_wgs, max_in, max_out, stream);
+    }
+  }
+  switch (variant) {
     case 0:
       hipLaunchKernelGGL(gf_apply_kernel<0>, dim3(n_wgs), dim3(256), lds, stream, args);
       break;

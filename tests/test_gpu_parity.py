@@ -96,6 +96,39 @@ def test_batch_decode_random_erasures_vs_oracle(ctx, oracle):
         off += k
 
 
+def test_many_blocks_round_trip(ctx, oracle):
+    """Enough blocks that every persistent workgroup of the phased/streamed
+    kernels walks several super-tiles across passes with different tables
+    (encode: k changes; decode: a different erasure pattern per block)."""
+    n = 2 << 20
+    ks = [30] * 10 + [8, 20, 4, 30, 12, 30, 6, 30]
+    gen = torch.Generator(device="cuda").manual_seed(0xB10C)
+    data = [torch.randint(0, 256, (k, n), dtype=torch.uint8, device="cuda", generator=gen) for k in ks]
+    par = [torch.empty(3, n, dtype=torch.uint8, device="cuda") for _ in ks]
+    ctx.encode_batch_dev(ks, 3, n, [d[i] for d in data for i in range(d.shape[0])],
+                         [p[j] for p in par for j in range(3)])
+    torch.cuda.synchronize()
+    for b in (0, 10, 12, len(ks) - 1):  # parity vs the oracle on sampled blocks
+        want = oracle.encode([data[b][i].cpu().numpy() for i in range(ks[b])], 3)
+        for j in range(3):
+            assert np.array_equal(par[b][j].cpu().numpy(), want[j]), (b, j)
+    rng = np.random.default_rng(3)
+    d_orig, d_out, erased = [], [], []
+    for b, k in enumerate(ks):
+        er = sorted(rng.choice(k, size=min(3, k), replace=False).tolist())
+        erased.append(er)
+        for i in range(k):
+            d_orig.append(None if i in er else data[b][i])
+            d_out.append(torch.empty(n, dtype=torch.uint8, device="cuda") if i in er else None)
+    ctx.decode_batch_dev(ks, 3, n, d_orig, [p[j] for p in par for j in range(3)], d_out)
+    torch.cuda.synchronize()
+    off = 0
+    for b, k in enumerate(ks):
+        for i in erased[b]:
+            assert torch.equal(d_out[off + i], data[b][i]), (b, i)
+        off += k
+
+
 def test_decode_inconsistent_input_matches_oracle(ctx, oracle):
     """Corrupted (non-codeword) input: restored bytes must equal the crate
     decoder's output, i.e. the same linear map, not just 'a' valid decode."""

@@ -57,3 +57,44 @@ def test_hazard_detector_flags_the_pattern():
     ok = ["\ts_load_dwordx2 s[14:15], s[6:7], 0x0", "\ts_waitcnt lgkmcnt(0)",
           "\tglobal_load_dwordx4 v[36:39], v40, s[14:15]"]
     assert _hazards(ok) == []
+
+
+def _inflight():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("inflight_check",
+                                                  os.path.join(ROOT, "tools", "inflight_check.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+def test_no_copy_of_inflight_asm_load_registers(tmp_path):
+    """The RS kernels' loads are inline asm waited for by a separate
+    `s_waitcnt vmcnt` asm; a compiler copy, spill or address use of a
+    destination register before its wait reads a stale value (a live-range
+    split at a control-flow merge did exactly that in a first version of the
+    streamed kernel, and a probe built the same way faulted the GPU).
+    Variant 9 is a traffic-only probe (no codec; refused without
+    BFRS_ALLOW_PROBE) and is exempt."""
+    ic = _inflight()
+    src = "\n".join(_isa(os.path.join(CSRC, "rs_kernels.hip"), tmp_path))
+    checked = 0
+    for name, body in ic.kernels(src):
+        if "gf_apply_kernelILi9E" in name:
+            continue
+        checked += 1
+        assert ic.check(body) == [], name
+    assert checked >= 10
+
+
+def test_inflight_checker_flags_a_copy():
+    ic = _inflight()
+    body = ["\t;;#ASMSTART", "\tglobal_load_dwordx4 v[10:13], v2, s[4:5]", "\t;;#ASMEND",
+            "\tv_mov_b64_e32 v[20:21], v[10:11]",
+            "\t;;#ASMSTART", "\ts_waitcnt vmcnt(0)", "\t;;#ASMEND",
+            "\tv_mov_b64_e32 v[22:23], v[12:13]", "\ts_endpgm"]
+    assert [t for _, t in ic.check(body)] == ["v_mov_b64_e32 v[20:21], v[10:11]"]
+    reuse = ["\t;;#ASMSTART", "\tglobal_load_dwordx4 v[10:13], v2, s[4:5]", "\t;;#ASMEND",
+             "\tglobal_load_dwordx4 v[30:33], v11, s[4:5]", "\ts_endpgm"]
+    assert len(ic.check(reuse)) == 1

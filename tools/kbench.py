@@ -39,12 +39,14 @@ def main():
     stream = torch.cuda.current_stream()
     enc_in = [data[i] for i in range(a.segments)]
     enc_out = [par[i] for i in range(3 * nb)]
-    dec_in, dec_out, seg = [], [], 0
+    dec_in, dec_out, seg, erased = [], [], 0, []
     for b, k in enumerate(shapes):
         er = [1, k // 2, k - 1]
         for i in range(k):
             dec_in.append(None if i in er else data[seg + i])
             dec_out.append(rest[3 * b + er.index(i)] if i in er else None)
+            if i in er:
+                erased.append((3 * b + er.index(i), seg + i))
         seg += k
     alg = sum(k + 3 for k in shapes) * S
 
@@ -56,6 +58,7 @@ def main():
 
     os.environ["BFRS_KERNEL_VARIANT"] = "1"
     os.environ.pop("BFRS_TILES_PER_WG", None)
+    ctx.encode_batch_dev(shapes, 3, S, enc_in, enc_out, stream=stream)  # parity for decode mode
     run()
     torch.cuda.synchronize()
     ref = par.clone()
@@ -87,6 +90,10 @@ def main():
             res[(v, t)].append(e0.elapsed_time(e1) / a.iters)
             if v != "9" and not a.decode:
                 assert torch.equal(par, ref), f"variant {v} output differs"
+            if v != "9" and a.decode:
+                for ri, di in erased:
+                    assert torch.equal(rest[ri], data[di]), f"variant {v} decode differs"
+                rest.zero_()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
         for _ in range(a.iters):
