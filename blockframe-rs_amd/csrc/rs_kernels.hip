@@ -105,15 +105,17 @@ __device__ __forceinline__ void mac_input_v1(const uint4 &L, const uint4 &H, uin
 }
 
 // Variant 9 (measurement only, NOT a codec): same memory traffic, no tables.
+// The XORs are asm so the compiler cannot fold "0 ^ load" into a register
+// copy of a load that is still in flight (tools/inflight_check.py).
 __device__ __forceinline__ void mac_input_stream(const uint4 &L, const uint4 &H,
                                                  uint32_t (&acc_lo)[16], uint32_t (&acc_hi)[16]) {
   const uint32_t l[4] = {L.x, L.y, L.z, L.w};
   const uint32_t h[4] = {H.x, H.y, H.z, H.w};
 #pragma unroll
-  for (int s = 0; s < 16; ++s) {
-    acc_lo[s] ^= l[s >> 2];
-    acc_hi[s] ^= h[s >> 2];
-  }
+  for (int d = 0; d < 4; ++d)
+    asm volatile("v_xor_b32 %0, %0, %2\n\tv_xor_b32 %1, %1, %3"
+                 : "+v"(acc_lo[4 * d]), "+v"(acc_hi[4 * d])
+                 : "v"(l[d]), "v"(h[d]));
 }
 
 // Byte t of acc[4d..4d+3] -> dword d of output t (4x4 byte transpose).
@@ -518,8 +520,8 @@ __device__ __forceinline__ void ring_tile_contig(const KernArgs &args, const Pas
 // Variants 5 / 10-15: the ring kernel.  LAYOUT 0 = half-chunk lanes (v5),
 // LAYOUT 1 = contiguous lines + DPP (falls back to LAYOUT 0 for a wave whose
 // span crosses the last full chunk).
-template <int NB, int LPOL = 0, int SPOL = 1, int LAYOUT = 0>
-__global__ __launch_bounds__(256) void gf_apply_ring_kernel(const KernArgs args) {
+template <int NB, int LPOL = 0, int SPOL = 1, int LAYOUT = 0, int MINW = 1>
+__global__ __launch_bounds__(256, MINW) void gf_apply_ring_kernel(const KernArgs args) {
   static_assert(NB == 3, "4-buffer ring");
   const uint32_t wg = blockIdx.x;
   const PassDesc &P = enter_pass(args, wg);
@@ -708,9 +710,21 @@ __device__ __forceinline__ void stream_load(const AS_CONST KernArgs *A, u32x4 &L
   gload_half_chunk<0>(L, H, A->ptrs[in + r], voff);
 }
 
+template <bool PROBE>
 __device__ __forceinline__ void stream_mac(const u32x4 &Lv, const u32x4 &Hv, uint32_t x,
                                            const TileDesc cur, uint32_t (&acc_lo)[16],
                                            uint32_t (&acc_hi)[16]) {
+  if constexpr (PROBE) {
+    // Traffic-only probe (measurement, NOT a codec).  The XORs are asm so the
+    // compiler cannot fold "0 ^ load" into a register copy of a load that is
+    // still in flight (tools/inflight_check.py).
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+      asm volatile("v_xor_b32 %0, %0, %2\n\tv_xor_b32 %1, %1, %3"
+                   : "+v"(acc_lo[d]), "+v"(acc_hi[d])
+                   : "v"(Lv[d]), "v"(Hv[d]));
+    return;
+  }
   uint32_t r = x + cur.rot;
   if (r >= cur.n_in) r -= cur.n_in;
   if (r >= cur.n_real) return;  // padding step (wave-uniform)
@@ -725,6 +739,7 @@ __device__ __forceinline__ void stream_mac(const u32x4 &Lv, const u32x4 &Hv, uin
 // ring entry points (buffer rotations) would make the compiler reconcile
 // register assignments with copies of registers whose loads are still in
 // flight (asm loads are invisible to it) -- a race.
+template <bool PROBE>
 __device__ __forceinline__ void stream_ring(const AS_CONST KernArgs *A, const TileDesc cur,
                                             const TileDesc nxt, bool has_next, uint32_t lane_off,
                                             u32x4 &L0, u32x4 &H0, u32x4 &L1, u32x4 &H1,
@@ -734,21 +749,21 @@ __device__ __forceinline__ void stream_ring(const AS_CONST KernArgs *A, const Ti
   for (uint32_t i = 0;; i += 4) {
     stream_load(A, L3, H3, i + 3, cur, nxt, has_next, lane_off);
     vm_wait<6>(L0, H0);
-    stream_mac(L0, H0, i, cur, acc_lo, acc_hi);
+    stream_mac<PROBE>(L0, H0, i, cur, acc_lo, acc_hi);
     stream_load(A, L0, H0, i + 4, cur, nxt, has_next, lane_off);
     vm_wait<6>(L1, H1);
-    stream_mac(L1, H1, i + 1, cur, acc_lo, acc_hi);
+    stream_mac<PROBE>(L1, H1, i + 1, cur, acc_lo, acc_hi);
     stream_load(A, L1, H1, i + 5, cur, nxt, has_next, lane_off);
     vm_wait<6>(L2, H2);
-    stream_mac(L2, H2, i + 2, cur, acc_lo, acc_hi);
+    stream_mac<PROBE>(L2, H2, i + 2, cur, acc_lo, acc_hi);
     stream_load(A, L2, H2, i + 6, cur, nxt, has_next, lane_off);
     vm_wait<6>(L3, H3);
-    stream_mac(L3, H3, i + 3, cur, acc_lo, acc_hi);
+    stream_mac<PROBE>(L3, H3, i + 3, cur, acc_lo, acc_hi);
     if (i + 4 >= n_in) break;
   }
 }
 
-template <int NC, int SPOL>
+template <int NC, int SPOL, bool PROBE = false>
 __global__ __launch_bounds__((NC + 4) * 64) void gf_apply_stream_kernel(const KernArgs args,
                                                                        uint32_t n_virtual) {
   static_assert(NC % 4 == 0, "whole 4-wave groups");
@@ -854,7 +869,7 @@ __global__ __launch_bounds__((NC + 4) * 64) void gf_apply_stream_kernel(const Ke
   stream_load(A, LB, HB, 1, cur, nxt, has_next, lane_off);
   stream_load(A, LC, HC, 2, cur, nxt, has_next, lane_off);
   for (;;) {
-    stream_ring(A, cur, nxt, has_next, lane_off, LA, HA, LB, HB, LC, HC, LD, HD, acc_lo, acc_hi);
+    stream_ring<PROBE>(A, cur, nxt, has_next, lane_off, LA, HA, LB, HB, LC, HC, LD, HD, acc_lo, acc_hi);
     asm volatile("s_barrier" ::: "memory");  // B1(n): image free
     if (cur.valid) {
       const AS_CONST PassDesc &P = A->passes[p];
@@ -921,7 +936,7 @@ __global__ __launch_bounds__(64) void gf_tail_kernel(const KernArgs args) {
 int kernel_variant() {
   const char *e = std::getenv("BFRS_KERNEL_VARIANT");
   int v = e ? atoi(e) : 5;
-  if (v == 9 && !std::getenv("BFRS_ALLOW_PROBE")) v = 1;
+  if ((v == 9 || v == 27) && !std::getenv("BFRS_ALLOW_PROBE")) v = 1;
   return v;
 }
 
@@ -932,21 +947,19 @@ int kernel_variant() {
 // BFRS_ALLOW_PROBE=1); 10/11/12 = 5 with nt loads / nt loads + plain stores /
 // plain stores; 13/14/15 = contiguous-line layout (DPP quad swap) with nt
 // loads + nt stores / plain loads + nt stores / nt loads + plain stores;
-// 16 = contiguous-line layout with plain loads + plain stores.
-// Results of each: DESIGN.md §9.
+// 16 = contiguous-line layout with plain loads + plain stores; 28 = 5 built
+// for >= 6 waves per SIMD (80 VGPRs).  Results of each: DESIGN.md §9.
 uint32_t tile_bytes() { return kTileHalfChunks * 32; }
 
 // Phased variants (waves x tiles per super-tile; grid = CUs x occupancy):
-// 17 = 16 x 4, 18 = 8 x 4, 19 = 16 x 4 with plain stores, 20 = 8 x 2,
-// 21 = 4 x 1, 22 = 4 x 2 (T > waves/4: the groups take several rounds).
-// Streamed (writer-wave) variants, + 4 writer waves each: 24 = 12 compute
-// waves x 3 tiles, 25 = 8 x 2, 26 = 24 with plain stores.
+// 17 = 16 x 4, 21 = 4 x 1.  Streamed (writer-wave) variants, + 4 writer
+// waves: 24 = 12 compute waves x 3 tiles; 27 = traffic-only probe of 24
+// (refused unless BFRS_ALLOW_PROBE=1).  Results: DESIGN.md §9.
 static uint32_t phased_T(int v) {
   switch (v) {
-    case 17: case 18: case 19: return 4;
-    case 20: case 22: case 25: return 2;
+    case 17: return 4;
     case 21: return 1;
-    case 24: case 26: return 3;
+    case 24: case 27: return 3;
     default: return 0;
   }
 }
@@ -981,7 +994,7 @@ static hipError_t launch_phased(const KernArgs &args, uint32_t n_virtual, uint32
   return hipGetLastError();
 }
 
-template <int NC, int SPOL>
+template <int NC, int SPOL, bool PROBE = false>
 static hipError_t launch_stream(const KernArgs &args, uint32_t n_virtual, uint32_t max_in,
                                 uint32_t max_out, hipStream_t stream) {
   constexpr uint32_t T = NC / 4;
@@ -995,7 +1008,7 @@ static hipError_t launch_stream(const KernArgs &args, uint32_t n_virtual, uint32
     return hipGetLastError();
   }
   const uint32_t grid = std::min<uint32_t>(n_virtual, uint32_t(device_cus()));
-  hipLaunchKernelGGL((gf_apply_stream_kernel<NC, SPOL>), dim3(grid), dim3((NC + 4) * 64), lds,
+  hipLaunchKernelGGL((gf_apply_stream_kernel<NC, SPOL, PROBE>), dim3(grid), dim3((NC + 4) * 64), lds,
                      stream, args, n_virtual);
   return hipGetLastError();
 }
@@ -1010,14 +1023,9 @@ hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in
     for (uint32_t p = 0; p < args.n_passes; ++p) max_out = std::max(max_out, args.passes[p].n_out);
     switch (variant) {
       case 17: return launch_phased<16, 4, 1>(args, n_wgs, max_in, max_out, stream);
-      case 18: return launch_phased<8, 4, 1>(args, n_wgs, max_in, max_out, stream);
-      case 19: return launch_phased<16, 4, 0>(args, n_wgs, max_in, max_out, stream);
-      case 20: return launch_phased<8, 2, 1>(args, n_wgs, max_in, max_out, stream);
       case 21: return launch_phased<4, 1, 1>(args, n_wgs, max_in, max_out, stream);
-      case 22: return launch_phased<4, 2, 1>(args, n_wgs, max_in, max_out, stream);
       case 24: return launch_stream<12, 1>(args, n_wgs, max_in, max_out, stream);
-      case 25: return launch_stream<8, 1>(args, n_wgs, max_in, max_out, stream);
-      default: return launch_stream<12, 0>(args, n_wgs, max_in, max_out, stream);
+      default: return launch_stream<12, 1, true>(args, n_wgs, max_in, max_out, stream);
     }
   }
   switch (variant) {
@@ -1059,6 +1067,9 @@ hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in
       break;
     case 16:
       hipLaunchKernelGGL((gf_apply_ring_kernel<3, 0, 0, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
+      break;
+    case 28:  // v5 built for >= 6 waves per SIMD
+      hipLaunchKernelGGL((gf_apply_ring_kernel<3, 0, 1, 0, 6>), dim3(n_wgs), dim3(256), lds, stream, args);
       break;
     default:  // 5
       hipLaunchKernelGGL((gf_apply_ring_kernel<3>), dim3(n_wgs), dim3(256), lds, stream, args);

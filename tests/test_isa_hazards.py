@@ -75,14 +75,12 @@ def test_no_copy_of_inflight_asm_load_registers(tmp_path):
     destination register before its wait reads a stale value (a live-range
     split at a control-flow merge did exactly that in a first version of the
     streamed kernel, and a probe built the same way faulted the GPU).
-    Variant 9 is a traffic-only probe (no codec; refused without
-    BFRS_ALLOW_PROBE) and is exempt."""
+    The traffic-only probes (variants 9, 27) are checked too: a probe that
+    faults costs a GPU box all the same."""
     ic = _inflight()
     src = "\n".join(_isa(os.path.join(CSRC, "rs_kernels.hip"), tmp_path))
     checked = 0
     for name, body in ic.kernels(src):
-        if "gf_apply_kernelILi9E" in name:
-            continue
         checked += 1
         assert ic.check(body) == [], name
     assert checked >= 10

@@ -9,6 +9,7 @@ import json
 import os
 import sys
 
+PROBES = ("9", "27")  # traffic-only probes: no codec output to check
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "blockframe-rs_amd"))
 
@@ -88,9 +89,9 @@ def main():
             e1.record(stream)
             torch.cuda.synchronize()
             res[(v, t)].append(e0.elapsed_time(e1) / a.iters)
-            if v != "9" and not a.decode:
+            if v not in PROBES and not a.decode:
                 assert torch.equal(par, ref), f"variant {v} output differs"
-            if v != "9" and a.decode:
+            if v not in PROBES and a.decode:
                 for ri, di in erased:
                     assert torch.equal(rest[ri], data[di]), f"variant {v} decode differs"
                 rest.zero_()
