@@ -42,6 +42,8 @@ def parse():
                          "(rocprof trace: 1.33 ms -> 0.92 ms per launch)")
     ap.add_argument("--segments", type=int, default=128, help="segments per GPU (C2: 128)")
     ap.add_argument("--segment-bytes", type=int, default=32 * 1024 * 1024)
+    ap.add_argument("--pitch", type=int, default=-1,
+                    help="shard row pitch in bytes (-1 = bfrs_shard_pitch; A/B of the HBM layout)")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-shard-bytes", type=int, default=8 * 1024 * 1024)
     ap.add_argument("--cpu-threads", type=int, default=0)
@@ -316,7 +318,13 @@ def main():
         lo_b, S, seed = 0, S_full, 0xB10C + rank
 
     # ---- resident workload (this rank's bytes of every segment)
-    data = torch.empty(nseg, S, dtype=torch.uint8, device="cuda")
+    # every shard set is one allocation with rows bfrs_shard_pitch(S) apart
+    def shards(n):
+        if args.pitch < 0:
+            return bfrs.empty_shards(n, S)
+        buf = torch.empty(n * max(args.pitch, S), dtype=torch.uint8, device="cuda")
+        return buf.as_strided((n, S), (max(args.pitch, S), 1))
+    data = shards(nseg)
     if args.strong:
         row = torch.empty(S_full, dtype=torch.uint8, device="cuda")
         for s in range(nseg):
@@ -326,8 +334,8 @@ def main():
     else:
         for s in range(nseg):
             synth.fill_segment_torch(data[s], seed, s)
-    parity = torch.empty(3 * nb, S, dtype=torch.uint8, device="cuda")
-    restored = torch.empty(3 * nb, S, dtype=torch.uint8, device="cuda")
+    parity = shards(3 * nb)
+    restored = shards(3 * nb)
     enc_in = [data[s] for s in range(nseg)]
     enc_out = [parity[i] for i in range(3 * nb)]
     dec_in, dec_out, seg = [], [], 0
@@ -449,7 +457,7 @@ def main():
                          if args.strong else
                          "BASELINE configs[1]+[2]: 128 x 32 MiB segments = 4xRS(30,3)+1xRS(8,3); "
                          "step = encode batch + 3-erasure decode of every block"),
-            "segments": nseg, "segment_bytes": S_full, "blocks": shapes, "parity_shards": 3,
+            "segments": nseg, "segment_bytes": S_full, "shard_pitch": int(data.stride(0)), "blocks": shapes, "parity_shards": 3,
             "parallelism": (f"64-B column stripes x{world}" if args.strong
                             else f"independent batch per GPU x{world}"),
         },

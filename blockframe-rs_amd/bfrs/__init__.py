@@ -44,7 +44,7 @@ E_NOT_RESTORED = -34
 # Every symbol include/bfrs.h declares (tests check the library exports them).
 EXPORTS = (
     "bfrs_abi_version", "bfrs_strerror", "bfrs_last_error", "bfrs_device_count", "bfrs_open",
-    "bfrs_close", "bfrs_synchronize", "bfrs_use_high_rate", "bfrs_encode_coefficient",
+    "bfrs_close", "bfrs_synchronize", "bfrs_shard_pitch", "bfrs_use_high_rate", "bfrs_encode_coefficient",
     "bfrs_plan_decode", "bfrs_encoder_new", "bfrs_encoder_add_original_shard",
     "bfrs_encoder_encode", "bfrs_encoder_recovery", "bfrs_encoder_free", "bfrs_decoder_new",
     "bfrs_decoder_add_original_shard", "bfrs_decoder_add_recovery_shard", "bfrs_decoder_decode",
@@ -102,6 +102,7 @@ def lib() -> ctypes.CDLL:
             "bfrs_strerror": ([ctypes.c_int], ctypes.c_char_p),
             "bfrs_last_error": ([], ctypes.c_char_p),
             "bfrs_device_count": ([], ctypes.c_int),
+            "bfrs_shard_pitch": ([_sz], _sz),
             "bfrs_open": ([ctypes.c_int, ctypes.POINTER(_vp)], ctypes.c_int),
             "bfrs_close": ([_vp], None),
             "bfrs_synchronize": ([_vp], ctypes.c_int),
@@ -233,6 +234,23 @@ def plan_decode(k: int, m: int, orig_present, rec_present):
 
 def device_count() -> int:
     return int(lib().bfrs_device_count())
+
+
+def shard_pitch(shard_bytes: int) -> int:
+    """bfrs_shard_pitch: byte distance between consecutive shards of one allocation."""
+    return int(lib().bfrs_shard_pitch(shard_bytes))
+
+
+def empty_shards(n: int, shard_bytes: int, device="cuda"):
+    """n shards of shard_bytes as rows of one device allocation, shard_pitch apart.
+
+    Returns a (n, shard_bytes) uint8 view with row stride shard_pitch(shard_bytes):
+    one column of many 32 MiB shards then spreads over the HBM channels
+     instead of aliasing onto the same ones."""
+    import torch
+    pitch = shard_pitch(shard_bytes)
+    buf = torch.empty(max(1, n * pitch), dtype=torch.uint8, device=device)
+    return buf.as_strided((n, shard_bytes), (pitch, 1))
 
 
 class Context:

@@ -15,7 +15,7 @@ Arena::~Arena() {
 }
 
 int Arena::reserve(size_t slot_bytes, size_t n) {
-  slot_bytes = std::max<size_t>(256, (slot_bytes + 255) / 256 * 256);
+  slot_bytes = std::max<size_t>(256, shard_pitch(slot_bytes));
   n = std::max<size_t>(1, n);
   if (h && slot_bytes <= slot && n <= nslots) return BFRS_OK;
   if (h) {

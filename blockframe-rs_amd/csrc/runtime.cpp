@@ -356,6 +356,8 @@ const char *bfrs_strerror(int code) {
 
 const char *bfrs_last_error(void) { return g_last_error.c_str(); }
 
+size_t bfrs_shard_pitch(size_t shard_bytes) { return bfrs::shard_pitch(shard_bytes); }
+
 int bfrs_device_count(void) {
   BFRS_API_BEGIN
   int n = 0;

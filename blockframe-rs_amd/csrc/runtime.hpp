@@ -19,6 +19,16 @@
 
 namespace bfrs {
 
+// Shard pitch for multi-shard allocations (bfrs_shard_pitch):
+// >= 1 MiB shards get a pitch = 12 KiB (mod 64 KiB) so that one column of
+// many shards does not alias onto the same HBM channels.
+inline size_t shard_pitch(size_t shard_bytes) {
+  size_t p = (shard_bytes + 255) / 256 * 256;
+  if (shard_bytes < (size_t(1) << 20)) return p;
+  p = (p + 4095) / 4096 * 4096;
+  return p + (12288 + 65536 - p % 65536) % 65536;
+}
+
 // Thread-local error reporting (bfrs_last_error).
 int set_error(int code, const std::string &msg);
 int hip_error(hipError_t e, const char *what);

@@ -70,6 +70,12 @@ int bfrs_open(int device, bfrs_ctx **out);
 void bfrs_close(bfrs_ctx *ctx);
 /* Blocks until all work the context queued has finished. */
 int bfrs_synchronize(bfrs_ctx *ctx);
+/* Recommended byte distance between consecutive shards of one allocation
+ * (HBM layout hint, no reference counterpart).  Shards of >= 1 MiB placed a
+ * power of two apart alias onto the same HBM channels when the kernel reads
+ * one column of all of them together; a pitch = 12 KiB (mod 64 KiB) spreads
+ * them (measured +5%).  Smaller shards: rounded up to 256 B. */
+size_t bfrs_shard_pitch(size_t shard_bytes);
 
 /* ---- codec rules (pure host logic) ------------------------------------ */
 /* 1 = HighRate, 0 = LowRate (reed-solomon-simd DefaultRate), <0 = unsupported. */

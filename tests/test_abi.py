@@ -125,3 +125,17 @@ def test_archive_entry_points_reject_null_arguments(bfrs):
     assert L.bfrs_merkle_root_hex(None, 1, buf) == E
     assert L.bfrs_manifest_check(None, 0, None, None, 0, None) == E
     L.bfrs_archive_close(None)  # no-op
+
+
+def test_shard_pitch_layout_hint(bfrs):
+    """bfrs_shard_pitch: small shards round to 256 B; >= 1 MiB shards get a
+    pitch = 12 KiB (mod 64 KiB), never below the shard size."""
+    assert bfrs.shard_pitch(0) == 0
+    assert bfrs.shard_pitch(1) == 256
+    assert bfrs.shard_pitch(8 << 10) == 8 << 10
+    assert bfrs.shard_pitch(32 << 20) == (32 << 20) + 12288
+    for s in [1 << 20, (1 << 20) + 1, 33554368, 25_000_000, 10**9 // 30]:
+        p = bfrs.shard_pitch(s)
+        assert s <= p < s + 65536 + 4096 and p % 65536 == 12288, (s, p)
+    t = bfrs.empty_shards(3, 1 << 20, device="cpu")
+    assert t.shape == (3, 1 << 20) and t.stride() == (bfrs.shard_pitch(1 << 20), 1)

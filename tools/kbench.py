@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--tpw", default="0")
     ap.add_argument("--segments", type=int, default=128)
     ap.add_argument("--decode", action="store_true")
+    ap.add_argument("--stagger", default="0",
+                    help="comma list: extra bytes between consecutive shards (row pitch S + x)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -31,70 +33,81 @@ def main():
     S = synth.SEGMENT_SIZE
     shapes = synth.block_shapes(a.segments)
     nb = len(shapes)
-    data = torch.empty(a.segments, S, dtype=torch.uint8, device="cuda")
-    for s in range(a.segments):
-        synth.fill_segment_torch(data[s], 0xB10C, s)
-    par = torch.empty(3 * nb, S, dtype=torch.uint8, device="cuda")
-    rest = torch.empty(3 * nb, S, dtype=torch.uint8, device="cuda")
+    def rows(n, pitch):
+        """n shard views of S bytes, row i at byte i * pitch of one buffer."""
+        buf = torch.empty(n * pitch, dtype=torch.uint8, device="cuda")
+        return [buf[i * pitch:i * pitch + S] for i in range(n)]
+
+    def build(stagger):
+        data = rows(a.segments, S + stagger)
+        for s_ in range(a.segments):
+            synth.fill_segment_torch(data[s_], 0xB10C, s_)
+        par = rows(3 * nb, S + stagger)
+        rest = rows(3 * nb, S + stagger)
+        dec_in, dec_out, seg, erased = [], [], 0, []
+        for b, k in enumerate(shapes):
+            er = [1, k // 2, k - 1]
+            for i in range(k):
+                dec_in.append(None if i in er else data[seg + i])
+                dec_out.append(rest[3 * b + er.index(i)] if i in er else None)
+                if i in er:
+                    erased.append((3 * b + er.index(i), seg + i))
+            seg += k
+        return dict(data=data, par=par, rest=rest, dec_in=dec_in, dec_out=dec_out, erased=erased)
+
+    layouts = {int(x): build(int(x)) for x in a.stagger.split(",")}
     ctx = bfrs.Context(0)
     stream = torch.cuda.current_stream()
-    enc_in = [data[i] for i in range(a.segments)]
-    enc_out = [par[i] for i in range(3 * nb)]
-    dec_in, dec_out, seg, erased = [], [], 0, []
-    for b, k in enumerate(shapes):
-        er = [1, k // 2, k - 1]
-        for i in range(k):
-            dec_in.append(None if i in er else data[seg + i])
-            dec_out.append(rest[3 * b + er.index(i)] if i in er else None)
-            if i in er:
-                erased.append((3 * b + er.index(i), seg + i))
-        seg += k
     alg = sum(k + 3 for k in shapes) * S
 
-    def run():
+    def run(L):
         if a.decode:
-            ctx.decode_batch_dev(shapes, 3, S, dec_in, enc_out, dec_out, stream=stream)
+            ctx.decode_batch_dev(shapes, 3, S, L["dec_in"], L["par"], L["dec_out"], stream=stream)
         else:
-            ctx.encode_batch_dev(shapes, 3, S, enc_in, enc_out, stream=stream)
+            ctx.encode_batch_dev(shapes, 3, S, L["data"], L["par"], stream=stream)
 
     os.environ["BFRS_KERNEL_VARIANT"] = "1"
     os.environ.pop("BFRS_TILES_PER_WG", None)
-    ctx.encode_batch_dev(shapes, 3, S, enc_in, enc_out, stream=stream)  # parity for decode mode
-    run()
+    for L in layouts.values():
+        ctx.encode_batch_dev(shapes, 3, S, L["data"], L["par"], stream=stream)  # parity for decode
+        run(L)
     torch.cuda.synchronize()
-    ref = par.clone()
+    L0 = next(iter(layouts.values()))
+    ref = torch.stack(L0["par"]).clone()
     import time
     t0 = time.perf_counter()  # clock settle (~1 s of launches; DESIGN.md §5)
     while time.perf_counter() - t0 < 1.0:
         for _ in range(16):
-            run()
+            run(L0)
         torch.cuda.synchronize()
-    configs = [(v, t) for v in a.variants.split(",") for t in a.tpw.split(",")]
+    configs = [(v, t, x) for v in a.variants.split(",") for t in a.tpw.split(",") for x in layouts]
     res = {c: [] for c in configs}
-    src = data.view(-1)[: alg // 2]
+    src = L0["data"][0].new_empty(alg // 2)
     dst = torch.empty_like(src)
     copy_ms = []
     for r in range(a.rounds):
-        for (v, t) in configs:
+        for (v, t, x) in configs:
+            L = layouts[x]
             os.environ["BFRS_KERNEL_VARIANT"] = v
             if t == "0":
                 os.environ.pop("BFRS_TILES_PER_WG", None)
             else:
                 os.environ["BFRS_TILES_PER_WG"] = t
-            run()  # warm
+            run(L)  # warm
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
             for _ in range(a.iters):
-                run()
+                run(L)
             e1.record(stream)
             torch.cuda.synchronize()
-            res[(v, t)].append(e0.elapsed_time(e1) / a.iters)
+            res[(v, t, x)].append(e0.elapsed_time(e1) / a.iters)
             if v not in PROBES and not a.decode:
-                assert torch.equal(par, ref), f"variant {v} output differs"
+                assert torch.equal(torch.stack(L["par"]), ref), f"variant {v} output differs"
             if v not in PROBES and a.decode:
-                for ri, di in erased:
-                    assert torch.equal(rest[ri], data[di]), f"variant {v} decode differs"
-                rest.zero_()
+                for ri, di in L["erased"]:
+                    assert torch.equal(L["rest"][ri], L["data"][di]), f"variant {v} decode differs"
+                for t_ in L["rest"]:
+                    t_.zero_()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
         for _ in range(a.iters):
@@ -103,9 +116,9 @@ def main():
         torch.cuda.synchronize()
         copy_ms.append(e0.elapsed_time(e1) / a.iters)
     out = {}
-    for (v, t), ms in res.items():
+    for (v, t, x), ms in res.items():
         m = float(np.median(ms))
-        out[f"v{v}_tpw{t}"] = {"ms": round(m, 4), "GBps": round(alg / m / 1e6, 1), "all_ms": [round(x, 4) for x in ms]}
+        out[f"v{v}_tpw{t}" + (f"_stagger{x}" if x else "")] = {"ms": round(m, 4), "GBps": round(alg / m / 1e6, 1), "all_ms": [round(x, 4) for x in ms]}
     cm = float(np.median(copy_ms))
     out["torch_copy_same_bytes"] = {"ms": round(cm, 4), "GBps": round(alg / cm / 1e6, 1)}
     print(json.dumps({"decode": a.decode, "alg_bytes": alg, **out}, indent=1))
