@@ -381,6 +381,35 @@ def test_config3_decode_3_erasures_128x32MiB(ctx, oracle):
     assert oracle.blake3_hex(b0) == oracle.blake3_hex(data[erased[0][0]].cpu().numpy())
 
 
+@pytest.mark.slow
+@pytest.mark.parametrize("world", [8])
+def test_config4_column_stripes_golden(ctx, bfrs, world):
+    """BASELINE config 4 (10 GiB = 320 x 32 MiB, 10 x RS(30,3) + RS(20,3)) as the
+    strong-scaled multi-GPU run splits it (bfrs.parallel.stripe_ranges): each
+    of `world` simulated ranks encodes its 64-byte-aligned column stripe of
+    every shard, in its own launch, into the same stripe of the parity.  The
+    assembled parity must equal the golden SHA-256 of the unsplit oracle
+    encode (tests/golden/rs_large.json): the partition needs no exchange."""
+    from bfrs import parallel, synth
+    g = json.load(open(os.path.join(GOLDEN, "rs_large.json")))["c4_320x32MiB"]
+    S, nseg = g["segment_size"], g["segments"]
+    shapes = synth.block_shapes(nseg)
+    assert shapes == g["blocks"]
+    data = bfrs.empty_shards(nseg, S)
+    for s in range(nseg):
+        synth.fill_segment_torch(data[s], g["seed"], s)
+    rec = bfrs.empty_shards(3 * len(shapes), S)
+    rec.fill_(0xA5)  # every byte must be overwritten by some stripe
+    for lo, hi in parallel.stripe_ranges(S, world):
+        ctx.encode_batch_dev(shapes, 3, hi - lo, [data[s][lo:hi] for s in range(nseg)],
+                             [rec[i][lo:hi] for i in range(rec.shape[0])])
+    torch.cuda.synchronize()
+    for b in range(len(shapes)):
+        for j in range(3):
+            h = hashlib.sha256(rec[3 * b + j].cpu().numpy().tobytes()).hexdigest()
+            assert h == g["parity_sha256"][b][j], (b, j)
+
+
 def test_in_tree_library_is_the_one_loaded(bfrs):
     import ctypes.util  # noqa: F401
     maps = open("/proc/self/maps").read()
