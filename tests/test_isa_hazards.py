@@ -26,7 +26,21 @@ def _isa(src, tmp_path):
     return out.read_text().split("\n")
 
 
+def _sgpr_dest(line):
+    """SGPRs an instruction writes through its first operand (s7 or s[6:7]), else ()."""
+    m = re.match(r"\s*([sv]_\w+)\s+s(?:(\d+)|\[(\d+):(\d+)\])\s*,", line)
+    if not m:
+        return ()
+    if m.group(2) is not None:
+        return (int(m.group(2)),)
+    return tuple(range(int(m.group(3)), int(m.group(4)) + 1))
+
+
 def _hazards(lines, window=6):
+    """(line, VALU writer, VMEM) triples where a VALU instruction's SGPR result is
+    still the value a saddr VMEM instruction reads, fewer than `window`
+    instructions later with no s_nop between (an SMEM/SALU rewrite of the
+    register in between ends the hazard)."""
     hits = []
     for i, l in enumerate(lines):
         m = re.search(r"global_(load|store)_dwordx\d+ .*?, s\[(\d+):(\d+)\]", l)
@@ -35,10 +49,14 @@ def _hazards(lines, window=6):
         lo, hi = int(m.group(2)), int(m.group(3))
         prev = [x for x in lines[max(0, i - 3 * window):i]
                 if x.strip() and not x.strip().startswith((";", "."))][-window:]
-        for w in prev:
-            mm = re.match(r"\s*v_\w+\s+s(\d+),", w) or re.match(r"\s*v_\w+\s+s\[(\d+):\d+\]", w)
-            if mm and lo <= int(mm.group(1)) <= hi and "s_nop" not in "".join(prev):
-                hits.append((i, w.strip(), l.strip()))
+        if any("s_nop" in x for x in prev):
+            continue
+        for r in range(lo, hi + 1):
+            for w in reversed(prev):  # the most recent writer of s<r> decides
+                if r in _sgpr_dest(w):
+                    if w.strip().startswith("v_"):
+                        hits.append((i, w.strip(), l.strip()))
+                    break
     return hits
 
 
@@ -57,6 +75,11 @@ def test_hazard_detector_flags_the_pattern():
     ok = ["\ts_load_dwordx2 s[14:15], s[6:7], 0x0", "\ts_waitcnt lgkmcnt(0)",
           "\tglobal_load_dwordx4 v[36:39], v40, s[14:15]"]
     assert _hazards(ok) == []
+    # the VALU result is only an SMEM address; the load overwrites the pair
+    dead = ["\tv_readfirstlane_b32 s14, v36", "\tv_readfirstlane_b32 s15, v37",
+            "\ts_load_dwordx2 s[14:15], s[14:15], 0x410", "\ts_waitcnt lgkmcnt(0)",
+            "\tglobal_load_dwordx4 v[6:9], v38, s[14:15]"]
+    assert _hazards(dead) == []
 
 
 def _inflight():
