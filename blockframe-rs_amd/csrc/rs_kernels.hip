@@ -373,7 +373,7 @@ __device__ __forceinline__ void input_ring(uint32_t n_in, const Load &load, cons
 // 16 B at +32 (high bytes): every 128-B line is touched by two instructions.
 // Accumulates lane `lane` (0..255) of `tile`; false if the lane's half-chunk
 // is past the last full chunk.  `off` = the half-chunk's shard byte offset.
-template <int LPOL, int ROT = 0>
+template <int LPOL, int ROT = 0, bool PROBE = false>
 __device__ __forceinline__ bool ring_acc_halfchunk(const KernArgs &args, const PassDesc &P,
                                                    uint32_t tile, uint32_t wave_id, uint32_t lane,
                                                    uint32_t (&acc_lo)[16], uint32_t (&acc_hi)[16],
@@ -389,8 +389,10 @@ __device__ __forceinline__ bool ring_acc_halfchunk(const KernArgs &args, const P
   // input index of step x (x >= n_in: repeat the last input -> cache hit)
   // ROT 0: every wave of a tile starts at its own input; 1: the whole
   // workgroup starts at one input (tiles rotated); 2: no rotation.
+  // ROT 3/4/5: groups of 2/4/8 consecutive tiles share a rotation.
   const uint32_t rot = !P.rotate || ROT == 2 ? 0
                        : ROT == 1           ? (tile * 4) % n_in
+                       : ROT >= 3           ? ((tile >> (ROT - 2)) * 4) % n_in
                                             : (tile * 4 + wave_id) % n_in;
   auto idx = [&](uint32_t x) -> uint32_t {
     if (x >= n_in) x = n_in - 1;
@@ -401,17 +403,21 @@ __device__ __forceinline__ bool ring_acc_halfchunk(const KernArgs &args, const P
       n_in, [&](u32x4 &L, u32x4 &H, uint32_t x) { gload_half_chunk<LPOL>(L, H, in[idx(x)], voff); },
       [&](const u32x4 &Lv, const u32x4 &Hv, uint32_t x) {
         const uint32_t r = idx(x);
-        mac_input_v1(make_uint4(Lv.x, Lv.y, Lv.z, Lv.w), make_uint4(Hv.x, Hv.y, Hv.z, Hv.w),
-                     0u, 0x80808080u, 2 * r, 2 * r + 1, acc_lo, acc_hi);
+        if constexpr (PROBE)  // traffic-only probe (measurement, NOT a codec)
+          mac_input_stream(make_uint4(Lv.x, Lv.y, Lv.z, Lv.w), make_uint4(Hv.x, Hv.y, Hv.z, Hv.w),
+                           acc_lo, acc_hi);
+        else
+          mac_input_v1(make_uint4(Lv.x, Lv.y, Lv.z, Lv.w), make_uint4(Hv.x, Hv.y, Hv.z, Hv.w),
+                       0u, 0x80808080u, 2 * r, 2 * r + 1, acc_lo, acc_hi);
       });
   return true;
 }
 
-template <int LPOL, int SPOL, int ROT = 0>
+template <int LPOL, int SPOL, int ROT = 0, bool PROBE = false>
 __device__ __forceinline__ void ring_tile_halfchunk(const KernArgs &args, const PassDesc &P,
                                                     uint32_t tile, uint32_t wave_id) {
   uint32_t acc_lo[16], acc_hi[16], off;
-  if (!ring_acc_halfchunk<LPOL, ROT>(args, P, tile, wave_id, threadIdx.x, acc_lo, acc_hi, off)) return;
+  if (!ring_acc_halfchunk<LPOL, ROT, PROBE>(args, P, tile, wave_id, threadIdx.x, acc_lo, acc_hi, off)) return;
   const uint32_t n_out = P.n_out;
   const uint64_t *outp = args.ptrs + P.out;
   const bool accumulate = P.accumulate != 0;
@@ -524,7 +530,8 @@ __device__ __forceinline__ void ring_tile_contig(const KernArgs &args, const Pas
 // Variants 5 / 10-15: the ring kernel.  LAYOUT 0 = half-chunk lanes (v5),
 // LAYOUT 1 = contiguous lines + DPP (falls back to LAYOUT 0 for a wave whose
 // span crosses the last full chunk).
-template <int NB, int LPOL = 0, int SPOL = 1, int LAYOUT = 0, int MINW = 1, int ROT = 0>
+template <int NB, int LPOL = 0, int SPOL = 1, int LAYOUT = 0, int MINW = 1, int ROT = 0,
+          bool PROBE = false>
 __global__ __launch_bounds__(256, MINW) void gf_apply_ring_kernel(const KernArgs args) {
   static_assert(NB == 3, "4-buffer ring");
   const uint32_t wg = blockIdx.x;
@@ -540,7 +547,7 @@ __global__ __launch_bounds__(256, MINW) void gf_apply_ring_kernel(const KernArgs
         continue;
       }
     }
-    ring_tile_halfchunk<LPOL, SPOL, ROT>(args, P, tile, wave_id);
+    ring_tile_halfchunk<LPOL, SPOL, ROT, PROBE>(args, P, tile, wave_id);
   }
 }
 
@@ -939,13 +946,16 @@ __global__ __launch_bounds__(64) void gf_tail_kernel(const KernArgs args) {
 // is a traffic-only probe and is refused unless BFRS_ALLOW_PROBE=1.
 int kernel_variant() {
   const char *e = std::getenv("BFRS_KERNEL_VARIANT");
-  int v = e ? atoi(e) : 36;
-  if ((v == 9 || v == 27) && !std::getenv("BFRS_ALLOW_PROBE")) v = 1;
+  int v = e ? atoi(e) : 41;
+  if ((v == 9 || v == 27 || v == 44) && !std::getenv("BFRS_ALLOW_PROBE")) v = 1;
   return v;
 }
 
-// Variants: 36 (default) = 5 with one input rotation per workgroup;
-// 5 = v1 arithmetic with a 4-buffer ring (3 inputs in flight per wave, each
+// Variants: 41 (default) = 5 with one input rotation per group of 16
+// consecutive tiles (the 16 workgroups read one shard's 128 KiB together);
+// 36 / 38 / 39 / 40 / 42 = the same with groups of 1 / 2 / 4 / 8 / 32 tiles;
+// 37 = no rotation; 43 = 41 built for >= 6 waves per SIMD; 44 = traffic-only
+// probe of 41 (refused unless BFRS_ALLOW_PROBE=1); 5 = v1 arithmetic with a 4-buffer ring (3 inputs in flight per wave, each
 // wave of a tile starting at its own input); 1 = ping-pong (1 in flight); 0 = naive indexing;
 // 3/4 = occupancy-bounded builds of 1; 7 = 1 with
 // an XCD-aware grid remap; 9 = traffic-only probe (refused unless
@@ -1075,6 +1085,27 @@ hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in
       break;
     case 36:  // v5, one rotation per workgroup (all 4 waves read one input)
       hipLaunchKernelGGL((gf_apply_ring_kernel<3, 0, 1, 0, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
+      break;
+    case 38:  // 36 with one rotation per 2 / 4 / 8 consecutive tiles
+      hipLaunchKernelGGL((gf_apply_ring_kernel<3, 0, 1, 0, 1, 3>), dim3(n_wgs), dim3(256), lds, stream, args);
+      break;
+    case 39:
+      hipLaunchKernelGGL((gf_apply_ring_kernel<3, 0, 1, 0, 1, 4>), dim3(n_wgs), dim3(256), lds, stream, args);
+      break;
+    case 40:
+      hipLaunchKernelGGL((gf_apply_ring_kernel<3, 0, 1, 0, 1, 5>), dim3(n_wgs), dim3(256), lds, stream, args);
+      break;
+    case 41:
+      hipLaunchKernelGGL((gf_apply_ring_kernel<3, 0, 1, 0, 1, 6>), dim3(n_wgs), dim3(256), lds, stream, args);
+      break;
+    case 42:
+      hipLaunchKernelGGL((gf_apply_ring_kernel<3, 0, 1, 0, 1, 7>), dim3(n_wgs), dim3(256), lds, stream, args);
+      break;
+    case 44:  // traffic-only probe of 41 (refused unless BFRS_ALLOW_PROBE=1)
+      hipLaunchKernelGGL((gf_apply_ring_kernel<3, 0, 1, 0, 1, 6, true>), dim3(n_wgs), dim3(256), lds, stream, args);
+      break;
+    case 43:  // 41 built for >= 6 waves per SIMD
+      hipLaunchKernelGGL((gf_apply_ring_kernel<3, 0, 1, 0, 6, 6>), dim3(n_wgs), dim3(256), lds, stream, args);
       break;
     case 37:  // v5 without rotation
       hipLaunchKernelGGL((gf_apply_ring_kernel<3, 0, 1, 0, 1, 2>), dim3(n_wgs), dim3(256), lds, stream, args);
