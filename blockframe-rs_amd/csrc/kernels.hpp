@@ -35,7 +35,7 @@ struct alignas(16) PassDesc {
   uint64_t full_chunks;      // whole 64-byte chunks per shard
   uint32_t tail_bytes;       // shard_bytes % 64 (tail chunk, crate tail layout)
   uint16_t accumulate;       // 1: XOR into existing outputs
-  uint16_t rotate;           // 1: waves start at different inputs (even, unpadded passes)
+  uint16_t rotate;           // 1: rotate the input order (even, unpadded passes)
   uint32_t n_real;           // inputs with a nonzero table (n_in - 1 for an odd count)
 };
 
@@ -49,8 +49,7 @@ constexpr uint32_t kMaxLaunchPtrs = 376;
 struct alignas(16) KernArgs {
   uint32_t n_passes;
   uint32_t tiles_per_wg;
-  uint32_t lds_image_off;    // phased kernels: LDS byte offset of the output image (set by the launcher)
-  uint32_t pad;
+  uint32_t pad[2];
   PassDesc passes[kMaxLaunchPasses];
   uint64_t ptrs[kMaxLaunchPtrs];
 };
@@ -59,9 +58,6 @@ static_assert(sizeof(KernArgs) <= 4096, "kernel arguments must fit 4 KiB");
 // Column bytes one workgroup tile covers in the selected kernel variant.
 uint32_t tile_bytes();
 int kernel_variant();
-// Phased (persistent, LDS-staged output) variants: tiles per virtual workgroup
-// (a contiguous "super-tile"); 0 for the one-tile-per-workgroup variants.
-uint32_t phased_tiles();
 
 hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in,
                            hipStream_t stream);

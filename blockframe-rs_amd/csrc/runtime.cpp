@@ -281,7 +281,6 @@ int Context::run_blocks(const std::vector<BlockIO> &blocks, size_t shard_bytes,
       const uint64_t total_tiles = uint64_t(n_tiles) * (last - first);
       uint32_t tpw = uint32_t(std::max<uint64_t>(1, total_tiles / 65536));
       if (const char *e = std::getenv("BFRS_TILES_PER_WG")) tpw = std::max(1, atoi(e));
-      if (const uint32_t T = phased_tiles()) tpw = T;  // super-tiles of a persistent grid
       const uint32_t wgs_per_pass = (n_tiles + tpw - 1) / tpw;
 
       KernArgs ka{};

@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/pmcw
 mkdir -p $OUT
-CMD="python3 tools/kbench.py --rounds 1 --iters 3 --variants ${VARS:-5,12,14,9}"
+CMD="python3 tools/kbench.py --rounds 1 --iters 3 --variants ${VARS:-41,5,44}"
 i=0
 for set in "TCC_EA0_WRREQ TCC_EA0_WRREQ_64B TCC_EA0_WR_UNCACHED_32B" \
            "TCC_EA0_WRREQ_STALL TCC_TOO_MANY_EA_WRREQS_STALL TCC_EA0_WRREQ_DRAM_CREDIT_STALL" \

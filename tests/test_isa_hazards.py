@@ -98,15 +98,15 @@ def test_no_copy_of_inflight_asm_load_registers(tmp_path):
     destination register before its wait reads a stale value (a live-range
     split at a control-flow merge did exactly that in a first version of the
     streamed kernel, and a probe built the same way faulted the GPU).
-    The traffic-only probes (variants 9, 27) are checked too: a probe that
-    faults costs a GPU box all the same."""
+    The traffic-only probe (variant 44) is checked too: a probe that faults
+    costs a GPU box all the same."""
     ic = _inflight()
     src = "\n".join(_isa(os.path.join(CSRC, "rs_kernels.hip"), tmp_path))
     checked = 0
     for name, body in ic.kernels(src):
         checked += 1
         assert ic.check(body) == [], name
-    assert checked >= 10
+    assert checked >= 7  # ring kernel x 7 read orders / probe, tail kernel
 
 
 def test_inflight_checker_flags_a_copy():
