@@ -61,10 +61,12 @@ __device__ __forceinline__ void mac_input_v1(const uint4 &L, const uint4 &H, uin
   const uint32_t h[4] = {H.x, H.y, H.z, H.w};
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
+    // nibble*8 per byte | flag; for the high-byte words (x & M) | F is one
+    // v_bitop3 (0xEA), measured -0.7% launch time over v_and + v_or
     const uint32_t ll = ((l[d] << 3) & 0x78787878u) | flag_l;
     const uint32_t lh = ((l[d] >> 1) & 0x78787878u) | flag_l;
-    const uint32_t hl = ((h[d] << 3) & 0x78787878u) | flag_h;
-    const uint32_t hh = ((h[d] >> 1) & 0x78787878u) | flag_h;
+    const uint32_t hl = __builtin_amdgcn_bitop3_b32(h[d] << 3, 0x78787878u, flag_h, 0xEA);
+    const uint32_t hh = __builtin_amdgcn_bitop3_b32(h[d] >> 1, 0x78787878u, flag_h, 0xEA);
     uint2 e[4][4];
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
@@ -291,7 +293,7 @@ __device__ __forceinline__ void ring_tile_halfchunk(const KernArgs &args, const 
 // The ring kernel: workgroup wg owns tiles_per_wg consecutive 8 KiB tiles of
 // one pass (one by default); ROT picks the read order (ring_acc_halfchunk).
 template <int ROT, bool PROBE = false>
-__global__ __launch_bounds__(256) void gf_apply_ring_kernel(const KernArgs args) {
+__global__ __launch_bounds__(256, 5) void gf_apply_ring_kernel(const KernArgs args) {
   const uint32_t wg = blockIdx.x;
   const PassDesc &P = enter_pass(args, wg);
   const uint32_t t_begin = (wg - P.wg_begin) * args.tiles_per_wg;
