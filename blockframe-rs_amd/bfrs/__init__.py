@@ -20,7 +20,8 @@ import os
 from typing import Optional, Sequence
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "libbfrs.so")
+# BFRS_LIB: another in-tree build of the library (A/B of two builds on one box)
+LIB_PATH = os.path.join(os.path.dirname(_HERE), os.environ.get("BFRS_LIB", "libbfrs.so"))
 
 # Error codes (include/bfrs.h)
 OK = 0

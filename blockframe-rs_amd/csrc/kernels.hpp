@@ -16,12 +16,17 @@ constexpr uint32_t kMaxPassOutputs = 4;
 // One workgroup tile = 256 lanes x one 32-byte half-chunk = 8 KiB of columns.
 constexpr uint32_t kTileHalfChunks = 256;
 
-// Nibble-table entry (8 B) index within one input's 64 entries; q = 2*byte_hi
-// + nib_hi selects which nibble of which symbol byte is looked up.  Layout
-// [nib_hi][byte_hi][v]: a 256-B LDS row per nibble half, the low byte's table
-// at +0 and the high byte's at +128 -- disjoint banks, so lanes looking up
-// the same nibble half of different bytes never conflict.
-constexpr uint32_t tab_idx(uint32_t q, uint32_t v) { return (q & 1) * 32 + (q >> 1) * 16 + v; }
+// Nibble-table entry (8 B) index within one input's 64 entries (512 B); q =
+// 2*byte_hi + nib_hi selects which nibble of which symbol byte is looked up.
+//   high nibbles (q = 1, 3): bytes [0, 256): entry v of byte byte_hi at
+//     16*v + 8*byte_hi, so the lookup offset is (x & 0xF0) | 8*byte_hi -- the
+//     nibble stays in place and one mask-and-flag makes the address byte;
+//   low nibbles (q = 0, 2): bytes [256, 512): 256 + 128*byte_hi + 8*v.
+// Either way 16 entries of one (nibble half, byte) span 32 distinct LDS banks,
+// so a ds_read_b64 with any nibble per lane is conflict free.
+constexpr uint32_t tab_idx(uint32_t q, uint32_t v) {
+  return (q & 1) ? 2 * v + (q >> 1) : 32 + (q >> 1) * 16 + v;
+}
 
 // One pass: out[t] (^)= sum_i coef(t,i) * in[i] for t < n_out, over the
 // 64-byte-chunk symbol layout of reed-solomon-simd.

@@ -19,15 +19,15 @@
 // nibble per lane is bank-conflict free.  Per symbol and input: 4 LDS lookups
 // and ~10 VALU, independent of the number of outputs (<= 4).
 //
-// LDS table layout per input i (512 B): entry tab_idx(q, v) (kernels.hpp) at
-// i*512 + nib_hi*256 + byte_hi*128 + v*8, q = 2*byte_hi + nib_hi (low/high
-// nibble of the symbol's low/high byte).  Address of a lookup: byte 0 =
-// byte_hi*128 + 8*v, bytes 1-2 = 2i + nib_hi.  Byte 0 for four symbols at once
-// comes from one shift+mask(+or) of the data dword (nibble*8 per byte, bit 7 =
-// byte_hi); one v_perm_b32 splices byte b of it under the wave-uniform
-// 2i + nib_hi -> 1 VALU/lookup.  The two bytes' tables for one nibble half sit
-// in disjoint banks, so lanes holding different bytes of their symbols (the
-// contiguous layout) look up conflict-free.
+// LDS table layout per input i (512 B, tab_idx in kernels.hpp): high-nibble
+// entries at i*512 + 16*v + 8*byte_hi, low-nibble entries at i*512 + 256 +
+// 128*byte_hi + 8*v (q = 2*byte_hi + nib_hi: low/high nibble of the symbol's
+// low/high byte).  A lookup address is byte 0 = the offset within the
+// 256-B half, bytes 1-2 = 2i + (low nibble).  Byte 0 for four symbols at once
+// is one mask of the data dword for high nibbles (x & 0xF0, | 8 for the high
+// byte: one v_bitop3) and a shift + mask for low nibbles (nibble*8, | 0x80 for
+// the high byte); one v_perm_b32 splices byte b of it under the wave-uniform
+// 2i + (low nibble) -> 1 VALU per lookup.
 #include "kernels.hpp"
 
 #include <algorithm>
@@ -50,32 +50,31 @@ __device__ __forceinline__ uint2 lds_entry(const char *, uint32_t byte_addr) {
   return make_uint2(uint32_t(v), uint32_t(v >> 32));
 }
 
-// Variant 1: v_perm addressing + 3-input XOR.  L/H: the two byte registers of
-// 16 symbols; flag_l/flag_h: 0x80808080 for the register holding high bytes,
-// 0 for low bytes; base_even = 2i, base_odd = 2i + 1.
-__device__ __forceinline__ void mac_input_v1(const uint4 &L, const uint4 &H, uint32_t flag_l,
-                                             uint32_t flag_h, uint32_t base_even,
-                                             uint32_t base_odd, uint32_t (&acc_lo)[16],
+// GF multiply-accumulate of one input into 16 symbols: v_perm addressing +
+// 3-input XOR.  L/H: the low-byte and high-byte registers of the lane's 16
+// symbols; base_hi = 2i (high-nibble half of input i's table), base_lo =
+// 2i + 1 (low-nibble half).
+__device__ __forceinline__ void mac_input_v1(const uint4 &L, const uint4 &H, uint32_t base_hi,
+                                             uint32_t base_lo, uint32_t (&acc_lo)[16],
                                              uint32_t (&acc_hi)[16]) {
   const uint32_t l[4] = {L.x, L.y, L.z, L.w};
   const uint32_t h[4] = {H.x, H.y, H.z, H.w};
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
-    // nibble*8 per byte | flag; for the high-byte words (x & M) | F is one
-    // v_bitop3 (0xEA), measured -0.7% launch time over v_and + v_or
-    const uint32_t ll = ((l[d] << 3) & 0x78787878u) | flag_l;
-    const uint32_t lh = ((l[d] >> 1) & 0x78787878u) | flag_l;
-    const uint32_t hl = __builtin_amdgcn_bitop3_b32(h[d] << 3, 0x78787878u, flag_h, 0xEA);
-    const uint32_t hh = __builtin_amdgcn_bitop3_b32(h[d] >> 1, 0x78787878u, flag_h, 0xEA);
+    // address bytes of 4 symbols; (x & M) | F is one v_bitop3 (0xEA)
+    const uint32_t ll = (l[d] << 3) & 0x78787878u;                                    // 8*v
+    const uint32_t lh = l[d] & 0xF0F0F0F0u;                                           // 16*v
+    const uint32_t hl = __builtin_amdgcn_bitop3_b32(h[d] << 3, 0x78787878u, 0x80808080u, 0xEA);
+    const uint32_t hh = __builtin_amdgcn_bitop3_b32(h[d], 0xF0F0F0F0u, 0x08080808u, 0xEA);
     uint2 e[4][4];
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       // selector: byte0 <- byte b of the nibble word, byte1..2 <- base, byte3 <- 0
       const uint32_t sel = 0x0C050400u | uint32_t(b);
-      e[b][0] = lds_entry(nullptr, __builtin_amdgcn_perm(base_even, ll, sel));
-      e[b][1] = lds_entry(nullptr, __builtin_amdgcn_perm(base_odd, lh, sel));
-      e[b][2] = lds_entry(nullptr, __builtin_amdgcn_perm(base_even, hl, sel));
-      e[b][3] = lds_entry(nullptr, __builtin_amdgcn_perm(base_odd, hh, sel));
+      e[b][0] = lds_entry(nullptr, __builtin_amdgcn_perm(base_lo, ll, sel));
+      e[b][1] = lds_entry(nullptr, __builtin_amdgcn_perm(base_hi, lh, sel));
+      e[b][2] = lds_entry(nullptr, __builtin_amdgcn_perm(base_lo, hl, sel));
+      e[b][3] = lds_entry(nullptr, __builtin_amdgcn_perm(base_hi, hh, sel));
     }
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
@@ -86,7 +85,7 @@ __device__ __forceinline__ void mac_input_v1(const uint4 &L, const uint4 &H, uin
   }
 }
 
-// Variant 9 (measurement only, NOT a codec): same memory traffic, no tables.
+// Traffic-only probe (measurement only, NOT a codec): same memory traffic, no tables.
 // The XORs are asm so the compiler cannot fold "0 ^ load" into a register
 // copy of a load that is still in flight (tools/inflight_check.py).
 __device__ __forceinline__ void mac_input_stream(const uint4 &L, const uint4 &H,
@@ -261,7 +260,7 @@ __device__ __forceinline__ bool ring_acc_halfchunk(const KernArgs &args, const P
                            acc_lo, acc_hi);
         else
           mac_input_v1(make_uint4(Lv.x, Lv.y, Lv.z, Lv.w), make_uint4(Hv.x, Hv.y, Hv.z, Hv.w),
-                       0u, 0x80808080u, 2 * r, 2 * r + 1, acc_lo, acc_hi);
+                       2 * r, 2 * r + 1, acc_lo, acc_hi);
       });
   return true;
 }
