@@ -17,7 +17,7 @@
 // outputs: low dword = the outputs' low bytes, high dword = their high bytes.
 // A 16-entry x 8-byte table spans 32 LDS banks, so a ds_read_b64 with any
 // nibble per lane is bank-conflict free.  Per symbol and input: 4 LDS lookups
-// and ~10 VALU, independent of the number of outputs (<= 4).
+// and ~9.6 VALU, independent of the number of outputs (<= 4).
 //
 // LDS table layout per input i (512 B, tab_idx in kernels.hpp): high-nibble
 // entries at i*512 + 16*v + 8*byte_hi, low-nibble entries at i*512 + 256 +
