@@ -302,7 +302,7 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dist = None
-    if world > 1:
+    if world > 1 or "TORCHELASTIC_RUN_ID" in os.environ:  # under torchrun: RCCL even at N=1
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
@@ -384,9 +384,9 @@ def main():
         step()
     ev1.record(stream)
     torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0  # this rank's K steps; the job time is the max over ranks
     if dist:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
     launch_ms = ev0.elapsed_time(ev1) / (2 * args.steps)
     elapsed = parallel.max_over_ranks(elapsed, dist, device="cuda")
 
