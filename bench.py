@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--segment-bytes", type=int, default=32 * 1024 * 1024)
     ap.add_argument("--pitch", type=int, default=-1,
                     help="shard row pitch in bytes (-1 = bfrs_shard_pitch; A/B of the HBM layout)")
+    ap.add_argument("--layout", choices=["single", "separate"], default="separate",
+                    help="shard sets in one device allocation or one each")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-shard-bytes", type=int, default=8 * 1024 * 1024)
     ap.add_argument("--cpu-threads", type=int, default=0)
@@ -319,12 +321,22 @@ def main():
 
     # ---- resident workload (this rank's bytes of every segment)
     # every shard set is one allocation with rows bfrs_shard_pitch(S) apart
-    def shards(n):
-        if args.pitch < 0:
-            return bfrs.empty_shards(n, S)
-        buf = torch.empty(n * max(args.pitch, S), dtype=torch.uint8, device="cuda")
-        return buf.as_strided((n, S), (max(args.pitch, S), 1))
-    data = shards(nseg)
+    # Shard rows pitch = bfrs_shard_pitch(S) apart.  --layout single: data,
+    # parity and restored rows in one allocation (as the archive pipeline's
+    # arenas hold a block's k + 3 slots); separate: one allocation per set.
+    pitch = bfrs.shard_pitch(S) if args.pitch < 0 else max(args.pitch, S)
+    n_rows = {"data": nseg, "parity": 3 * nb, "restored": 3 * nb}
+    if args.layout == "single":
+        whole = torch.empty(sum(n_rows.values()) * pitch, dtype=torch.uint8, device="cuda")
+    sets, row0 = {}, 0
+    for name, n in n_rows.items():
+        if args.layout == "single":
+            sets[name] = whole[row0 * pitch:].as_strided((n, S), (pitch, 1))
+            row0 += n
+        else:
+            buf = torch.empty(n * pitch, dtype=torch.uint8, device="cuda")
+            sets[name] = buf.as_strided((n, S), (pitch, 1))
+    data = sets["data"]
     if args.strong:
         row = torch.empty(S_full, dtype=torch.uint8, device="cuda")
         for s in range(nseg):
@@ -334,8 +346,7 @@ def main():
     else:
         for s in range(nseg):
             synth.fill_segment_torch(data[s], seed, s)
-    parity = shards(3 * nb)
-    restored = shards(3 * nb)
+    parity, restored = sets["parity"], sets["restored"]
     enc_in = [data[s] for s in range(nseg)]
     enc_out = [parity[i] for i in range(3 * nb)]
     dec_in, dec_out, seg = [], [], 0
@@ -457,7 +468,7 @@ def main():
                          if args.strong else
                          "BASELINE configs[1]+[2]: 128 x 32 MiB segments = 4xRS(30,3)+1xRS(8,3); "
                          "step = encode batch + 3-erasure decode of every block"),
-            "segments": nseg, "segment_bytes": S_full, "shard_pitch": int(data.stride(0)), "blocks": shapes, "parity_shards": 3,
+            "segments": nseg, "segment_bytes": S_full, "shard_pitch": int(data.stride(0)), "layout": args.layout, "blocks": shapes, "parity_shards": 3,
             "parallelism": (f"64-B column stripes x{world}" if args.strong
                             else f"independent batch per GPU x{world}"),
         },
