@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
 from typing import Optional, Sequence
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -92,11 +93,27 @@ _sz = ctypes.c_size_t
 _pp = ctypes.POINTER(ctypes.c_void_p)
 
 
+def _torch_runtime_first() -> None:
+    """Load PyTorch's ROCm runtime before libbfrs.so when torch is installed.
+
+    torch bundles its own HIP/ROCr libraries.  If libbfrs.so (linked against
+    /opt/rocm) loads first, the two HIP runtimes end up with separate device
+    state and whichever initialises the GPU second sees no device (measured on
+    the MI355X boxes: `bfrs.lib(); torch.cuda.is_available(); bfrs.Context(0)`
+    fails with BFRS_E_NO_DEVICE).  Loaded in the other order they share the
+    process's ROCr and both work, so the binding imports torch first.  Hosts
+    without torch (a Rust caller of the C-ABI) are unaffected."""
+    import importlib.util
+    if "torch" not in sys.modules and importlib.util.find_spec("torch") is not None:
+        import torch  # noqa: F401
+
+
 def lib() -> ctypes.CDLL:
     global _lib
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"libbfrs.so not built at {LIB_PATH}; run __graft_entry__.build()")
+        _torch_runtime_first()
         L = ctypes.CDLL(LIB_PATH)
         sig = {
             "bfrs_abi_version": ([], ctypes.c_int),

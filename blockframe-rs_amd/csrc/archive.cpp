@@ -126,7 +126,9 @@ int Commit::rs13_segments(size_t nseg, bool cv_hash, std::vector<uint8_t> *seg_c
   hashes->assign(nseg, {});
   if (cv_hash) seg_cvs->assign(nseg * 32, 0);
   const size_t slot = (std::min(S, m.n) + 63) / 64 * 64;
-  Arena arena[2], pbuf[2];
+  StagingCache &sc = staging(ctx);
+  std::lock_guard<std::mutex> staging_lock(sc.mu);
+  Arena *arena = sc.a, *pbuf = sc.a + 2;
   for (int i = 0; i < 2; ++i) {
     int rc = arena[i].reserve(slot, 4 * std::min(kRound, nseg));
     if (rc) return rc;
@@ -321,9 +323,11 @@ int Commit::tier3(std::string *out_dir) {
   const bool cv_hash = pow2_kib(S) && nseg >= 2;
   std::vector<uint8_t> seg_cvs(cv_hash ? nseg * 32 : 0);
   std::vector<std::string> block_roots(nblocks);
-  Arena arena[2];
-  for (auto &a : arena) {
-    int rc = a.reserve(S, kBlockSegments + kParity);
+  StagingCache &sc = staging(ctx);
+  std::lock_guard<std::mutex> staging_lock(sc.mu);
+  Arena *arena = sc.a, *pbuf = sc.a + 2;  // pbuf: pinned parity of the block being written
+  for (int i = 0; i < 2; ++i) {
+    int rc = arena[i].reserve(S, kBlockSegments + kParity);
     if (rc) return rc;
   }
   auto geom = [&](size_t b, size_t *s0, size_t *k, size_t *shard) {
@@ -341,9 +345,8 @@ int Commit::tier3(std::string *out_dir) {
       if (len < shard) std::memset(a.hs(s) + len, 0, shard - len);
     });
   };
-  Arena pbuf[2];  // pinned parity of the block being written (device side unused)
-  for (auto &a : pbuf) {
-    int rc = a.reserve(S, kParity);
+  for (int i = 0; i < 2; ++i) {
+    int rc = pbuf[i].reserve(S, kParity);
     if (rc) return rc;
   }
   std::atomic<bool> write_ok{true};
@@ -792,7 +795,9 @@ int bfrs_repair(bfrs_ctx *ctx, const char *archive_dir, bfrs_repair_report *repo
   int rc = load_geometry(archive_dir, &g);
   if (rc) return rc;
   if (g.mf.tier == 3) {  // repair_blocked (health.rs:642-765), intended semantics
-    Arena a;
+    StagingCache &sc = staging(ctx);
+    std::lock_guard<std::mutex> staging_lock(sc.mu);
+    Arena &a = sc.a[0];
     for (const auto &kv : g.mf.blocks) {
       const size_t b = size_t(kv.first);
       BlockState bs;
@@ -878,7 +883,9 @@ int bfrs_health_check(bfrs_ctx *ctx, const char *archive_dir, char *json_out, si
     else ++unrecoverable;
   };
   if (g.mf.tier == 3) {
-    Arena a;
+    StagingCache &sc = staging(ctx);
+    std::lock_guard<std::mutex> staging_lock(sc.mu);
+    Arena &a = sc.a[0];
     for (const auto &kv : g.mf.blocks) {
       const size_t b = size_t(kv.first);
       BlockState bs;

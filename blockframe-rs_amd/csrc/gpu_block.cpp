@@ -34,6 +34,13 @@ int Arena::reserve(size_t slot_bytes, size_t n) {
   return BFRS_OK;
 }
 
+StagingCache &staging(bfrs_ctx *ctx) {
+  Context &c = ctx->impl;
+  std::lock_guard<std::mutex> l(c.staging_init);
+  if (!c.staging) c.staging = std::make_shared<StagingCache>();
+  return *static_cast<StagingCache *>(c.staging.get());
+}
+
 int gpu_hash_hex(bfrs_ctx *ctx, const std::vector<const uint8_t *> &d_msgs,
                  const std::vector<size_t> &lens, std::vector<std::string> *hex,
                  const uint64_t *chunk_offsets, std::vector<uint8_t> *cvs) {

@@ -12,6 +12,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -37,6 +38,15 @@ struct Arena {
 int gpu_hash_hex(bfrs_ctx *ctx, const std::vector<const uint8_t *> &d_msgs,
                  const std::vector<size_t> &lens, std::vector<std::string> *hex,
                  const uint64_t *chunk_offsets = nullptr, std::vector<uint8_t> *cvs = nullptr);
+
+// The context's staging arenas (Context::staging): archive calls on one
+// context take `mu` for their duration and use a[0..1] as block arenas and
+// a[2..3] as parity buffers.  Arenas grow and are never shrunk.
+struct StagingCache {
+  std::mutex mu;
+  Arena a[4];
+};
+StagingCache &staging(bfrs_ctx *ctx);
 
 // State of tier-3 block b in an Arena: slots [0, k) segments, [k, k+3) parity.
 struct BlockState {

@@ -94,6 +94,7 @@ static int upload_plan(Plan *p) {
 Context::~Context() {
   if (device >= 0) (void)hipSetDevice(device);
   if (stream) (void)hipStreamSynchronize(stream);
+  staging.reset();  // archive staging arenas (pinned + device)
   plans.clear();
   if (d_scratch) (void)hipFree(d_scratch);
   for (auto &ps : pipe_stream)

@@ -95,6 +95,12 @@ struct Context {
   void *pipe_buf = nullptr;
   size_t pipe_cap = 0;  // bytes per slot
 
+  // Pinned-host + device staging arenas of the archive pipeline
+  // (gpu_block.hpp StagingCache, type-erased here), kept across calls:
+  // pinning a GiB per commit or repair cost more than the work itself.
+  std::shared_ptr<void> staging;
+  std::mutex staging_init;
+
   // BLAKE3 (hash_gpu.cpp): device work area + pinned descriptor/result area.
   void *d_hash = nullptr;
   size_t d_hash_cap = 0;

@@ -442,3 +442,18 @@ def test_repair_tier3_parity_only(ctx, bfrs, tmp_path):
     for p in range(3):
         assert np.array_equal(_read(os.path.join(pdir, f"block_parity_{p}.dat")), good[p])
     assert bfrs.health_check(ctx, adir)["status"] == "Healthy"
+
+
+def test_binding_loads_torch_runtime_first():
+    """bfrs.lib() before torch, then torch initialises the GPU, then a context
+    opens: the binding must have loaded torch's ROCm runtime first
+    (bfrs._torch_runtime_first), or the second HIP runtime sees no device."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys; sys.path.insert(0, 'blockframe-rs_amd'); import bfrs; bfrs.lib(); "
+            "import torch; assert torch.cuda.is_available(); c = bfrs.Context(0); c.close(); "
+            "print('ok')")
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
