@@ -649,6 +649,7 @@ class Archive:
         _check(lib().bfrs_archive_open(ctx.handle, os.fsencode(archive_dir), cache_segments,
                                        1 if write_back else 0, ctypes.byref(h)))
         self.handle = h.value
+        self._read = lib().bfrs_archive_read
 
     @property
     def size(self) -> int:
@@ -659,9 +660,17 @@ class Archive:
     def read_into(self, offset: int, out) -> int:
         import numpy as np
         a = out if isinstance(out, np.ndarray) else np.frombuffer(out, dtype=np.uint8)
-        n = _sz()
-        _check(lib().bfrs_archive_read(self.handle, offset, a.size,
-                                       a.ctypes.data if a.size else None, ctypes.byref(n)))
+        if a.size and not a.flags.c_contiguous:
+            raise ValueError("read_into: destination must be C-contiguous")
+        return self.read_into_ptr(offset, a.__array_interface__["data"][0] if a.size else 0,
+                                  a.size)
+
+    def read_into_ptr(self, offset: int, addr: int, size: int) -> int:
+        """bfrs_archive_read into host memory at `addr` (the FUSE reply buffer's
+        role): no per-call buffer objects, so a request loop measures the read
+        path rather than Python."""
+        n = _sz()  # per call: readers on other threads share this handle
+        _check(self._read(self.handle, offset, size, addr or None, ctypes.byref(n)))
         return n.value
 
     def read(self, offset: int, size: int) -> bytes:

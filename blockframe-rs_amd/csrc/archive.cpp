@@ -20,12 +20,14 @@
 #include <cctype>
 #include <condition_variable>
 #include <cstring>
+#include <deque>
 #include <list>
 #include <memory>
 #include <mutex>
 #include <sstream>
 #include <thread>
 #include <unordered_map>
+#include <unordered_set>
 
 #include "archive_io.hpp"
 #include "blake3.hpp"
@@ -522,9 +524,12 @@ using SegPtr = std::shared_ptr<Seg>;
 // Archive read handle (src/mount/filesystem_unix.rs:176-305 + cache.rs).
 // Segments are cached in pinned buffers (LRU); a miss reads the file,
 // verifies it on the GPU and, if it is missing or corrupt, reconstructs it
-// (tier 3: RS(k,3) decode of its block on the GPU, device re-verify).  A
-// prefetch thread loads and verifies the next segment when reads move to a
-// new one, so sequential reads overlap disk/PCIe/hash with serving.
+// (tier 3: RS(k,3) decode of its block on the GPU, device re-verify).  When
+// reads move to a new segment, the next kPrefetchDepth segments are queued
+// for kPrefetchWorkers threads that load and verify them (reconstructing a
+// damaged one with its block), so sequential reads
+// overlap file reads, PCIe and hashing with serving (the file read of one
+// segment overlaps the GPU verify of another).
 struct bfrs_archive {
   bfrs_ctx *ctx = nullptr;
   Geometry g;
@@ -538,10 +543,13 @@ struct bfrs_archive {
   std::list<size_t> lru;
   std::unordered_map<size_t, std::pair<SegPtr, std::list<size_t>::iterator>> cache;
   bfrs_archive_stats st{};
-  long long want = -1, inflight = -1, last_gi = -1;
+  static constexpr size_t kPrefetchDepth = 4, kPrefetchWorkers = 2;
+  std::deque<size_t> wantq;               // queued, not started
+  std::unordered_set<size_t> inflight;    // being loaded by a prefetch worker
+  long long last_gi = -1;
   long long reader_gi = -1;  // segment a reader is loading itself (prefetch skips it)
   bool stop = false;
-  std::thread worker;
+  std::vector<std::thread> workers;
 
   std::mutex gpu_mu;  // the context and the arena (one user at a time)
   Arena arena;
@@ -552,7 +560,8 @@ struct bfrs_archive {
       stop = true;
     }
     cv.notify_all();
-    if (worker.joinable()) worker.join();
+    for (auto &w : workers)
+      if (w.joinable()) w.join();
     cache.clear();
   }
 
@@ -627,6 +636,13 @@ int bfrs_archive::recover(size_t gi, SegPtr *out) {
     std::vector<std::pair<size_t, SegPtr>> restored;
     {
       std::lock_guard<std::mutex> lg(gpu_mu);
+      {  // another thread's reconstruction of this block may have restored it meanwhile
+        std::lock_guard<std::mutex> l(mu);
+        if (SegPtr c = lookup(gi)) {
+          *out = c;
+          return BFRS_OK;
+        }
+      }
       const size_t b = gi / kBlockSegments;
       BlockState bs;
       int rc = load_block(ctx, g, b, arena, &bs);
@@ -687,23 +703,28 @@ int bfrs_archive::recover(size_t gi, SegPtr *out) {
 void bfrs_archive::prefetch_loop() {
   std::unique_lock<std::mutex> l(mu);
   for (;;) {
-    cv.wait(l, [&] { return stop || want >= 0; });
+    cv.wait(l, [&] { return stop || !wantq.empty(); });
     if (stop) return;
-    const size_t gi = size_t(want);
-    want = -1;
-    if (cache.count(gi) || reader_gi == (long long)gi) continue;
-    inflight = (long long)gi;
+    const size_t gi = wantq.front();
+    wantq.pop_front();
+    if (cache.count(gi) || inflight.count(gi) || reader_gi == (long long)gi) continue;
+    inflight.insert(gi);
     l.unlock();
     SegPtr seg;
     bool ok = false;
-    const int rc = load_clean(gi, &seg, &ok);  // damaged segments are left to the reader
+    int rc = load_clean(gi, &seg, &ok);
+    bool restored = false;
+    if (rc == BFRS_OK && !ok) {  // damaged: reconstruct it (and its block's siblings) ahead of the reader
+      rc = recover(gi, &seg);
+      restored = rc == BFRS_OK;
+    }
     l.lock();
-    if (rc == BFRS_OK && ok) {
+    if (rc == BFRS_OK && (ok || restored)) {
       put(gi, seg);
-      ++st.verified;
+      st.verified += ok;
       ++st.prefetched;
     }
-    inflight = -1;
+    inflight.erase(gi);
     cv.notify_all();
   }
 }
@@ -984,7 +1005,9 @@ int bfrs_archive_open(bfrs_ctx *ctx, const char *archive_dir, size_t cache_segme
   if (rc) return rc;
   a->pool = std::make_shared<PinnedPool>(a->g.S);
   a->prefetch = a->g.nseg > 1;
-  if (a->prefetch) a->worker = std::thread(&bfrs_archive::prefetch_loop, a.get());
+  if (a->prefetch)
+    for (size_t w = 0; w < bfrs_archive::kPrefetchWorkers; ++w)
+      a->workers.emplace_back(&bfrs_archive::prefetch_loop, a.get());
   *out = a.release();
   return BFRS_OK;
   BFRS_API_END
@@ -1014,12 +1037,13 @@ int bfrs_archive_read(bfrs_archive *a, uint64_t offset, size_t len, uint8_t *out
     SegPtr seg = a->lookup(gi);
     if (seg) {
       ++a->st.hits;
-    } else if (a->inflight == (long long)gi) {  // the prefetcher is loading it
-      a->cv.wait(l, [&] { return a->inflight != (long long)gi; });
+    } else if (a->inflight.count(gi)) {  // a prefetch worker is loading it
+      a->cv.wait(l, [&] { return !a->inflight.count(gi); });
       continue;
     } else {
       ++a->st.misses;
-      if (a->want == (long long)gi) a->want = -1;  // not started yet: load it here instead
+      // queued but not started: load it here instead
+      a->wantq.erase(std::remove(a->wantq.begin(), a->wantq.end(), gi), a->wantq.end());
       a->reader_gi = (long long)gi;
       l.unlock();
       bool ok = false;
@@ -1033,11 +1057,16 @@ int bfrs_archive_read(bfrs_archive *a, uint64_t offset, size_t len, uint8_t *out
     }
     if (a->prefetch && (long long)gi != a->last_gi) {  // moved to a new segment
       a->last_gi = (long long)gi;
-      const size_t nx = gi + 1;
-      if (nx < a->g.nseg && !a->cache.count(nx) && a->inflight != (long long)nx) {
-        a->want = (long long)nx;
-        a->cv.notify_all();
-      }
+      // the next segments, at most half the cache so they are not evicted unread
+      const size_t depth = std::min(bfrs_archive::kPrefetchDepth, std::max<size_t>(1, a->cap / 2));
+      bool queued = false;
+      for (size_t nx = gi + 1; nx <= gi + depth && nx < a->g.nseg; ++nx)
+        if (!a->cache.count(nx) && !a->inflight.count(nx) &&
+            std::find(a->wantq.begin(), a->wantq.end(), nx) == a->wantq.end()) {
+          a->wantq.push_back(nx);
+          queued = true;
+        }
+      if (queued) a->cv.notify_all();
     }
     if (in_seg >= seg->n) return set_error(BFRS_E_WRAPPER, "segment shorter than manifest size");
     const size_t n = std::min(len - *nread, seg->n - in_seg);
