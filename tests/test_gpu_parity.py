@@ -96,6 +96,40 @@ def test_batch_decode_random_erasures_vs_oracle(ctx, oracle):
         off += k
 
 
+def test_every_k_1_to_30_one_batch(ctx, oracle):
+    """One encode launch and one decode launch over 30 blocks with k = 1..30
+    (every block shape BlockFrame's tier 3 can produce, odd k included: the
+    unrotated padded passes), a ragged shard size, all against the oracle."""
+    n = 3 * 8192 + 64 * 5 + 38
+    ks = list(range(1, 31))
+    rng = np.random.default_rng(130)
+    host = [[rng.integers(0, 256, n, dtype=np.uint8) for _ in range(k)] for k in ks]
+    d_orig = [t for blk in host for t in _dev_shards(blk)]
+    d_rec = [torch.empty(n, dtype=torch.uint8, device="cuda") for _ in range(3 * len(ks))]
+    ctx.encode_batch_dev(ks, 3, n, d_orig, d_rec)
+    torch.cuda.synchronize()
+    pars = []
+    for b, blk in enumerate(host):
+        want = oracle.encode(blk, 3)
+        pars.append(want)
+        for j in range(3):
+            assert np.array_equal(d_rec[3 * b + j].cpu().numpy(), want[j]), (ks[b], j)
+    dd_orig, d_out, erased = [], [], []
+    for b, k in enumerate(ks):
+        er = sorted(rng.choice(k, size=min(3, k), replace=False).tolist())
+        erased.append(er)
+        for i in range(k):
+            dd_orig.append(None if i in er else d_orig[sum(ks[:b]) + i])
+            d_out.append(torch.empty(n, dtype=torch.uint8, device="cuda") if i in er else None)
+    ctx.decode_batch_dev(ks, 3, n, dd_orig, d_rec, d_out)
+    torch.cuda.synchronize()
+    off = 0
+    for b, k in enumerate(ks):
+        for i in erased[b]:
+            assert np.array_equal(d_out[off + i].cpu().numpy(), host[b][i]), (k, i)
+        off += k
+
+
 def test_many_blocks_round_trip(ctx, oracle):
     """Enough blocks that every persistent workgroup of the phased/streamed
     kernels walks several super-tiles across passes with different tables
