@@ -21,6 +21,9 @@ int Context::blake3_dev(size_t n, const uint8_t *const *d_msgs, const size_t *le
   if (!d_msgs || !lens || !digests)
     return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_blake3_batch_dev: NULL argument");
   if (n > (1u << 30)) return set_error(BFRS_E_INVALID_ARGUMENT, "too many messages");
+  // the work areas below are per context; archive handles call this from
+  // their prefetch threads while the owner may hash on the same context
+  std::lock_guard<std::mutex> hash_lock(hash_mu);
   HIP_TRY(hipSetDevice(device));
 
   // kernel-1 groups (messages in order, groups of a message contiguous)

@@ -101,7 +101,9 @@ struct Context {
   std::shared_ptr<void> staging;
   std::mutex staging_init;
 
-  // BLAKE3 (hash_gpu.cpp): device work area + pinned descriptor/result area.
+  // BLAKE3 (hash_gpu.cpp): device work area + pinned descriptor/result area,
+  // guarded by hash_mu (callers on several threads may share a context).
+  std::mutex hash_mu;
   void *d_hash = nullptr;
   size_t d_hash_cap = 0;
   void *h_hash = nullptr;

@@ -19,6 +19,9 @@
  * Threading: a context may be used by one thread at a time; distinct
  * contexts may be used concurrently (also on the same device), mirroring
  * rayon's one-encoder-per-block use at src/chunker/commit.rs:391-466.
+ * Exceptions, serialised inside the library: the archive calls (commit,
+ * repair, health check) and an open archive handle, whose prefetch threads
+ * and readers share its context; a handle may be read from several threads.
  */
 #ifndef BFRS_H
 #define BFRS_H
