@@ -291,9 +291,20 @@ __device__ __forceinline__ void ring_tile_halfchunk(const KernArgs &args, const 
 
 // The ring kernel: workgroup wg owns tiles_per_wg consecutive 8 KiB tiles of
 // one pass (one by default); ROT picks the read order (ring_acc_halfchunk).
-template <int ROT, bool PROBE = false>
+// XGRP: workgroup -> tile remap so that the 16 tiles of a read group run on
+// one XCD (hardware deals workgroups round-robin over the 8 XCDs): within
+// each full run of 128 workgroups, XCD x's q-th workgroup takes tile
+// 16 * (8 * (q / 16) + x) + q % 16.  Bijective; speed only.
+__device__ __forceinline__ uint32_t xcd_group_remap(uint32_t b, uint32_t n) {
+  const uint32_t full = n & ~127u;
+  if (b >= full) return b;
+  const uint32_t base = b & ~127u, r = b & 127u, x = r & 7u, q = r >> 3;
+  return base + 16u * (8u * (q >> 4) + x) + (q & 15u);
+}
+
+template <int ROT, bool PROBE = false, bool XGRP = false>
 __global__ __launch_bounds__(256, 5) void gf_apply_ring_kernel(const KernArgs args) {
-  const uint32_t wg = blockIdx.x;
+  const uint32_t wg = XGRP ? xcd_group_remap(blockIdx.x, gridDim.x) : blockIdx.x;
   const PassDesc &P = enter_pass(args, wg);
   const uint32_t t_begin = (wg - P.wg_begin) * args.tiles_per_wg;
   const uint32_t t_end = min(t_begin + args.tiles_per_wg, P.n_tiles);
@@ -338,16 +349,17 @@ __global__ __launch_bounds__(64) void gf_tail_kernel(const KernArgs args) {
 }  // namespace
 
 // Kernel variant selector for A/B measurement (tools/kbench.py).
-// 41 (default): one input rotation per group of 16 consecutive tiles (the 16
+// 58 (default): 41 with each read group's 16 workgroups on one XCD.
+// 41: one input rotation per group of 16 consecutive tiles (the 16
 // workgroups stream one shard's 128 KiB together); 36 / 40 / 42: groups of
 // 1 / 8 / 32 tiles; 5: one rotation per wave (each wave of a tile on its own
-// shard); 37: no rotation; 44: traffic-only probe of 41 (wrong output; refused
+// shard); 37: no rotation; 44: traffic-only probe of 58 (wrong output; refused
 // unless BFRS_ALLOW_PROBE=1).  Rejected variants were removed; their code is
 // in the git history and their results in DESIGN.md §9.
 int kernel_variant() {
   const char *e = std::getenv("BFRS_KERNEL_VARIANT");
-  int v = e ? atoi(e) : 41;
-  if (v == 44 && !std::getenv("BFRS_ALLOW_PROBE")) v = 41;
+  int v = e ? atoi(e) : 58;
+  if (v == 44 && !std::getenv("BFRS_ALLOW_PROBE")) v = 58;
   return v;
 }
 
@@ -374,10 +386,13 @@ hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in
       hipLaunchKernelGGL((gf_apply_ring_kernel<7>), dim3(n_wgs), dim3(256), lds, stream, args);
       break;
     case 44:
-      hipLaunchKernelGGL((gf_apply_ring_kernel<6, true>), dim3(n_wgs), dim3(256), lds, stream, args);
+      hipLaunchKernelGGL((gf_apply_ring_kernel<6, true, true>), dim3(n_wgs), dim3(256), lds, stream, args);
       break;
-    default:  // 41
+    case 41:
       hipLaunchKernelGGL((gf_apply_ring_kernel<6>), dim3(n_wgs), dim3(256), lds, stream, args);
+      break;
+    default:  // 58: 41 with each read group's 16 workgroups on one XCD
+      hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, true>), dim3(n_wgs), dim3(256), lds, stream, args);
   }
   return hipGetLastError();
 }

@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out
 mkdir -p "$OUT"
 TAG=${TAG:-r01}
-for v in ${VARIANTS:-5 36 37 40 42}; do
+for v in ${VARIANTS:-5 36 37 40 41 42}; do
   BFRS_KERNEL_VARIANT=$v timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -q -m gpu \
       --timeout 240 --timeout-method thread -k "golden or mixed or random or multiphase or many" \
       > "$OUT/pytest_v${v}_$TAG.log" 2>&1
