@@ -291,20 +291,22 @@ __device__ __forceinline__ void ring_tile_halfchunk(const KernArgs &args, const 
 
 // The ring kernel: workgroup wg owns tiles_per_wg consecutive 8 KiB tiles of
 // one pass (one by default); ROT picks the read order (ring_acc_halfchunk).
-// XGRP: workgroup -> tile remap so that the 16 tiles of a read group run on
-// one XCD (hardware deals workgroups round-robin over the 8 XCDs): within
-// each full run of 128 workgroups, XCD x's q-th workgroup takes tile
-// 16 * (8 * (q / 16) + x) + q % 16.  Bijective; speed only.
+// XG > 0: workgroup -> tile remap so that XG consecutive tiles (a read
+// group) run on one XCD (hardware deals workgroups round-robin over the 8
+// XCDs): within each full run of 8*XG workgroups, XCD x's q-th workgroup
+// takes tile XG * (8 * (q / XG) + x) + q % XG.  Bijective; speed only.
+template <uint32_t XG>
 __device__ __forceinline__ uint32_t xcd_group_remap(uint32_t b, uint32_t n) {
-  const uint32_t full = n & ~127u;
+  constexpr uint32_t run = 8 * XG;
+  const uint32_t full = n / run * run;
   if (b >= full) return b;
-  const uint32_t base = b & ~127u, r = b & 127u, x = r & 7u, q = r >> 3;
-  return base + 16u * (8u * (q >> 4) + x) + (q & 15u);
+  const uint32_t base = b / run * run, r = b - base, x = r & 7u, q = r >> 3;
+  return base + XG * (8u * (q / XG) + x) + q % XG;
 }
 
-template <int ROT, bool PROBE = false, bool XGRP = false>
+template <int ROT, bool PROBE = false, uint32_t XG = 0>
 __global__ __launch_bounds__(256, 5) void gf_apply_ring_kernel(const KernArgs args) {
-  const uint32_t wg = XGRP ? xcd_group_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+  const uint32_t wg = XG ? xcd_group_remap<XG>(blockIdx.x, gridDim.x) : blockIdx.x;
   const PassDesc &P = enter_pass(args, wg);
   const uint32_t t_begin = (wg - P.wg_begin) * args.tiles_per_wg;
   const uint32_t t_end = min(t_begin + args.tiles_per_wg, P.n_tiles);
@@ -386,13 +388,13 @@ hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in
       hipLaunchKernelGGL((gf_apply_ring_kernel<7>), dim3(n_wgs), dim3(256), lds, stream, args);
       break;
     case 44:
-      hipLaunchKernelGGL((gf_apply_ring_kernel<6, true, true>), dim3(n_wgs), dim3(256), lds, stream, args);
+      hipLaunchKernelGGL((gf_apply_ring_kernel<6, true, 16>), dim3(n_wgs), dim3(256), lds, stream, args);
       break;
     case 41:
       hipLaunchKernelGGL((gf_apply_ring_kernel<6>), dim3(n_wgs), dim3(256), lds, stream, args);
       break;
     default:  // 58: 41 with each read group's 16 workgroups on one XCD
-      hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, true>), dim3(n_wgs), dim3(256), lds, stream, args);
+      hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16>), dim3(n_wgs), dim3(256), lds, stream, args);
   }
   return hipGetLastError();
 }
