@@ -90,6 +90,20 @@ def cpu_baseline(args):
     t_dec = time.perf_counter() - t0
     assert np.array_equal(out[0][12], data[0][12])
     gib = threads * 30 * n / 2**30
+    # single core, one RS(30,3) block of 2 MiB shards (also report 1 core)
+    n1 = 2 << 20
+    d1 = [[synth.segment_np(0xC1, i, n1) for i in range(30)]]
+    p1 = [[np.empty(n1, np.uint8) for _ in range(3)]]
+    t0 = time.perf_counter()
+    oracle.batch(eng, False, 1, [30], 3, n1, d1, [[None] * 3], p1)
+    t1_enc = time.perf_counter() - t0
+    o1 = [[None if i in (1, 12, 25) else d1[0][i] for i in range(30)]]
+    r1 = [[np.empty(n1, np.uint8) if i in (1, 12, 25) else None for i in range(30)]]
+    t0 = time.perf_counter()
+    oracle.batch(eng, True, 1, [30], 3, n1, o1, p1, r1)
+    t1_dec = time.perf_counter() - t0
+    assert np.array_equal(r1[0][25], d1[0][25])
+    gib1 = 30 * n1 / 2**30
     return {
         "value": round(2 * gib / (t_enc + t_dec), 3),
         "unit": "GiB/s",
@@ -98,6 +112,10 @@ def cpu_baseline(args):
         "engine": "avx2" if eng == oracle.ENGINE_AVX2 else "scalar",
         "encode_GiBps": round(gib / t_enc, 3),
         "decode_GiBps": round(gib / t_dec, 3),
+        "single_core": {"value": round(2 * gib1 / (t1_enc + t1_dec), 3),
+                        "encode_GiBps": round(gib1 / t1_enc, 3),
+                        "decode_GiBps": round(gib1 / t1_dec, 3),
+                        "sample": "1 block x RS(30,3) x 2 MiB shards, 1 thread"},
         "sample": f"{threads} blocks x RS(30,3) x {n // 2**20} MiB shards, one block per thread; "
                   "encode + 3-erasure decode (restatement of reed-solomon-simd 3.1.0, not the crate)",
     }
@@ -413,6 +431,13 @@ def main():
         torch.cuda.synchronize()
         return a.elapsed_time(b) / n
     enc_ms, dec_ms = per_launch(encode), per_launch(decode)
+    # reference point on this box: a plain device copy (torch copy_) moving the
+    # same read + write bytes as one gf_apply launch (SURVEY 8(d) "achievable")
+    alg_bytes_launch = sum(k + 3 for k in shapes) * S
+    cp_src = torch.empty(alg_bytes_launch // 2, dtype=torch.uint8, device="cuda")
+    cp_dst = torch.empty_like(cp_src)
+    copy_ms = per_launch(lambda _h: cp_dst.copy_(cp_src))
+    del cp_src, cp_dst
     # correctness guard on the measured buffers (compare on device)
     seg = 0
     for b, k in enumerate(shapes):
@@ -484,6 +509,10 @@ def main():
             "launch_ms": round(launch_ms, 4),
             "launch_ms_by_direction": {"encode": round(enc_ms, 4), "decode": round(dec_ms, 4)},
             "timing": "HIP events on the launch stream over the timed region / launches",
+            "device_copy_reference": {
+                "GBps": round(alg_bytes_launch / (copy_ms * 1e-3) / 1e9, 1),
+                "ms": round(copy_ms, 4),
+                "what": "torch copy_ of alg_bytes/2 bytes (same read + write bytes as one launch), same box"},
         },
         "cpu_baseline": cpu,
         "pcie_inclusive": pcie,

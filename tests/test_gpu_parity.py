@@ -448,3 +448,18 @@ def test_in_tree_library_is_the_one_loaded(bfrs):
     import ctypes.util  # noqa: F401
     maps = open("/proc/self/maps").read()
     assert bfrs.LIB_PATH in maps
+
+
+@pytest.mark.parametrize("byte", [0x00, 0xAB, 0xFF])
+def test_constant_byte_shards(ctx, oracle, byte):
+    """Constant-byte input (mirrors src/chunker/tests.rs:19-27's constant-fill
+    files): parity vs oracle, and a 3-erasure round trip."""
+    n = 8192 + 64
+    d = [np.full(n, byte, np.uint8) for _ in range(30)]
+    want = oracle.encode(d, 3)
+    got = ctx.encode(d, 3)
+    assert all(np.array_equal(a, b) for a, b in zip(got, want))
+    o = [None if i in (0, 15, 29) else d[i] for i in range(30)]
+    rest = ctx.decode(o, want)
+    for i in (0, 15, 29):
+        assert np.array_equal(rest[i], d[i])
