@@ -10,17 +10,31 @@ Both go through the C-ABI (bfrs_encode_batch_dev / bfrs_decode_batch_dev) on
 torch's current stream, one kernel launch each.
 
 value = original-data GiB processed by all ranks (encode + decode) / max-rank time.
-Multi-GPU (torchrun): every rank owns an independent batch (weak scaling, no
-collective on the data path; the only collectives are the barrier and the
-max-time reduction).
 
-Extra fields: per-direction GiB/s, `roofline` for gf_apply_kernel measured
-with HIP events on the launch stream, `cpu_baseline` = the oracle's AVX2
-engine (restatement of reed-solomon-simd, not the crate) on a bounded sample.
+Multi-GPU: one process per GPU.  `--gpus N` with N > 1 either runs under
+torchrun (WORLD_SIZE must equal N) or, without WORLD_SIZE, spawns the N rank
+processes itself before anything touches the GPU.  Every rank owns an
+independent batch (weak scaling, no collective on the data path; the only
+collectives are the barriers and the max-time reduction).
+
+Sub-objects of the same JSON line:
+  c4_strong    BASELINE configs[3]: 320 x 32 MiB (10 x RS(30,3) + 1 x RS(20,3)),
+               64-B column stripes of every shard over the ranks (strong scaling)
+  roofline     gf_apply launch time from HIP events on the launch stream;
+               traffic = PMC bytes of this launch shape (source file named)
+  cpu_baseline the oracle's AVX2 engine (restatement of reed-solomon-simd, not
+               the crate) on C2's exact blocks; host CPU model and core counts
+  crate_api    the crate-shaped host-memory path BlockFrame calls per block
+               (bfrs_generate_parity / bfrs_recover_segment_rs30_3)
+  pcie_inclusive  the same batch from pinned host memory (H2D + kernel + D2H)
+  c5           BASELINE configs[4]: read of a corrupted 4 GiB tier-3 archive
+               through the mount's read core (bfrs_archive_read)
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -29,9 +43,10 @@ sys.path.insert(0, os.path.join(ROOT, "blockframe-rs_amd"))
 
 METRIC = "GiB/s device-resident RS(30,3) encode & 3-erasure decode, 32MB segments"
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
@@ -47,81 +62,509 @@ def parse():
     ap.add_argument("--layout", choices=["single", "separate"], default="separate",
                     help="shard sets in one device allocation or one each")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
-    ap.add_argument("--cpu-shard-bytes", type=int, default=8 * 1024 * 1024)
-    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="threads for the all-cores CPU variants (0 = this host's CPU share)")
     ap.add_argument("--pcie", choices=["auto", "off"], default="auto",
                     help="also time the host-memory path (pinned buffers, H2D+kernel+D2H)")
+    ap.add_argument("--crate", choices=["auto", "off"], default="auto",
+                    help="time the crate-shaped per-block host API (N=1)")
+    ap.add_argument("--c4", choices=["auto", "off"], default="auto",
+                    help="c4_strong sub-object (configs[3], strong scaling over the ranks)")
+    ap.add_argument("--c4-segments", type=int, default=320)
+    ap.add_argument("--c5", choices=["auto", "off"], default="auto",
+                    help="c5 sub-object (configs[4], N=1)")
     ap.add_argument("--strong", action="store_true",
-                    help="config C4: one job (default 320 segments) column-striped over the ranks")
+                    help="value = config C4 (default 320 segments) column-striped over the ranks")
     ap.add_argument("--workload", choices=["c2c3", "c5"], default="c2c3",
-                    help="c5 = BASELINE configs[4]: read of a corrupted tier-3 archive through "
-                         "the mount's read path (bfrs_archive_read), end-to-end MB/s")
+                    help="c5 = only the BASELINE configs[4] read-path line")
     ap.add_argument("--c5-gib", type=float, default=4.0, help="c5 file size (SURVEY C5: 4 GiB)")
     ap.add_argument("--c5-read-bytes", type=int, default=128 << 10, help="FUSE max_read")
     ap.add_argument("--c5-dir", default=None, help="scratch directory (default $TMPDIR)")
-    a = ap.parse_args()
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                    help="process-group backend (nccl = RCCL on ROCm)")
+    ap.add_argument("--one-device", action="store_true",
+                    help="every rank uses device 0 (tests: 2 ranks on one GPU over gloo)")
+    ap.add_argument("--dump-dir", default=None,
+                    help="each rank writes its C4 parity stripes here (tests assemble them)")
+    ap.add_argument("--stub", action="store_true",
+                    help="CPU-only rehearsal of the launcher/partition/timing path: no GPU, "
+                         "the codec calls replaced by a stand-in (tests only, never a bench line)")
+    a = ap.parse_args(argv)
     if a.strong and a.segments == 128:
         a.segments = 320
+    if a.stub:
+        a.backend = "gloo"
+        a.cpu_baseline = a.pcie = a.crate = a.c5 = "off"
     return a
 
 
-def cpu_baseline(args):
-    """Oracle (AVX2 nibble-table engine, the crate's Avx2 technique) on host
-    cores: T independent RS(30,3) blocks, one per thread (rayon over blocks,
-    src/chunker/commit.rs:391), encode then 3-erasure decode."""
+# ---------------------------------------------------------------- launcher
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args) -> int:
+    """--gpus N without torchrun: start N rank processes (this process never
+    touches the GPU), wait, return the first non-zero exit code."""
+    port = _free_port()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rcs = [p.wait() for p in procs]
+    return next((rc for rc in rcs if rc), 0)
+
+
+class Runtime:
+    """Device, process group and clock of one rank (stub: CPU only)."""
+
+    def __init__(self, args):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        if self.world != args.gpus:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={self.world}")
+        import torch
+        self.torch = torch
+        self.stub = args.stub
+        if self.stub:
+            self.device = torch.device("cpu")
+        else:
+            self.device = torch.device("cuda", 0 if args.one_device else self.local)
+            torch.cuda.set_device(self.device)
+        self.dist = None
+        if self.world > 1 or "TORCHELASTIC_RUN_ID" in os.environ:  # under torchrun: RCCL even at N=1
+            import torch.distributed as dist
+            kw = {}
+            if args.backend == "nccl":
+                kw["device_id"] = self.device
+            dist.init_process_group(args.backend, **kw)
+            assert dist.get_world_size() == self.world == args.gpus
+            self.dist = dist
+        self.coll_device = "cpu" if args.backend == "gloo" else self.device
+
+    def sync(self):
+        if not self.stub:
+            self.torch.cuda.synchronize()
+
+    def barrier(self):
+        if self.dist:
+            self.dist.barrier()
+
+    def max_over_ranks(self, x: float) -> float:
+        from bfrs import parallel
+        return parallel.max_over_ranks(x, self.dist, device=self.coll_device)
+
+    def observed_world(self) -> int:
+        return self.dist.get_world_size() if self.dist else 1
+
+    def close(self):
+        if self.dist:
+            self.dist.destroy_process_group()
+
+
+def timed(rt, step, steps):
+    """K steps between barrier + synchronize on both sides; returns (this
+    rank's seconds, max over ranks)."""
+    rt.barrier()
+    rt.sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    rt.sync()
+    el = time.perf_counter() - t0
+    rt.barrier()
+    return el, rt.max_over_ranks(el)
+
+
+def settle(rt, step, ms):
+    """Untimed steps for `ms` of wall time (clock ramp)."""
+    n, t0 = 0, time.perf_counter()
+    while (time.perf_counter() - t0) * 1e3 < ms:
+        step()
+        n += 1
+        if n % 16 == 0:
+            rt.sync()
+    rt.sync()
+    return n
+
+
+# ---------------------------------------------------------------- workloads
+class ShardSets:
+    """Data, parity and restored shard rows of one batch, rows
+    bfrs_shard_pitch(S) apart, plus the pointer lists of one
+    encode and one 3-erasure decode of every block."""
+
+    def __init__(self, rt, shapes, S, layout="separate", pitch=-1):
+        import numpy as np
+        torch = rt.torch
+        nseg, nb = sum(shapes), len(shapes)
+        if rt.stub:
+            pitch = S
+        else:
+            import bfrs
+            pitch = bfrs.shard_pitch(S) if pitch < 0 else max(pitch, S)
+        n_rows = {"data": nseg, "parity": 3 * nb, "restored": 3 * nb}
+        sets, row0 = {}, 0
+        if layout == "single":
+            whole = torch.empty(sum(n_rows.values()) * pitch, dtype=torch.uint8, device=rt.device)
+        for name, n in n_rows.items():
+            if layout == "single":
+                sets[name] = whole[row0 * pitch:].as_strided((n, S), (pitch, 1))
+                row0 += n
+            else:
+                buf = torch.empty(n * pitch, dtype=torch.uint8, device=rt.device)
+                sets[name] = buf.as_strided((n, S), (pitch, 1))
+        self.shapes, self.S, self.pitch = shapes, S, pitch
+        self.data, self.parity, self.restored = sets["data"], sets["parity"], sets["restored"]
+        self.enc_in = [self.data[s] for s in range(nseg)]
+        self.enc_out = [self.parity[i] for i in range(3 * nb)]
+        self.dec_in, self.dec_out, self.erased = [], [], []
+        seg = 0
+        for b, k in enumerate(shapes):
+            er = sorted(np.random.default_rng(0xDEC0DE + b).choice(k, min(3, k), replace=False).tolist())
+            self.erased.append(er)
+            for i in range(k):
+                self.dec_in.append(None if i in er else self.data[seg + i])
+                self.dec_out.append(self.restored[3 * b + er.index(i)] if i in er else None)
+            seg += k
+
+    def check_restored(self):
+        seg = 0
+        for b, k in enumerate(self.shapes):
+            for t, i in enumerate(self.erased[b]):
+                assert self.torch_equal(self.restored[3 * b + t], self.data[seg + i]), "decode mismatch"
+            seg += k
+
+    @staticmethod
+    def torch_equal(a, b):
+        import torch
+        return torch.equal(a, b)
+
+
+def codec_calls(rt, ctx, sets):
+    """(encode(stream), decode(stream)) for the batch; stub: a stand-in that
+    only touches the same buffers (launcher tests on CPU, never measured)."""
+    if rt.stub:
+        def enc(_h=None):
+            off = 0
+            for b, k in enumerate(sets.shapes):
+                x = sets.data[off:off + k].sum(dim=0, dtype=rt.torch.uint8)
+                for j in range(3):
+                    sets.parity[3 * b + j].copy_(x + j)
+                off += k
+
+        def dec(_h=None):
+            off = 0
+            for b, k in enumerate(sets.shapes):
+                for t, i in enumerate(sets.erased[b]):
+                    sets.restored[3 * b + t].copy_(sets.data[off + i])
+                off += k
+        return enc, dec
+    enc = ctx.prepare_encode(sets.shapes, 3, sets.S, sets.enc_in, sets.enc_out)
+    dec = ctx.prepare_decode(sets.shapes, 3, sets.S, sets.dec_in, sets.enc_out, sets.dec_out)
+    return enc, dec
+
+
+def fill(rt, sets, seed, lo_b=0, S_full=None):
+    """Synthetic splitmix64 bytes; with a stripe [lo_b, lo_b + S) of S_full-byte segments."""
+    from bfrs import synth
+    torch = rt.torch
+    if S_full is None or S_full == sets.S:
+        for s in range(sets.data.shape[0]):
+            synth.fill_segment_torch(sets.data[s], seed, s)
+        return
+    row = torch.empty(S_full + 8, dtype=torch.uint8, device=rt.device)
+    n8 = (S_full + 7) // 8 * 8
+    for s in range(sets.data.shape[0]):
+        synth.fill_segment_torch(row[:n8], seed, s)
+        sets.data[s].copy_(row[lo_b:lo_b + sets.S])
+
+
+def run_c4_strong(rt, ctx, args, stream_handle):
+    """BASELINE configs[3]: one 320-segment job, rank g owns the 64-B-aligned
+    column stripe g of every shard.  Encode and 3-erasure decode
+    timed separately; GiB/s of the WHOLE job's original data."""
+    from bfrs import parallel, synth
+    S_full = args.segment_bytes
+    shapes = synth.block_shapes(args.c4_segments)
+    lo_b, hi_b = parallel.stripe_ranges(S_full, rt.world)[rt.rank]
+    sets = ShardSets(rt, shapes, hi_b - lo_b, args.layout, -1)
+    fill(rt, sets, 0xB10C, lo_b, S_full)
+    enc, dec = codec_calls(rt, ctx, sets)
+    steps = max(3, args.steps // 2)
+    settle(rt, lambda: enc(stream_handle), min(args.settle_ms, 300.0))
+    _, t_enc = timed(rt, lambda: enc(stream_handle), steps)
+    settle(rt, lambda: dec(stream_handle), min(args.settle_ms, 300.0))
+    _, t_dec = timed(rt, lambda: dec(stream_handle), steps)
+    rt.sync()
+    sets.check_restored()
+    if args.dump_dir:
+        import numpy as np
+        os.makedirs(args.dump_dir, exist_ok=True)
+        np.save(os.path.join(args.dump_dir, f"c4_parity_rank{rt.rank}.npy"),
+                sets.parity.cpu().numpy())
+        with open(os.path.join(args.dump_dir, f"c4_stripe_rank{rt.rank}.json"), "w") as f:
+            json.dump({"lo": lo_b, "hi": hi_b, "shapes": shapes, "segment_bytes": S_full}, f)
+    job = sum(shapes) * S_full
+    out = {
+        "workload": "configs[3]: 320 x 32 MiB = 10xRS(30,3)+1xRS(20,3), 64-B column stripes over "
+                    f"{rt.world} GPU(s)",
+        "scaling": "strong", "blocks": shapes, "stripe_bytes_per_gpu": hi_b - lo_b,
+        "steps": steps,
+        "encode_GiBps": round(job * steps / 2**30 / t_enc, 2),
+        "decode_GiBps": round(job * steps / 2**30 / t_dec, 2),
+        "value": round(2 * job * steps / 2**30 / (t_enc + t_dec), 2),
+        "unit": "GiB/s",
+        "ms_per_encode": round(t_enc / steps * 1e3, 4), "ms_per_decode": round(t_dec / steps * 1e3, 4),
+    }
+    del sets
+    return out
+
+
+# ---------------------------------------------------------------- host side
+def host_info():
+    """CPU model and the core counts this host offers (nproc shows the whole
+    machine on the GPU boxes; the affinity mask and the cgroup quota show
+    this job's share)."""
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = float(q) / float(p)
+    except (OSError, ValueError):
+        pass
+    aff = len(os.sched_getaffinity(0))
+    share = aff
+    if quota:
+        share = min(share, max(1, int(quota)))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit():
+        share = min(share, int(omp))
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": aff,
+            "cgroup_cpu_quota": quota, "omp_num_threads": omp, "cpu_share": share}
+
+
+def cpu_baseline(args, sets, info):
+    """The oracle's AVX2 nibble-table engine (the crate's Avx2 technique) on
+    host cores, on C2's exact blocks (4 x RS(30,3) + 1 x RS(8,3) of 32 MiB,
+    copied from the GPU), encode then the same 3-erasure decodes:
+      striped       all cores, 64-B column stripes of every shard (value)
+      rayon_blocks  one block per thread, as rayon's into_par_iter over blocks
+                    (src/chunker/commit.rs:391-393): at most 5-way parallel
+      rayon_blocks_wrapper_copies  + the reference wrappers' copies: the pad
+                    to_vec of every segment and the to_vec of every output
+                    (src/chunker/generate.rs:75-82,95-96; recovery.rs:167-169)
+      single_core   one RS(30,3) block on one thread
+    Restatement of reed-solomon-simd 3.1.0, not the crate."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
-    from bfrs import synth
-    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
     eng = oracle.ENGINE_AVX2 if oracle.lib().oracle_have_avx2() else oracle.ENGINE_SCALAR
-    n = args.cpu_shard_bytes
-    ks = [30] * threads
-    data = [[synth.segment_np(0xC0, b * 30 + i, n) for i in range(30)] for b in range(threads)]
-    par = [[np.empty(n, np.uint8) for _ in range(3)] for _ in range(threads)]
-    t0 = time.perf_counter()
-    oracle.batch(eng, False, threads, ks, 3, n, data, [[None] * 3] * threads, par)
-    t_enc = time.perf_counter() - t0
-    orig = [[None if i in (1, 12, 25) else blk[i] for i in range(30)] for blk in data]
-    out = [[np.empty(n, np.uint8) if i in (1, 12, 25) else None for i in range(30)]
-           for _ in range(threads)]
-    t0 = time.perf_counter()
-    oracle.batch(eng, True, threads, ks, 3, n, orig, par, out)
-    t_dec = time.perf_counter() - t0
-    assert np.array_equal(out[0][12], data[0][12])
-    gib = threads * 30 * n / 2**30
-    # single core, one RS(30,3) block of 2 MiB shards (SURVEY 8(d): also report 1 core)
-    n1 = 2 << 20
-    d1 = [[synth.segment_np(0xC1, i, n1) for i in range(30)]]
-    p1 = [[np.empty(n1, np.uint8) for _ in range(3)]]
-    t0 = time.perf_counter()
-    oracle.batch(eng, False, 1, [30], 3, n1, d1, [[None] * 3], p1)
-    t1_enc = time.perf_counter() - t0
-    o1 = [[None if i in (1, 12, 25) else d1[0][i] for i in range(30)]]
-    r1 = [[np.empty(n1, np.uint8) if i in (1, 12, 25) else None for i in range(30)]]
-    t0 = time.perf_counter()
-    oracle.batch(eng, True, 1, [30], 3, n1, o1, p1, r1)
-    t1_dec = time.perf_counter() - t0
-    assert np.array_equal(r1[0][25], d1[0][25])
-    gib1 = 30 * n1 / 2**30
+    shapes, S = sets.shapes, sets.S
+    host = sets.data.cpu().numpy()  # C2's exact bytes
+    nb = len(shapes)
+    blocks, off = [], 0
+    for k in shapes:
+        blocks.append([host[off + i] for i in range(k)])
+        off += k
+    par = [[np.empty(S, np.uint8) for _ in range(3)] for _ in range(nb)]
+    rest = [[np.empty(S, np.uint8) if i in sets.erased[b] else None for i in range(k)]
+            for b, k in enumerate(shapes)]
+    dec_in = [[None if i in sets.erased[b] else blocks[b][i] for i in range(k)]
+              for b, k in enumerate(shapes)]
+    data_gib = sum(shapes) * S / 2**30
+    threads = args.cpu_threads or info["cpu_share"]
+
+    def run(nthreads, ks, orig, rec, out, decode, copies=False):
+        t0 = time.perf_counter()
+        oracle.batch(eng, decode, nthreads, ks, 3, len(orig[0][0]) if orig[0][0] is not None
+                     else len(rec[0][0]), orig, rec, out, copies=copies)
+        return time.perf_counter() - t0
+
+    res = {}
+    # rayon over blocks (codec only, then + wrapper copies)
+    for name, copies in (("rayon_blocks", False), ("rayon_blocks_wrapper_copies", True)):
+        t_e = run(min(threads, nb), shapes, blocks, [[None] * 3] * nb, par, False, copies)
+        t_d = run(min(threads, nb), shapes, dec_in, par, rest, True, copies)
+        res[name] = {"threads": min(threads, nb), "encode_GiBps": round(data_gib / t_e, 3),
+                     "decode_GiBps": round(data_gib / t_d, 3),
+                     "value": round(2 * data_gib / (t_e + t_d), 3)}
+    for b, k in enumerate(shapes):
+        want = oracle.encode(blocks[b][:k], 3, eng) if b == nb - 1 else None
+        if want is not None:
+            assert all(np.array_equal(par[b][j], want[j]) for j in range(3)), "cpu parity check"
+        for i in sets.erased[b]:
+            assert np.array_equal(rest[b][i], blocks[b][i]), "cpu decode check"
+    # column stripes over all cores: 16 stripes per shard (64-B aligned)
+    nst = 16
+    sw = S // nst
+    ks, so, sr, sp, sd, sdo = [], [], [], [], [], []
+    for b, k in enumerate(shapes):
+        for t in range(nst):
+            sl = slice(t * sw, (t + 1) * sw)
+            ks.append(k)
+            so.append([blocks[b][i][sl] for i in range(k)])
+            sp.append([par[b][j][sl] for j in range(3)])
+            sd.append([None if x is None else x[sl] for x in dec_in[b]])
+            sdo.append([None if x is None else x[sl] for x in rest[b]])
+    t_e = run(threads, ks, so, [[None] * 3] * len(ks), sp, False)
+    t_d = run(threads, ks, sd, sp, sdo, True)
+    res["striped"] = {"threads": threads, "stripes_per_shard": nst,
+                      "encode_GiBps": round(data_gib / t_e, 3), "decode_GiBps": round(data_gib / t_d, 3),
+                      "value": round(2 * data_gib / (t_e + t_d), 3)}
+    # one core, one RS(30,3) block
+    b0 = [blocks[0]]
+    p0 = [[np.empty(S, np.uint8) for _ in range(3)]]
+    t_e = run(1, [shapes[0]], b0, [[None] * 3], p0, False)
+    t_d = run(1, [shapes[0]], [dec_in[0]], p0, [rest[0]], True)
+    g1 = shapes[0] * S / 2**30
+    res["single_core"] = {"threads": 1, "encode_GiBps": round(g1 / t_e, 3), "decode_GiBps": round(g1 / t_d, 3),
+                          "value": round(2 * g1 / (t_e + t_d), 3),
+                          "sample": f"block 0 of C2 (RS({shapes[0]},3), 32 MiB shards)"}
+    st = res["striped"]
     return {
-        "value": round(2 * gib / (t_enc + t_dec), 3),
-        "unit": "GiB/s",
-        "cores": threads,
-        "kind": "port",
+        "value": st["value"], "unit": "GiB/s", "cores": threads, "kind": "port",
         "engine": "avx2" if eng == oracle.ENGINE_AVX2 else "scalar",
-        "encode_GiBps": round(gib / t_enc, 3),
-        "decode_GiBps": round(gib / t_dec, 3),
-        "single_core": {"value": round(2 * gib1 / (t1_enc + t1_dec), 3),
-                        "encode_GiBps": round(gib1 / t1_enc, 3),
-                        "decode_GiBps": round(gib1 / t1_dec, 3),
-                        "sample": "1 block x RS(30,3) x 2 MiB shards, 1 thread"},
-        "sample": f"{threads} blocks x RS(30,3) x {n // 2**20} MiB shards, one block per thread; "
-                  "encode + 3-erasure decode (restatement of reed-solomon-simd 3.1.0, not the crate)",
+        "encode_GiBps": st["encode_GiBps"], "decode_GiBps": st["decode_GiBps"],
+        "sample": f"C2's exact blocks ({'+'.join(map(str, shapes))} x 32 MiB), encode + the bench's "
+                  f"3-erasure decodes, 64-B column stripes over {threads} threads (restatement of "
+                  "reed-solomon-simd 3.1.0, not the crate)",
+        "host": info,
+        "variants": res,
     }
 
 
-def run_c5(args):
+def crate_api(ctx, sets, reps=3):
+    """The per-block host-memory path BlockFrame calls:
+    Chunker::generate_parity on one RS(30,3) block of 32 MiB segments
+    (src/chunker/generate.rs:59-104) and recover_segment_rs30_3 of one erased
+    segment (src/filestore/recovery.rs:118-173), pageable host buffers in and
+    out as the Rust Vecs are."""
+    import numpy as np
+    import bfrs
+    S, k = sets.S, sets.shapes[0]
+    segs = [sets.data[i].cpu().numpy() for i in range(k)]
+    ch = bfrs.Chunker(ctx)
+    t_gen = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        par = ch.generate_parity(segs, k, 3)
+        t_gen.append(time.perf_counter() - t0)
+    par = [np.frombuffer(p, np.uint8) for p in par]
+    target = sets.erased[0][0]
+    slots = [None if i == target else segs[i] for i in range(k)] + [None] * (30 - k)
+    t_rec = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        got = bfrs.recover_segment_rs30_3(ctx, slots, par, target)
+        t_rec.append(time.perf_counter() - t0)
+    assert np.array_equal(np.frombuffer(got, np.uint8), segs[target]), "crate_api recover mismatch"
+    gib = k * S / 2**30
+    tg, tr = min(t_gen), min(t_rec)
+    return {
+        "generate_parity": {"ms": round(tg * 1e3, 2), "GiBps": round(gib / tg, 2),
+                            "what": f"RS({k},3) block of {S >> 20} MiB segments, pageable host in/out"},
+        "recover_segment_rs30_3": {"ms": round(tr * 1e3, 2), "GiBps_of_block": round(gib / tr, 2),
+                                   "what": "one erased segment of that block, pageable host in/out"},
+        "reps": reps, "timing": "best of reps, wall clock",
+    }
+
+
+def pcie_inclusive(ctx, sets, steps=2):
+    """The reference path starts and ends in host memory: time the same batch
+    through bfrs_encode_host_batch / bfrs_decode_host_batch from pinned host
+    buffers (H2D + kernel + D2H pipelined over 3 streams).  Reported beside
+    `value`, never as `value`."""
+    import torch
+    shapes, S = sets.shapes, sets.S
+    nseg, nb = sum(shapes), len(shapes)
+    h_data = torch.empty(nseg, S, dtype=torch.uint8, pin_memory=True)
+    h_data.copy_(sets.data)
+    h_par = torch.empty(3 * nb, S, dtype=torch.uint8, pin_memory=True)
+    h_rest = torch.empty(3 * nb, S, dtype=torch.uint8, pin_memory=True)
+    enc_in = [h_data[s] for s in range(nseg)]
+    enc_out = [h_par[i] for i in range(3 * nb)]
+    dec_in_h, dec_out_h, seg = [], [], 0
+    for b, k in enumerate(shapes):
+        er = sets.erased[b]
+        for i in range(k):
+            dec_in_h.append(None if i in er else h_data[seg + i])
+            dec_out_h.append(h_rest[3 * b + er.index(i)] if i in er else None)
+        seg += k
+    ctx.encode_host_batch(shapes, 3, S, enc_in, enc_out)  # warm
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ctx.encode_host_batch(shapes, 3, S, enc_in, enc_out)
+    t_enc = (time.perf_counter() - t0) / steps
+    ctx.decode_host_batch(shapes, 3, S, dec_in_h, enc_out, dec_out_h)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ctx.decode_host_batch(shapes, 3, S, dec_in_h, enc_out, dec_out_h)
+    t_dec = (time.perf_counter() - t0) / steps
+    seg = 0
+    for b, k in enumerate(shapes):
+        for t, i in enumerate(sets.erased[b]):
+            assert torch.equal(h_rest[3 * b + t], h_data[seg + i]), "host-path decode mismatch"
+        seg += k
+    gib = nseg * S / 2**30
+    return {
+        "encode_GiBps": round(gib / t_enc, 2), "decode_GiBps": round(gib / t_dec, 2),
+        "encode_ms": round(t_enc * 1e3, 2), "decode_ms": round(t_dec * 1e3, 2),
+        "h2d_bytes_encode": nseg * S, "d2h_bytes_encode": 3 * nb * S,
+        "note": "pinned host buffers; bfrs_*_host_batch (8 MiB column slabs over 3 HIP streams)",
+    }
+
+
+def pmc_traffic(alg_bytes):
+    """HBM bytes per launch from the committed rocprofv3 PMC record of this
+    launch shape (FETCH_SIZE / WRITE_SIZE, separate passes), with its source."""
+    if not os.path.exists(PMC_FILE):
+        return None, None
+    try:
+        rec = json.load(open(PMC_FILE))
+    except (OSError, ValueError):
+        return None, None
+    if rec.get("algorithmic_read_bytes", 0) + rec.get("algorithmic_write_bytes", 0) != alg_bytes:
+        return None, None
+    src = {"file": os.path.relpath(PMC_FILE, ROOT), "round": rec.get("round"),
+           "kernel": rec.get("kernel"), "how": rec.get("source"),
+           "ratio_to_algorithmic": rec.get("ratio_to_algorithmic")}
+    return rec.get("hbm_bytes_per_launch"), src
+
+
+# ---------------------------------------------------------------- c5
+def c5_make_file(path, nbytes, seed=5):
+    """Synthetic file bytes (splitmix64 on the GPU, 256 MiB pieces)."""
+    import torch
+    from bfrs import synth
+    piece = 256 << 20
+    buf = torch.empty(piece + 8, dtype=torch.uint8, device="cuda")
+    with open(path, "wb") as f:
+        left, i = nbytes, 0
+        while left:
+            c = min(left, piece)
+            c8 = (c + 7) // 8 * 8
+            synth.fill_segment_torch(buf[:c8], seed, i)
+            f.write(buf[:c].cpu().numpy().tobytes())
+            left -= c
+            i += 1
+    del buf
+
+
+def run_c5(args, ctx=None):
     """BASELINE configs[4]: FUSE read of a corrupted large file.  The mount's
     read() core (src/mount/filesystem_unix.rs:176-305) is bfrs_archive_read:
     offset -> segment, LRU cache, device BLAKE3 on every miss, RS(k,3) block
@@ -134,22 +577,18 @@ def run_c5(args):
     import tempfile
     import numpy as np
     import bfrs
-    ctx = bfrs.Context(0)
+    own = ctx is None
+    if own:
+        ctx = bfrs.Context(0)
     work = tempfile.mkdtemp(prefix="bfrs_c5_", dir=args.c5_dir)
     try:
         n = int(args.c5_gib * (1 << 30)) + 12345  # ragged tail segment
         src = os.path.join(work, "large.bin")
-        rng = np.random.default_rng(5)
-        with open(src, "wb") as f:
-            left = n
-            while left:
-                c = min(left, 256 << 20)
-                f.write(rng.integers(0, 256, size=c, dtype=np.uint8).tobytes())
-                left -= c
+        c5_make_file(src, n)
         t0 = time.perf_counter()
-        adir = bfrs.commit(ctx, src, os.path.join(work, "archive"),
-                           segment_size=args.segment_bytes)
+        adir = bfrs.commit(ctx, src, os.path.join(work, "archive"), segment_size=args.segment_bytes)
         commit_s = time.perf_counter() - t0
+        os.unlink(src)
         m = json.load(open(os.path.join(adir, "manifest.json")))
         want = m["original_hash"]
 
@@ -184,28 +623,24 @@ def run_c5(args):
         dirty_s, dirty_st, out = sweep()
         ok = clean_ok and bfrs.blake3_hex(out, threads=16) == want
         del out
-        line = {
+        res = {
             "metric": "MB/s end-to-end read of a corrupted tier-3 file (BASELINE configs[4])",
-            "value": round(n / dirty_s / 1e6, 1), "unit": "MB/s", "n_gpus": 1,
-            "higher_is_better": True, "vs_baseline": None, "dtype": "u8",
-            "data": "synthetic random bytes; files in the page cache",
-            "config": {"workload": "configs[4]: 4 GiB tier-3 archive, 3 bit-flipped segments per "
-                                   "block, sequential 128 KiB reads through bfrs_archive_read",
-                       "bytes": n, "segment_bytes": args.segment_bytes,
-                       "read_bytes": args.c5_read_bytes, "blocks": len(m["merkle_tree"]["blocks"]),
-                       "damaged_segments": len(damaged)},
+            "value": round(n / dirty_s / 1e6, 1), "unit": "MB/s",
+            "workload": "configs[4]: 4 GiB tier-3 archive, 3 bit-flipped segments per block, "
+                        "sequential 128 KiB reads through bfrs_archive_read; files in the page cache",
+            "bytes": n, "segment_bytes": args.segment_bytes, "read_bytes": args.c5_read_bytes,
+            "blocks": len(m["merkle_tree"]["blocks"]), "damaged_segments": len(damaged),
             "clean_read_MBps": round(n / clean_s / 1e6, 1),
             "commit_MBps": round(n / commit_s / 1e6, 1),
             "stats_corrupted": dirty_st, "stats_clean": clean_st, "blake3_match": ok,
         }
         if args.cpu_baseline == "auto":
-            line["cpu_baseline"] = c5_cpu_baseline(adir, m, damaged, n)
-        print(json.dumps(line), flush=True)
-        if not ok:
-            sys.exit(1)
+            res["cpu_baseline"] = c5_cpu_baseline(adir, m, damaged, n)
+        return res
     finally:
         shutil.rmtree(work, ignore_errors=True)
-        ctx.close()
+        if own:
+            ctx.close()
 
 
 def c5_cpu_baseline(adir, m, damaged, nbytes):
@@ -236,7 +671,6 @@ def c5_cpu_baseline(adir, m, damaged, nbytes):
     t0 = time.perf_counter()
     d = read(seg_path(target))
     assert oracle.blake3_hex(d) != blk["segments"][target]
-    shard = S
     segs = []
     for s in range(len(blk["segments"])):
         if s == target:
@@ -244,8 +678,8 @@ def c5_cpu_baseline(adir, m, damaged, nbytes):
             continue
         x = read(seg_path(s))
         good = oracle.blake3_hex(x) == blk["segments"][s]
-        if good and x.size < shard:
-            x = np.concatenate([x, np.zeros(shard - x.size, np.uint8)])
+        if good and x.size < S:
+            x = np.concatenate([x, np.zeros(S - x.size, np.uint8)])
         segs.append(x if good else None)
     par = []
     for p in range(3):
@@ -266,219 +700,126 @@ def c5_cpu_baseline(adir, m, damaged, nbytes):
     }
 
 
-def pcie_inclusive(ctx, data, shapes, S, dec_in, erased, steps=2):
-    """The reference path starts and ends in host memory: time the same batch
-    through bfrs_encode_host_batch / bfrs_decode_host_batch from pinned host
-    buffers (H2D + kernel + D2H pipelined over 3 streams).  Reported beside
-    `value`, never as `value`."""
-    import torch
-    nseg = data.shape[0]
-    nb = len(shapes)
-    h_data = torch.empty(nseg, S, dtype=torch.uint8, pin_memory=True)
-    h_data.copy_(data)
-    h_par = torch.empty(3 * nb, S, dtype=torch.uint8, pin_memory=True)
-    h_rest = torch.empty(3 * nb, S, dtype=torch.uint8, pin_memory=True)
-    enc_in = [h_data[s] for s in range(nseg)]
-    enc_out = [h_par[i] for i in range(3 * nb)]
-    dec_in_h, dec_out_h, seg = [], [], 0
-    for b, k in enumerate(shapes):
-        for i in range(k):
-            dec_in_h.append(None if i in erased[b] else h_data[seg + i])
-            dec_out_h.append(h_rest[3 * b + erased[b].index(i)] if i in erased[b] else None)
-        seg += k
-    ctx.encode_host_batch(shapes, 3, S, enc_in, enc_out)  # warm
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        ctx.encode_host_batch(shapes, 3, S, enc_in, enc_out)
-    t_enc = (time.perf_counter() - t0) / steps
-    ctx.decode_host_batch(shapes, 3, S, dec_in_h, enc_out, dec_out_h)
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        ctx.decode_host_batch(shapes, 3, S, dec_in_h, enc_out, dec_out_h)
-    t_dec = (time.perf_counter() - t0) / steps
-    seg = 0
-    for b, k in enumerate(shapes):
-        for t, i in enumerate(erased[b]):
-            assert torch.equal(h_rest[3 * b + t], h_data[seg + i]), "host-path decode mismatch"
-        seg += k
-    gib = sum(shapes) * S / 2**30
-    return {
-        "encode_GiBps": round(gib / t_enc, 2), "decode_GiBps": round(gib / t_dec, 2),
-        "encode_ms": round(t_enc * 1e3, 2), "decode_ms": round(t_dec * 1e3, 2),
-        "h2d_bytes_encode": sum(shapes) * S, "d2h_bytes_encode": 3 * nb * S,
-        "note": "pinned host buffers; bfrs_*_host_batch (8 MiB column slabs over 3 HIP streams)",
-    }
-
-
+# ---------------------------------------------------------------- main
 def main():
     args = parse()
     if args.workload == "c5":
-        return run_c5(args)
-    import numpy as np
-    import torch
-    import bfrs
+        line = run_c5(args)
+        line.update({"n_gpus": 1, "higher_is_better": True, "vs_baseline": None, "dtype": "u8",
+                     "data": "synthetic splitmix64 bytes; files in the page cache"})
+        print(json.dumps(line), flush=True)
+        return 0 if line["blake3_match"] else 1
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(args)
     from bfrs import parallel, synth
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dist = None
-    if world > 1 or "TORCHELASTIC_RUN_ID" in os.environ:  # under torchrun: RCCL even at N=1
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-
+    rt = Runtime(args)
+    torch = rt.torch
     S_full = args.segment_bytes
-    nseg = args.segments
-    shapes = synth.block_shapes(nseg)
-    nb = len(shapes)
-    if args.strong:
-        # C4: every rank owns a 64-byte-aligned column stripe of every shard
-        lo_b, hi_b = parallel.stripe_ranges(S_full, world)[rank]
+    shapes = synth.block_shapes(args.segments)
+    if args.strong:  # value = C4: this rank's 64-B column stripe of every shard
+        lo_b, hi_b = parallel.stripe_ranges(S_full, rt.world)[rt.rank]
         S, seed = hi_b - lo_b, 0xB10C
     else:
-        lo_b, S, seed = 0, S_full, 0xB10C + rank
+        lo_b, S, seed = 0, S_full, 0xB10C + rt.rank
+    sets = ShardSets(rt, shapes, S, args.layout, args.pitch)
+    fill(rt, sets, seed, lo_b, S_full)
 
-    # ---- resident workload (this rank's bytes of every segment)
-    # every shard set is one allocation with rows bfrs_shard_pitch(S) apart
-    # Shard rows pitch = bfrs_shard_pitch(S) apart.  --layout single: data,
-    # parity and restored rows in one allocation (as the archive pipeline's
-    # arenas hold a block's k + 3 slots); separate: one allocation per set.
-    pitch = bfrs.shard_pitch(S) if args.pitch < 0 else max(args.pitch, S)
-    n_rows = {"data": nseg, "parity": 3 * nb, "restored": 3 * nb}
-    if args.layout == "single":
-        whole = torch.empty(sum(n_rows.values()) * pitch, dtype=torch.uint8, device="cuda")
-    sets, row0 = {}, 0
-    for name, n in n_rows.items():
-        if args.layout == "single":
-            sets[name] = whole[row0 * pitch:].as_strided((n, S), (pitch, 1))
-            row0 += n
-        else:
-            buf = torch.empty(n * pitch, dtype=torch.uint8, device="cuda")
-            sets[name] = buf.as_strided((n, S), (pitch, 1))
-    data = sets["data"]
-    if args.strong:
-        row = torch.empty(S_full, dtype=torch.uint8, device="cuda")
-        for s in range(nseg):
-            synth.fill_segment_torch(row, seed, s)
-            data[s].copy_(row[lo_b:lo_b + S])
-        del row
+    ctx = None
+    if not rt.stub:
+        import bfrs
+        ctx = bfrs.Context(rt.device.index)
+        stream = torch.cuda.current_stream()
+        sh = stream.cuda_stream
     else:
-        for s in range(nseg):
-            synth.fill_segment_torch(data[s], seed, s)
-    parity, restored = sets["parity"], sets["restored"]
-    enc_in = [data[s] for s in range(nseg)]
-    enc_out = [parity[i] for i in range(3 * nb)]
-    dec_in, dec_out, seg = [], [], 0
-    erased = []
-    for b, k in enumerate(shapes):
-        er = sorted(np.random.default_rng(0xDEC0DE + b).choice(k, 3, replace=False).tolist())
-        erased.append(er)
-        for i in range(k):
-            dec_in.append(None if i in er else data[seg + i])
-            dec_out.append(restored[3 * b + er.index(i)] if i in er else None)
-        seg += k
-
-    ctx = bfrs.Context(local)
-    stream = torch.cuda.current_stream()
-    sh = stream.cuda_stream
-    encode = ctx.prepare_encode(shapes, 3, S, enc_in, enc_out)
-    decode = ctx.prepare_decode(shapes, 3, S, dec_in, enc_out, dec_out)
+        sh = None
+    encode, decode = codec_calls(rt, ctx, sets)
 
     def step():
         encode(sh)
         decode(sh)
 
-    settle_steps = 0
-    t_settle = time.perf_counter()
-    while (time.perf_counter() - t_settle) * 1e3 < args.settle_ms:
-        step()
-        settle_steps += 1
-        if settle_steps % 16 == 0:
-            torch.cuda.synchronize()
+    settle_steps = settle(rt, step, args.settle_ms)
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
+    rt.sync()
     # (the correctness guard runs after the timed region: host work here would
     # idle the GPU and the timed region would start on ramping clocks again)
 
     # Timed region: K steps between a barrier + synchronize on both sides.
     # HIP events on the launch stream bracket the same region: every launch
     # in it is gf_apply (2 per step), so their mean duration = span / 2K.
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
+    if not rt.stub:
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    rt.barrier()
+    rt.sync()
     t0 = time.perf_counter()
-    ev0.record(stream)
-    for i in range(args.steps):
+    if not rt.stub:
+        ev0.record(stream)
+    for _ in range(args.steps):
         step()
-    ev1.record(stream)
-    torch.cuda.synchronize()
+    if not rt.stub:
+        ev1.record(stream)
+    rt.sync()
     elapsed = time.perf_counter() - t0  # this rank's K steps; the job time is the max over ranks
-    if dist:
-        dist.barrier()
-    launch_ms = ev0.elapsed_time(ev1) / (2 * args.steps)
-    elapsed = parallel.max_over_ranks(elapsed, dist, device="cuda")
+    rt.barrier()
+    launch_ms = ev0.elapsed_time(ev1) / (2 * args.steps) if not rt.stub else None
+    elapsed = rt.max_over_ranks(elapsed)
 
-    # Per-direction rates: short back-to-back loops after the timed region.
-    def per_launch(fn, n=max(3, args.steps // 2)):
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record(stream)
-        for _ in range(n):
-            fn(sh)
-        b.record(stream)
-        torch.cuda.synchronize()
-        return a.elapsed_time(b) / n
-    enc_ms, dec_ms = per_launch(encode), per_launch(decode)
-    # reference point on this box: a plain device copy (torch copy_) moving the
-    # same read + write bytes as one gf_apply launch (SURVEY 8(d) "achievable")
-    alg_bytes_launch = sum(k + 3 for k in shapes) * S
-    cp_src = torch.empty(alg_bytes_launch // 2, dtype=torch.uint8, device="cuda")
-    cp_dst = torch.empty_like(cp_src)
-    copy_ms = per_launch(lambda _h: cp_dst.copy_(cp_src))
-    del cp_src, cp_dst
-    # correctness guard on the measured buffers (compare on device)
-    seg = 0
-    for b, k in enumerate(shapes):
-        for t, i in enumerate(erased[b]):
-            assert torch.equal(restored[3 * b + t], data[seg + i]), "decode mismatch"
-        seg += k
+    enc_ms = dec_ms = copy_ms = None
+    if not rt.stub:
+        # Per-direction rates: short back-to-back loops after the timed region.
+        def per_launch(fn, n=max(3, args.steps // 2)):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            for _ in range(n):
+                fn(sh)
+            b.record(stream)
+            torch.cuda.synchronize()
+            return a.elapsed_time(b) / n
+        enc_ms, dec_ms = per_launch(encode), per_launch(decode)
+        # reference point on this box: a plain device copy (torch copy_) moving the
+        # same read + write bytes as one gf_apply launch (SURVEY 8(d) "achievable")
+        alg_bytes_launch = sum(k + 3 for k in shapes) * S
+        cp_src = torch.empty(alg_bytes_launch // 2, dtype=torch.uint8, device=rt.device)
+        cp_dst = torch.empty_like(cp_src)
+        copy_ms = per_launch(lambda _h: cp_dst.copy_(cp_src))
+        del cp_src, cp_dst
+    rt.sync()
+    sets.check_restored()  # correctness guard on the measured buffers (on device)
     data_bytes = sum(shapes) * S                     # original data per direction (this rank)
     alg_bytes = sum(k + 3 for k in shapes) * S        # HBM bytes per launch (both directions)
     scaling = "strong" if args.strong else "weak"
     job_bytes_step = 2 * sum(shapes) * (S_full if args.strong else S)
-    value = parallel.throughput(job_bytes_step, world, args.steps, elapsed, scaling)
+    value = parallel.throughput(job_bytes_step, rt.world, args.steps, elapsed, scaling)
 
-    if rank != 0:
-        if dist:
-            dist.destroy_process_group()
-        return
+    c4 = None
+    if args.c4 == "auto" and not args.strong:
+        c4 = run_c4_strong(rt, ctx, args, sh)
 
-    pcie = None
-    if world == 1 and args.pcie == "auto" and not args.strong:
-        pcie = pcie_inclusive(ctx, data, shapes, S, dec_in, erased)
+    if rt.rank != 0:
+        rt.close()
+        return 0
 
-    achieved = alg_bytes / (launch_ms * 1e-3) / 1e9
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc):
-        try:
-            rec = json.load(open(pmc))
-            # only when the profiled launch is this launch shape
-            if rec.get("algorithmic_read_bytes", 0) + rec.get("algorithmic_write_bytes", 0) == alg_bytes:
-                traffic = rec.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
-    cpu = None
-    if world == 1 and args.cpu_baseline == "auto":
-        cpu = cpu_baseline(args)
+    n1 = rt.world == 1
+    info = host_info()
+    pcie = crate = cpu = c5 = None
+    if n1 and args.pcie == "auto" and not args.strong:
+        pcie = pcie_inclusive(ctx, sets)
+    if n1 and args.crate == "auto" and not args.strong:
+        crate = crate_api(ctx, sets)
+    if n1 and args.cpu_baseline == "auto" and not args.strong:
+        cpu = cpu_baseline(args, sets, info)
+    del sets
+    if n1 and args.c5 == "auto" and not args.strong:
+        c5 = run_c5(args, ctx)
 
     line = {
         "metric": METRIC,
         "value": round(value, 2),
         "unit": "GiB/s",
-        "n_gpus": world,
+        "n_gpus": rt.world,
+        "world_size_observed": rt.observed_world(),
         "steps": args.steps,
         "warmup": args.warmup,
         "settle": {"ms": args.settle_ms, "steps": settle_steps,
@@ -488,39 +829,58 @@ def main():
         "scaling": scaling,
         "vs_baseline": None,
         "dtype": "u8",
-        "data": f"synthetic splitmix64 bytes (seed 0xB10C+rank), resident in HBM",
+        "data": ("STUB (CPU rehearsal of the launcher, not a measurement)" if rt.stub else
+                 "synthetic splitmix64 bytes (seed 0xB10C+rank), resident in HBM"),
         "config": {
             "workload": ("BASELINE configs[3]: 10 GiB archive, 320 x 32 MiB segments = "
                          "10xRS(30,3)+1xRS(20,3), column-striped over the GPUs"
                          if args.strong else
                          "BASELINE configs[1]+[2]: 128 x 32 MiB segments = 4xRS(30,3)+1xRS(8,3); "
                          "step = encode batch + 3-erasure decode of every block"),
-            "segments": nseg, "segment_bytes": S_full, "shard_pitch": int(data.stride(0)), "layout": args.layout, "blocks": shapes, "parity_shards": 3,
-            "parallelism": (f"64-B column stripes x{world}" if args.strong
-                            else f"independent batch per GPU x{world}"),
+            "segments": args.segments, "segment_bytes": S_full, "shard_pitch": int(sets_pitch(S, args, rt)),
+            "layout": args.layout, "blocks": shapes, "parity_shards": 3,
+            "parallelism": (f"64-B column stripes x{rt.world}" if args.strong
+                            else f"independent batch per GPU x{rt.world}"),
+            "kernel_variant": os.environ.get("BFRS_KERNEL_VARIANT", "default"),
         },
-        "encode_GiBps_per_gpu": round(data_bytes / 2**30 / (enc_ms * 1e-3), 2),
-        "decode_GiBps_per_gpu": round(data_bytes / 2**30 / (dec_ms * 1e-3), 2),
-        "roofline": {
-            "bound": "hbm", "kernel": "gf_apply_kernel",
+    }
+    if not rt.stub:
+        achieved = alg_bytes / (launch_ms * 1e-3) / 1e9
+        traffic, traffic_src = pmc_traffic(alg_bytes)
+        line["encode_GiBps_per_gpu"] = round(data_bytes / 2**30 / (enc_ms * 1e-3), 2)
+        line["decode_GiBps_per_gpu"] = round(data_bytes / 2**30 / (dec_ms * 1e-3), 2)
+        line["roofline"] = {
+            "bound": "hbm", "kernel": "gf_apply_ring_kernel",
             "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+            "traffic_source": traffic_src,
             "alg_bytes_per_launch": alg_bytes,
             "launch_ms": round(launch_ms, 4),
             "launch_ms_by_direction": {"encode": round(enc_ms, 4), "decode": round(dec_ms, 4)},
             "timing": "HIP events on the launch stream over the timed region / launches",
             "device_copy_reference": {
-                "GBps": round(alg_bytes_launch / (copy_ms * 1e-3) / 1e9, 1),
+                "GBps": round(alg_bytes / (copy_ms * 1e-3) / 1e9, 1),
                 "ms": round(copy_ms, 4),
                 "what": "torch copy_ of alg_bytes/2 bytes (same read + write bytes as one launch), same box"},
-        },
-        "cpu_baseline": cpu,
-        "pcie_inclusive": pcie,
-    }
+        }
+        line["cpu_baseline"] = cpu
+        line["crate_api"] = crate
+        line["pcie_inclusive"] = pcie
+        line["c5"] = c5
+    line["c4_strong"] = c4
     print(json.dumps(line), flush=True)
-    if dist:
-        dist.destroy_process_group()
+    rt.close()
+    if c5 is not None and not c5["blake3_match"]:
+        return 1
+    return 0
+
+
+def sets_pitch(S, args, rt):
+    if rt.stub:
+        return S
+    import bfrs
+    return bfrs.shard_pitch(S) if args.pitch < 0 else max(args.pitch, S)
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

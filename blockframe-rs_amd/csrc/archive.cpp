@@ -313,6 +313,19 @@ int Commit::tier3(std::string *out_dir) {
   const std::string dir = root + "/" + name + "_computing";
   const size_t nseg = (m.n + S - 1) / S;
   const size_t nblocks = (nseg + kBlockSegments - 1) / kBlockSegments;
+  // A block's shard size is its first segment's length (generate.rs:66-72);
+  // the crate rejects an odd one (ReedSolomonEncoder::new, generate.rs:84,
+  // called at commit.rs:440-441): a file whose last block is one odd-length
+  // segment fails here, before anything is written.
+  for (size_t b = 0; b < nblocks; ++b) {
+    const size_t shard = std::min(S, m.n - b * kBlockSegments * S);
+    if (shard & 1) {
+      std::ostringstream os;
+      os << "invalid shard size: " << shard << " bytes (block " << b
+         << "; must be non-zero and a multiple of 2)";
+      return set_error(BFRS_E_INVALID_SHARD_SIZE, os.str());
+    }
+  }
   for (size_t b = 0; b < nblocks; ++b)
     if (!mkdirs(dir + "/blocks/block_" + std::to_string(b) + "/segments") ||
         !mkdirs(dir + "/blocks/block_" + std::to_string(b) + "/parity"))
@@ -545,9 +558,10 @@ struct bfrs_archive {
   bfrs_archive_stats st{};
   static constexpr size_t kPrefetchDepth = 4, kPrefetchWorkers = 2;
   std::deque<size_t> wantq;               // queued, not started
-  std::unordered_set<size_t> inflight;    // being loaded by a prefetch worker
+  // segments being loaded (by a prefetch worker or a reader); everyone else
+  // waits on cv for them instead of loading them again
+  std::unordered_set<size_t> inflight;
   long long last_gi = -1;
-  long long reader_gi = -1;  // segment a reader is loading itself (prefetch skips it)
   bool stop = false;
   std::vector<std::thread> workers;
 
@@ -655,10 +669,11 @@ int bfrs_archive::recover(size_t gi, SegPtr *out) {
         if (!need) continue;
         uint8_t *buf = pool->get();
         if (!buf) return set_error(BFRS_E_NOMEM, "pinned segment buffer allocation failed");
+        // owned by a Seg before anything can fail, so every path returns it to the pool
+        restored.emplace_back(b * kBlockSegments + s, std::make_shared<Seg>(pool, buf, bs.lens[s]));
         std::memcpy(buf, arena.hs(s), bs.lens[s]);
         if (!was_ok[s] && write_back && !write_file(t3_seg(g.dir, b, s), buf, bs.lens[s]))
           return io_error("write back segment");
-        restored.emplace_back(b * kBlockSegments + s, std::make_shared<Seg>(pool, buf, bs.lens[s]));
       }
       std::lock_guard<std::mutex> l(mu);
       ++st.recoveries;
@@ -692,8 +707,9 @@ int bfrs_archive::recover(size_t gi, SegPtr *out) {
   if (write_back && !write_file(seg_path(gi), v.data(), v.size())) return io_error("write back segment");
   uint8_t *buf = pool->get();
   if (!buf) return set_error(BFRS_E_NOMEM, "pinned segment buffer allocation failed");
+  auto seg = std::make_shared<Seg>(pool, buf, v.size());
   std::memcpy(buf, v.data(), v.size());
-  *out = std::make_shared<Seg>(pool, buf, v.size());
+  *out = std::move(seg);
   std::lock_guard<std::mutex> l(mu);
   ++st.recoveries;
   ++st.recovered_segments;
@@ -707,7 +723,7 @@ void bfrs_archive::prefetch_loop() {
     if (stop) return;
     const size_t gi = wantq.front();
     wantq.pop_front();
-    if (cache.count(gi) || inflight.count(gi) || reader_gi == (long long)gi) continue;
+    if (cache.count(gi) || inflight.count(gi)) continue;
     inflight.insert(gi);
     l.unlock();
     SegPtr seg;
@@ -798,7 +814,12 @@ int bfrs_commit(bfrs_ctx *ctx, const char *file_path, const char *archive_root,
   if (tier == 0) tier = c.m.n <= kTier1Limit ? 1 : c.m.n <= kTier2Limit ? 2 : 3;
   std::string dir;
   int rc = tier == 1 ? c.tier1(&dir) : tier == 2 ? c.tier2(&dir) : c.tier3(&dir);
-  if (rc) return rc;
+  if (rc) {  // no half-written archive: drop this call's work directory
+    const std::string computing = c.root + "/" + c.name + "_computing";
+    struct stat cs;
+    if (tier != 1 && stat(computing.c_str(), &cs) == 0) (void)rmtree(computing);
+    return rc;
+  }
   if (out_dir && out_cap) {
     std::strncpy(out_dir, dir.c_str(), out_cap - 1);
     out_dir[out_cap - 1] = 0;
@@ -1037,20 +1058,21 @@ int bfrs_archive_read(bfrs_archive *a, uint64_t offset, size_t len, uint8_t *out
     SegPtr seg = a->lookup(gi);
     if (seg) {
       ++a->st.hits;
-    } else if (a->inflight.count(gi)) {  // a prefetch worker is loading it
+    } else if (a->inflight.count(gi)) {  // a prefetch worker or another reader is loading it
       a->cv.wait(l, [&] { return !a->inflight.count(gi); });
       continue;
     } else {
       ++a->st.misses;
       // queued but not started: load it here instead
       a->wantq.erase(std::remove(a->wantq.begin(), a->wantq.end(), gi), a->wantq.end());
-      a->reader_gi = (long long)gi;
+      a->inflight.insert(gi);
       l.unlock();
       bool ok = false;
       int rc = a->load_clean(gi, &seg, &ok);
       if (rc == BFRS_OK && !ok) rc = a->recover(gi, &seg);
       l.lock();
-      a->reader_gi = -1;
+      a->inflight.erase(gi);
+      a->cv.notify_all();
       if (rc) return rc;
       if (ok) ++a->st.verified;
       a->put(gi, seg);

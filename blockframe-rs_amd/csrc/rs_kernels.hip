@@ -265,6 +265,149 @@ __device__ __forceinline__ bool ring_acc_halfchunk(const KernArgs &args, const P
   return true;
 }
 
+// ---- contiguous-line layout (LAY 1, round 2) --------------------------------
+// Every load / store instruction covers 1 KiB of contiguous columns (16 whole
+// 64-byte chunks = 8 whole 128-B lines), so each HBM line is fetched by one
+// instruction: the half-chunk layout above touches every line with two
+// instructions (32 B of each chunk each), which costs 7% of the memory
+// system's rate in the traffic-only probes and doubles the fetch with `nt`
+// loads (tools/membench8.hip, profiles/r02/).  A wave covers 2 KiB = 32
+// chunks per input: load A = chunks 0..15, load B = chunks 16..31.  Lanes
+// 0-31 load the low halves (16 B each) of A's chunks, lanes 32-63 their high
+// halves; same for B.  One v_permlane32_swap per dword (A's lanes 32-63 <->
+// B's lanes 0-31) then gives every lane the low bytes (A) and high bytes (B)
+// of its own 16 symbols -- exactly the half-chunk register contents, so the
+// GF arithmetic (mac_input_v1) is unchanged.  Outputs are swapped back the
+// same way before their contiguous stores.
+template <int LPOL = 0>
+__device__ __forceinline__ void gload_ct(u32x4 &A, u32x4 &B, uint64_t base, uint32_t offA,
+                                         uint32_t offB) {
+  if constexpr (LPOL == 1)
+    asm volatile(
+        "global_load_dwordx4 %0, %2, %4 nt\n\t"
+        "global_load_dwordx4 %1, %3, %4 nt"
+        : "=&v"(A), "=&v"(B)
+        : "v"(offA), "v"(offB), "s"(base)
+        : "memory");
+  else
+    asm volatile(
+        "global_load_dwordx4 %0, %2, %4\n\t"
+        "global_load_dwordx4 %1, %3, %4"
+        : "=&v"(A), "=&v"(B)
+        : "v"(offA), "v"(offB), "s"(base)
+        : "memory");
+}
+
+// A's lanes 32-63 <-> B's lanes 0-31, dword by dword.
+__device__ __forceinline__ void halves_swap(u32x4 &A, u32x4 &B) {
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const auto r = __builtin_amdgcn_permlane32_swap(A[d], B[d], false, false);
+    A[d] = r[0];
+    B[d] = r[1];
+  }
+}
+
+// Lane offsets of the wave's two 1 KiB runs (chunk base wchunk0); a lane whose
+// chunk is past the last full chunk reads chunk 0's bytes instead (never
+// stored) so every lane takes part in the swaps.
+struct CtLane {
+  uint32_t offA, offB;
+  uint32_t fb;  // an offset inside the shard's first chunk
+  bool okA, okB;
+};
+__device__ __forceinline__ CtLane ct_lane(uint64_t wchunk0, uint64_t full_chunks) {
+  const uint32_t l = threadIdx.x & 63;
+  const uint32_t in_kib = ((l & 31) >> 1) * 64 + (l >> 5) * 32 + (l & 1) * 16;
+  const uint64_t cA = wchunk0 + ((l & 31) >> 1), cB = cA + 16;
+  CtLane r;
+  r.okA = cA < full_chunks;
+  r.okB = cB < full_chunks;
+  const uint32_t fallback = (l >> 5) * 32 + (l & 1) * 16;
+  r.fb = fallback;
+  r.offA = r.okA ? uint32_t(wchunk0 * 64) + in_kib : fallback;
+  r.offB = r.okB ? uint32_t(wchunk0 * 64) + 1024 + in_kib : fallback;
+  return r;
+}
+
+// TAIL 1: the ring's loads past the last input (issued only to keep the
+// vmcnt arithmetic constant, never consumed) read the last input's first
+// chunk -- one hot 64-B line -- instead of re-reading 2 KiB of its columns,
+// which with non-temporal loads costs real HBM traffic (2 of 30 inputs).
+template <int LPOL, int ROT = 0, bool PROBE = false, int TAIL = 0>
+__device__ __forceinline__ bool ring_acc_ct(const KernArgs &args, const PassDesc &P, uint32_t tile,
+                                            uint32_t wave_id, uint32_t (&acc_lo)[16],
+                                            uint32_t (&acc_hi)[16], CtLane &ln) {
+  const uint32_t n_in = P.n_in;
+  const uint64_t *in = args.ptrs + P.in;
+  const uint64_t wchunk0 = (uint64_t(tile) * 4 + wave_id) * 32;
+  if (wchunk0 >= P.full_chunks) return false;  // wave-uniform
+  ln = ct_lane(wchunk0, P.full_chunks);
+  const uint32_t offA = ln.offA, offB = ln.offB;
+#pragma unroll
+  for (int s = 0; s < 16; ++s) acc_lo[s] = acc_hi[s] = 0;
+  const uint32_t rot = !P.rotate || ROT == 2 ? 0
+                       : ROT == 1           ? (tile * 4) % n_in
+                       : ROT >= 3           ? ((tile >> (ROT - 2)) * 4) % n_in
+                                            : (tile * 4 + wave_id) % n_in;
+  auto idx = [&](uint32_t x) -> uint32_t {
+    if (x >= n_in) x = n_in - 1;
+    const uint32_t y = rot + x;
+    return y >= n_in ? y - n_in : y;
+  };
+  input_ring(
+      n_in,
+      [&](u32x4 &A, u32x4 &B, uint32_t x) {
+        // branch-free (a branch here made the compiler spill in-flight ring
+        // registers; tools/inflight_check.py): select the offsets only
+        const bool past = TAIL && x >= n_in;
+        gload_ct<LPOL>(A, B, in[idx(x)], past ? ln.fb : offA, past ? ln.fb : offB);
+      },
+      [&](const u32x4 &Av, const u32x4 &Bv, uint32_t x) {
+        const uint32_t r = idx(x);
+        u32x4 L = Av, H = Bv;
+        halves_swap(L, H);
+        if constexpr (PROBE)  // traffic-only probe (measurement, NOT a codec)
+          mac_input_stream(make_uint4(L.x, L.y, L.z, L.w), make_uint4(H.x, H.y, H.z, H.w), acc_lo,
+                           acc_hi);
+        else
+          mac_input_v1(make_uint4(L.x, L.y, L.z, L.w), make_uint4(H.x, H.y, H.z, H.w), 2 * r,
+                       2 * r + 1, acc_lo, acc_hi);
+      });
+  return true;
+}
+
+template <int LPOL, int SPOL, int ROT = 0, bool PROBE = false, int TAIL = 0>
+__device__ __forceinline__ void ring_tile_ct(const KernArgs &args, const PassDesc &P, uint32_t tile,
+                                             uint32_t wave_id) {
+  uint32_t acc_lo[16], acc_hi[16];
+  CtLane ln;
+  if (!ring_acc_ct<LPOL, ROT, PROBE, TAIL>(args, P, tile, wave_id, acc_lo, acc_hi, ln)) return;
+  const uint32_t n_out = P.n_out;
+  const uint64_t *outp = args.ptrs + P.out;
+  const bool accumulate = P.accumulate != 0;
+  for (uint32_t t = 0; t < n_out; ++t) {
+    u32x4 ol = {gather_byte(acc_lo, 0, t), gather_byte(acc_lo, 1, t), gather_byte(acc_lo, 2, t),
+                gather_byte(acc_lo, 3, t)};
+    u32x4 oh = {gather_byte(acc_hi, 0, t), gather_byte(acc_hi, 1, t), gather_byte(acc_hi, 2, t),
+                gather_byte(acc_hi, 3, t)};
+    halves_swap(ol, oh);  // back to the contiguous layout: ol -> run A, oh -> run B
+    const uint64_t dst = outp[t];
+    if (accumulate) {
+      if (ln.okA) {
+        const uint4 p = load16(dst + ln.offA);
+        ol ^= u32x4{p.x, p.y, p.z, p.w};
+      }
+      if (ln.okB) {
+        const uint4 p = load16(dst + ln.offB);
+        oh ^= u32x4{p.x, p.y, p.z, p.w};
+      }
+    }
+    if (ln.okA) store16_pol<SPOL>(dst + ln.offA, ol);
+    if (ln.okB) store16_pol<SPOL>(dst + ln.offB, oh);
+  }
+}
+
 template <int LPOL, int SPOL, int ROT = 0, bool PROBE = false>
 __device__ __forceinline__ void ring_tile_halfchunk(const KernArgs &args, const PassDesc &P,
                                                     uint32_t tile, uint32_t wave_id) {
@@ -304,15 +447,23 @@ __device__ __forceinline__ uint32_t xcd_group_remap(uint32_t b, uint32_t n) {
   return base + XG * (8u * (q / XG) + x) + q % XG;
 }
 
-template <int ROT, bool PROBE = false, uint32_t XG = 0>
+// LAY 0: half-chunk lanes (round 1); LAY 1: contiguous lines + lane-half
+// swaps (ring_acc_ct).  LPOL 1: non-temporal loads (only sound with LAY 1,
+// where every line is read by one instruction).
+template <int ROT, bool PROBE = false, uint32_t XG = 0, int LAY = 0, int LPOL = 0, int TAIL = 0>
 __global__ __launch_bounds__(256, 5) void gf_apply_ring_kernel(const KernArgs args) {
-  const uint32_t wg = XG ? xcd_group_remap<XG>(blockIdx.x, gridDim.x) : blockIdx.x;
+  uint32_t wg = blockIdx.x;
+  if constexpr (XG > 0) wg = xcd_group_remap<XG>(blockIdx.x, gridDim.x);
   const PassDesc &P = enter_pass(args, wg);
   const uint32_t t_begin = (wg - P.wg_begin) * args.tiles_per_wg;
   const uint32_t t_end = min(t_begin + args.tiles_per_wg, P.n_tiles);
   const uint32_t wave_id = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  for (uint32_t tile = t_begin; tile < t_end; ++tile)
-    ring_tile_halfchunk<0, 1, ROT, PROBE>(args, P, tile, wave_id);
+  for (uint32_t tile = t_begin; tile < t_end; ++tile) {
+    if constexpr (LAY == 1)
+      ring_tile_ct<LPOL, 1, ROT, PROBE, TAIL>(args, P, tile, wave_id);
+    else
+      ring_tile_halfchunk<0, 1, ROT, PROBE>(args, P, tile, wave_id);
+  }
 }
 
 // Tail chunk (shard_bytes % 64 = tb != 0): tb/2 symbols, low bytes at
@@ -361,7 +512,7 @@ __global__ __launch_bounds__(64) void gf_tail_kernel(const KernArgs args) {
 int kernel_variant() {
   const char *e = std::getenv("BFRS_KERNEL_VARIANT");
   int v = e ? atoi(e) : 58;
-  if (v == 44 && !std::getenv("BFRS_ALLOW_PROBE")) v = 58;
+  if ((v == 44 || v == 72 || v == 74) && !std::getenv("BFRS_ALLOW_PROBE")) v = 58;
   return v;
 }
 
@@ -392,6 +543,21 @@ hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in
       break;
     case 41:
       hipLaunchKernelGGL((gf_apply_ring_kernel<6>), dim3(n_wgs), dim3(256), lds, stream, args);
+      break;
+    case 70:  // 58 with contiguous-line loads/stores (LAY 1)
+      hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16, 1, 0>), dim3(n_wgs), dim3(256), lds, stream, args);
+      break;
+    case 71:  // 70 with non-temporal loads
+      hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
+      break;
+    case 72:  // traffic-only probe of 71
+      hipLaunchKernelGGL((gf_apply_ring_kernel<6, true, 16, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
+      break;
+    case 73:  // 71 with the ring's past-the-end loads on one hot line
+      hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16, 1, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
+      break;
+    case 74:  // traffic-only probe of 73
+      hipLaunchKernelGGL((gf_apply_ring_kernel<6, true, 16, 1, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
       break;
     default:  // 58: 41 with each read group's 16 workgroups on one XCD
       hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16>), dim3(n_wgs), dim3(256), lds, stream, args);

@@ -114,6 +114,7 @@ int Context::init(int dev) {
     return set_error(BFRS_E_NO_DEVICE, "no HIP device available (no CPU fallback)");
   if (dev < 0 || dev >= n) return set_error(BFRS_E_NO_DEVICE, "HIP device id out of range");
   device = dev;
+  if (const char *e = std::getenv("BFRS_PLAN_CACHE")) max_plans = std::max(1, atoi(e));
   HIP_TRY(hipSetDevice(dev));
   HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
   for (auto &ps : pipe_stream) HIP_TRY(hipStreamCreateWithFlags(&ps, hipStreamNonBlocking));
@@ -138,6 +139,7 @@ int Context::scratch(size_t bytes, void **out) {
 int Context::run_host(bool decode, size_t nblocks, const uint32_t *ks, size_t m,
                       size_t shard_bytes, const uint8_t *const *orig, const uint8_t *const *rec,
                       uint8_t *const *out) {
+  std::lock_guard<std::mutex> pipe_lock(pipe_mu);
   // Slab width: whole 64-byte chunks, ~8 MiB of columns per shard (env
   // BFRS_SLAB_BYTES overrides), the shard's tail chunk rides in the last slab.
   size_t slab = 8u << 20;
@@ -206,43 +208,74 @@ int Context::run_host(bool decode, size_t nblocks, const uint32_t *ks, size_t m,
   return BFRS_OK;
 }
 
-int Context::get_encode_plan(size_t k, size_t m, const Plan **out) {
-  std::ostringstream key;
-  key << "E" << k << "," << m;
-  std::lock_guard<std::mutex> g(mu);
-  auto it = plans.find(key.str());
-  if (it == plans.end()) {
-    auto p = std::make_unique<Plan>();
-    p->coef = plan_encode(k, m);
+namespace {
+// Cache lookup / insert under Context::mu.  When the cache is full, the
+// least recently used half of the plans nobody else holds is dropped, after a
+// device synchronize: a plan's tables may still be read by queued kernels of
+// an earlier call even when no BlockIO holds it any more.
+template <typename Make>
+int cached_plan(Context &c, const std::string &key, Make make, PlanRef *out) {
+  std::lock_guard<std::mutex> g(c.mu);
+  auto it = c.plans.find(key);
+  if (it == c.plans.end()) {
+    if (c.plans.size() >= c.max_plans) {
+      std::vector<std::pair<uint64_t, std::string>> idle;
+      for (auto &kv : c.plans)
+        if (kv.second.use_count() == 1) idle.emplace_back(kv.second->last_use, kv.first);
+      if (!idle.empty()) {
+        HIP_TRY(hipDeviceSynchronize());
+        std::sort(idle.begin(), idle.end());
+        const size_t drop = std::max<size_t>(1, idle.size() / 2);
+        for (size_t i = 0; i < drop; ++i) c.plans.erase(idle[i].second);
+      }
+    }
+    auto p = std::make_shared<Plan>();
+    p->coef = make();
     int rc = upload_plan(p.get());
     if (rc) return rc;
-    it = plans.emplace(key.str(), std::move(p)).first;
+    it = c.plans.emplace(key, std::move(p)).first;
   }
-  *out = it->second.get();
+  it->second->last_use = ++c.plan_tick;
+  *out = it->second;
   return BFRS_OK;
+}
+}  // namespace
+
+int Context::get_encode_plan(size_t k, size_t m, PlanRef *out) {
+  return cached_plan(*this, "E" + std::to_string(k) + "," + std::to_string(m),
+                     [&] { return plan_encode(k, m); }, out);
 }
 
 int Context::get_decode_plan(size_t k, size_t m, const std::vector<uint8_t> &orig_present,
-                             const std::vector<uint8_t> &rec_present, const Plan **out) {
+                             const std::vector<uint8_t> &rec_present, PlanRef *out) {
   std::string key = "D" + std::to_string(k) + "," + std::to_string(m) + ":";
   for (uint8_t b : orig_present) key.push_back(b ? '1' : '0');
   key.push_back('/');
   for (uint8_t b : rec_present) key.push_back(b ? '1' : '0');
-  std::lock_guard<std::mutex> g(mu);
-  auto it = plans.find(key);
-  if (it == plans.end()) {
-    if (plans.size() > 4096) plans.clear();  // bound the cache
-    auto p = std::make_unique<Plan>();
-    p->coef = plan_decode(k, m, orig_present, rec_present);
-    int rc = upload_plan(p.get());
+  return cached_plan(*this, key, [&] { return plan_decode(k, m, orig_present, rec_present); }, out);
+}
+
+int Context::run_blocks(const std::vector<BlockIO> &blocks, size_t shard_bytes, hipStream_t s) {
+  if (shard_bytes <= kMaxWindowBytes) return run_window(blocks, shard_bytes, s);
+  // column windows of kMaxWindowBytes (a multiple of 64: the crate's chunk
+  // layout is per 64-byte chunk, so a window is a valid shard of its own);
+  // the last window keeps the tail chunk
+  std::vector<BlockIO> w = blocks;
+  for (size_t off = 0; off < shard_bytes;) {
+    size_t len = std::min(kMaxWindowBytes, shard_bytes - off);
+    if (shard_bytes - (off + len) < 64) len = shard_bytes - off;
+    for (size_t b = 0; b < blocks.size(); ++b) {
+      for (size_t i = 0; i < blocks[b].in.size(); ++i) w[b].in[i] = blocks[b].in[i] + off;
+      for (size_t i = 0; i < blocks[b].out.size(); ++i) w[b].out[i] = blocks[b].out[i] + off;
+    }
+    int rc = run_window(w, len, s);
     if (rc) return rc;
-    it = plans.emplace(key, std::move(p)).first;
+    off += len;
   }
-  *out = it->second.get();
   return BFRS_OK;
 }
 
-int Context::run_blocks(const std::vector<BlockIO> &blocks, size_t shard_bytes,
+int Context::run_window(const std::vector<BlockIO> &blocks, size_t shard_bytes,
                         hipStream_t s) {
   const uint64_t full_chunks = shard_bytes / 64;
   const uint32_t tail = uint32_t(shard_bytes % 64);

@@ -69,12 +69,16 @@ struct Plan {
   std::vector<PlanPass> passes;
   uint32_t n_phases = 0;
   void *d_tables = nullptr;  // one allocation for all pass tables
+  uint64_t last_use = 0;     // plan-cache LRU tick (under Context::mu)
   ~Plan();
 };
+using PlanRef = std::shared_ptr<const Plan>;
 
-// One RS block in a batch: device addresses of its pass inputs/outputs.
+// One RS block in a batch: device addresses of its pass inputs/outputs.  The
+// plan reference keeps its device tables alive while the batch is queued
+// (the cache evicts only plans nobody holds, after a device synchronize).
 struct BlockIO {
-  const Plan *plan;
+  PlanRef plan;
   std::vector<const uint8_t *> in;  // plan.coef.cols device pointers
   std::vector<uint8_t *> out;       // plan.coef.rows device pointers
 };
@@ -83,14 +87,19 @@ struct Context {
   int device = 0;
   hipStream_t stream = nullptr;
   std::mutex mu;  // guards the plan cache (contexts are single-threaded otherwise)
-  std::map<std::string, std::unique_ptr<Plan>> plans;
+  std::map<std::string, std::shared_ptr<Plan>> plans;
+  uint64_t plan_tick = 0;
+  size_t max_plans = 4096;  // BFRS_PLAN_CACHE overrides at bfrs_open (tests)
 
   // Scratch device memory for the host-memory API.
   void *d_scratch = nullptr;
   size_t scratch_cap = 0;
 
   // Host-path pipeline: slots of device slab buffers, one stream each.
+  // pipe_mu serialises run_host: archive prefetch threads, repair and the
+  // owner's host-batch calls may share one context.
   static constexpr int kPipeSlots = 3;
+  std::mutex pipe_mu;
   hipStream_t pipe_stream[kPipeSlots] = {};
   void *pipe_buf = nullptr;
   size_t pipe_cap = 0;  // bytes per slot
@@ -118,11 +127,15 @@ struct Context {
   int blake3_dev(size_t n, const uint8_t *const *d_msgs, const size_t *lens,
                  const uint64_t *chunk_offsets, uint8_t *digests, uint8_t *cvs,
                  hipStream_t stream);
-  int get_encode_plan(size_t k, size_t m, const Plan **out);
+  int get_encode_plan(size_t k, size_t m, PlanRef *out);
   int get_decode_plan(size_t k, size_t m, const std::vector<uint8_t> &orig_present,
-                      const std::vector<uint8_t> &rec_present, const Plan **out);
-  // Queue the passes of all blocks (same shard_bytes) on `stream`.
+                      const std::vector<uint8_t> &rec_present, PlanRef *out);
+  // Queue the passes of all blocks (same shard_bytes) on `stream`.  Shards
+  // longer than kMaxWindowBytes run as column windows (the kernels address a
+  // shard with 32-bit lane offsets).
+  static constexpr size_t kMaxWindowBytes = size_t(1) << 31;
   int run_blocks(const std::vector<BlockIO> &blocks, size_t shard_bytes, hipStream_t stream);
+  int run_window(const std::vector<BlockIO> &blocks, size_t shard_bytes, hipStream_t stream);
   int scratch(size_t bytes, void **out);
   // Streams host-memory blocks through HBM (see bfrs_encode_host_batch).
   // orig/rec/out are per-block host pointer lists (decode: NULL = missing).

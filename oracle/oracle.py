@@ -40,6 +40,7 @@ def lib() -> ctypes.CDLL:
         L.oracle_batch.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint32,
                                    ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32,
                                    ctypes.c_size_t, P, P, P]
+        L.oracle_batch2.argtypes = L.oracle_batch.argtypes + [ctypes.c_int]
         L.oracle_use_high_rate.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
         L.oracle_supported.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
         for f in ("oracle_gf_exp", "oracle_gf_log"):
@@ -134,9 +135,10 @@ def merkle_root_hex(leaves) -> str:
     return buf.value.decode()
 
 
-def batch(engine, decode_, threads, ks, m, shard_bytes, orig, rec, out):
+def batch(engine, decode_, threads, ks, m, shard_bytes, orig, rec, out, copies=False):
     """Multi-threaded block-parallel driver (CPU baseline).  orig/rec/out are
-    per-block lists of numpy arrays (or None)."""
+    per-block lists of numpy arrays (or None).  copies: also make the
+    reference wrappers' input/output copies around every block."""
     nb = len(ks)
     keep = []
     def tbl(lists):
@@ -147,9 +149,10 @@ def batch(engine, decode_, threads, ks, m, shard_bytes, orig, rec, out):
             arr[b] = ctypes.cast(p, ctypes.c_void_p)
         return arr
     karr = (ctypes.c_uint32 * nb)(*ks)
-    rc = lib().oracle_batch(engine, int(decode_), threads, nb, karr, m, shard_bytes,
-                            ctypes.cast(tbl(orig), ctypes.POINTER(ctypes.c_void_p)),
-                            ctypes.cast(tbl(rec), ctypes.POINTER(ctypes.c_void_p)),
-                            ctypes.cast(tbl(out), ctypes.POINTER(ctypes.c_void_p)))
+    rc = lib().oracle_batch2(engine, int(decode_), threads, nb, karr, m, shard_bytes,
+                             ctypes.cast(tbl(orig), ctypes.POINTER(ctypes.c_void_p)),
+                             ctypes.cast(tbl(rec), ctypes.POINTER(ctypes.c_void_p)),
+                             ctypes.cast(tbl(out), ctypes.POINTER(ctypes.c_void_p)),
+                             int(copies))
     if rc != 0:
         raise ValueError(f"oracle_batch rc={rc}")

@@ -548,7 +548,46 @@ typedef struct {
   int next;
   int err;
   pthread_mutex_t mu;
+  int copies; /* 1: the reference wrappers' copies around every call (see oracle_batch2) */
 } batch_t;
+
+/* One block with the copies BlockFrame's wrappers make around the crate call:
+ * every input is copied first (generate.rs:75-82 pads each segment with
+ * to_vec; the decoder wrappers take owned Vecs), the codec writes into its own
+ * buffers, and the results are copied out (recovery_iter().to_vec(),
+ * generate.rs:95-96; restored_original(..).to_vec(), recovery.rs:167-169). */
+static int block_with_copies(const batch_t *b, uint32_t i) {
+  const uint32_t k = b->k[i], m = b->m, nout = b->decode ? k : m;
+  const size_t n = b->shard_bytes;
+  const uint8_t **in = (const uint8_t **)calloc(k + m, sizeof(void *));
+  uint8_t **out = (uint8_t **)calloc(nout, sizeof(void *));
+  int rc = 0;
+  for (uint32_t x = 0; x < k + m && !rc; ++x) {
+    const uint8_t *src = x < k ? b->orig[i][x] : (b->decode ? b->rec[i][x - k] : NULL);
+    if (!src) continue;
+    uint8_t *c = (uint8_t *)malloc(n);
+    if (!c) rc = -100;
+    else memcpy(c, src, n);
+    in[x] = c;
+  }
+  for (uint32_t x = 0; x < nout && !rc; ++x)
+    if (b->out[i][x]) {
+      out[x] = (uint8_t *)malloc(n);
+      if (!out[x]) rc = -100;
+    }
+  if (!rc)
+    rc = b->decode ? oracle_decode_engine(b->engine, k, m, n, in, in + k, out)
+                   : oracle_encode_engine(b->engine, k, m, n, in, out);
+  for (uint32_t x = 0; x < nout; ++x)
+    if (out[x]) {
+      if (!rc) memcpy(b->out[i][x], out[x], n);
+      free(out[x]);
+    }
+  for (uint32_t x = 0; x < k + m; ++x) free((void *)in[x]);
+  free(in);
+  free(out);
+  return rc;
+}
 
 static void *batch_worker(void *arg) {
   batch_t *b = (batch_t *)arg;
@@ -557,7 +596,8 @@ static void *batch_worker(void *arg) {
     int i = b->next++;
     pthread_mutex_unlock(&b->mu);
     if (i >= (int)b->nblocks) break;
-    int rc = b->decode ? oracle_decode_engine(b->engine, b->k[i], b->m, b->shard_bytes, b->orig[i],
+    int rc = b->copies ? block_with_copies(b, (uint32_t)i)
+           : b->decode ? oracle_decode_engine(b->engine, b->k[i], b->m, b->shard_bytes, b->orig[i],
                                               b->rec[i], b->out[i])
                        : oracle_encode_engine(b->engine, b->k[i], b->m, b->shard_bytes, b->orig[i],
                                               b->out[i]);
@@ -570,16 +610,22 @@ static void *batch_worker(void *arg) {
   return NULL;
 }
 
-int oracle_batch(int engine, int decode, int threads, uint32_t nblocks, const uint32_t *k,
-                 uint32_t m, size_t shard_bytes, const uint8_t *const *const *orig,
-                 const uint8_t *const *const *rec, uint8_t *const *const *out) {
+int oracle_batch2(int engine, int decode, int threads, uint32_t nblocks, const uint32_t *k,
+                  uint32_t m, size_t shard_bytes, const uint8_t *const *const *orig,
+                  const uint8_t *const *const *rec, uint8_t *const *const *out, int copies) {
   ensure_tables();
   batch_t b = {engine, decode, nblocks, m, k, shard_bytes, orig, rec, out, 0, 0,
-               PTHREAD_MUTEX_INITIALIZER};
+               PTHREAD_MUTEX_INITIALIZER, copies};
   if (threads < 1) threads = 1;
   pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)threads);
   for (int t = 0; t < threads; ++t) pthread_create(&th[t], NULL, batch_worker, &b);
   for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
   free(th);
   return b.err;
+}
+
+int oracle_batch(int engine, int decode, int threads, uint32_t nblocks, const uint32_t *k,
+                 uint32_t m, size_t shard_bytes, const uint8_t *const *const *orig,
+                 const uint8_t *const *const *rec, uint8_t *const *const *out) {
+  return oracle_batch2(engine, decode, threads, nblocks, k, m, shard_bytes, orig, rec, out, 0);
 }

@@ -71,3 +71,42 @@ def test_gloo_two_ranks_max_and_weak_throughput():
     for rank, m, v in res:
         assert m == 2.0                      # max over ranks
         assert v == pytest.approx(2 * 2 * 10 / 2.0)  # 2 ranks x 2 GiB x 10 steps / 2 s
+
+
+def test_bench_launcher_two_ranks_stub():
+    """bench.py --gpus 2 without torchrun: the parent spawns two rank
+    processes (gloo here; the codec calls are stubbed, no GPU), the line
+    reports n_gpus 2 with a world size of 2 observed by the process group, and
+    value is the whole-job weak-scaling rate from the max-over-ranks time."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--stub",
+           "--segments", "8", "--segment-bytes", "65536", "--steps", "3", "--warmup", "1",
+           "--settle-ms", "5", "--c4-segments", "40"]
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1  # rank 0 only
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["world_size_observed"] == 2
+    assert line["scaling"] == "weak" and line["data"].startswith("STUB")
+    # value = 2 ranks x (encode + decode) x 8 segments x 64 KiB x steps / max time
+    want = 2 * 2 * 8 * 65536 * 3 / 2**30 / (line["ms_per_step"] * 3 / 1e3)
+    assert line["value"] == pytest.approx(want, rel=0.02, abs=0.01)
+    c4 = line["c4_strong"]
+    assert c4["scaling"] == "strong" and c4["stripe_bytes_per_gpu"] == 32768
+    assert c4["blocks"] == [30, 10]
+
+
+def test_bench_refuses_mismatched_world(monkeypatch):
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--stub"],
+                       capture_output=True, text=True, timeout=120, env=env, cwd=root)
+    assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr

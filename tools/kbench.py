@@ -10,7 +10,7 @@ import os
 import sys
 import time
 
-PROBES = ("44",)  # traffic-only probes: no codec output to check
+PROBES = ("44", "72", "74")  # traffic-only probes: no codec output to check
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "blockframe-rs_amd"))
 
