@@ -18,14 +18,17 @@ constexpr uint32_t kTileHalfChunks = 256;
 
 // Nibble-table entry (8 B) index within one input's 64 entries (512 B); q =
 // 2*byte_hi + nib_hi selects which nibble of which symbol byte is looked up.
-//   high nibbles (q = 1, 3): bytes [0, 256): entry v of byte byte_hi at
-//     16*v + 8*byte_hi, so the lookup offset is (x & 0xF0) | 8*byte_hi -- the
-//     nibble stays in place and one mask-and-flag makes the address byte;
-//   low nibbles (q = 0, 2): bytes [256, 512): 256 + 128*byte_hi + 8*v.
-// Either way 16 entries of one (nibble half, byte) span 32 distinct LDS banks,
-// so a ds_read_b64 with any nibble per lane is conflict free.
+// Entry v of (nibble half, byte) sits at 16*v + 8*byte_hi of its 256-B half:
+//   high nibbles (q = 1, 3): bytes [0, 256), lookup offset (x & 0xF0) + 8*byte_hi
+//     -- the nibble stays in place;
+//   low nibbles (q = 0, 2): bytes [256, 512), offset ((x << 4) & 0xF0) + 8*byte_hi.
+// Both offsets are one SDWA op from the raw data byte (v_and_b32_sdwa /
+// v_lshlrev_b32_sdwa dst_sel:BYTE_0), the 8*byte_hi + half + input part an
+// immediate of the ds_read (the unrolled kernel, rs_kernels.hip).  The 16
+// entries of one (nibble half, byte) span 32 distinct LDS banks (a half-wave's
+// 32 ds_read_b64 hit distinct banks or broadcast): conflict free.
 constexpr uint32_t tab_idx(uint32_t q, uint32_t v) {
-  return (q & 1) ? 2 * v + (q >> 1) : 32 + (q >> 1) * 16 + v;
+  return (q & 1) ? 2 * v + (q >> 1) : 32 + 2 * v + (q >> 1);
 }
 
 // One pass: out[t] (^)= sum_i coef(t,i) * in[i] for t < n_out, over the
@@ -64,7 +67,9 @@ static_assert(sizeof(KernArgs) <= 4096, "kernel arguments must fit 4 KiB");
 uint32_t tile_bytes();
 int kernel_variant();
 
-hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in,
+// subfield: every pass of the launch has GF(2^8)-subfield coefficients
+// (PlanPass::subfield), so the subfield kernel form may run.
+hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in, bool subfield,
                            hipStream_t stream);
 hipError_t launch_gf_tail(const KernArgs &args, hipStream_t stream);
 

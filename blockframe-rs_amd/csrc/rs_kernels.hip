@@ -21,16 +21,19 @@
 //
 // LDS table layout per input i (512 B, tab_idx in kernels.hpp): high-nibble
 // entries at i*512 + 16*v + 8*byte_hi, low-nibble entries at i*512 + 256 +
-// 128*byte_hi + 8*v (q = 2*byte_hi + nib_hi: low/high nibble of the symbol's
-// low/high byte).  A lookup address is byte 0 = the offset within the
-// 256-B half, bytes 1-2 = 2i + (low nibble).  Byte 0 for four symbols at once
-// is one mask of the data dword for high nibbles (x & 0xF0, | 8 for the high
-// byte: one v_bitop3) and a shift + mask for low nibbles (nibble*8, | 0x80 for
-// the high byte); one v_perm_b32 splices byte b of it under the wave-uniform
-// 2i + (low nibble) -> 1 VALU per lookup.
+// 16*v + 8*byte_hi (q = 2*byte_hi + nib_hi: low/high nibble of the symbol's
+// low/high byte).  Looped kernels: a lookup address is byte 0 = the offset
+// within the 256-B half, bytes 1-2 = 2i + (low nibble).  Byte 0 for four
+// symbols at once is one mask of the data dword for high nibbles (x & 0xF0,
+// | 8 for the high byte: one v_bitop3) and a shift + mask for low nibbles
+// ((x << 4) & 0xF0, | 8 for the high byte); one v_perm_b32 splices byte b of it
+// under the wave-uniform 2i + (low nibble) -> 1 VALU per lookup.  The unrolled
+// kernel (tile_unrolled) needs no mask: one SDWA op per lookup straight from
+// the data byte, the input's table base in the ds_read immediate.
 #include "kernels.hpp"
 
 #include <algorithm>
+#include <utility>
 
 namespace bfrs {
 namespace {
@@ -62,9 +65,9 @@ __device__ __forceinline__ void mac_input_v1(const uint4 &L, const uint4 &H, uin
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
     // address bytes of 4 symbols; (x & M) | F is one v_bitop3 (0xEA)
-    const uint32_t ll = (l[d] << 3) & 0x78787878u;                                    // 8*v
+    const uint32_t ll = (l[d] << 4) & 0xF0F0F0F0u;                                    // 16*v
     const uint32_t lh = l[d] & 0xF0F0F0F0u;                                           // 16*v
-    const uint32_t hl = __builtin_amdgcn_bitop3_b32(h[d] << 3, 0x78787878u, 0x80808080u, 0xEA);
+    const uint32_t hl = __builtin_amdgcn_bitop3_b32(h[d] << 4, 0xF0F0F0F0u, 0x08080808u, 0xEA);
     const uint32_t hh = __builtin_amdgcn_bitop3_b32(h[d], 0xF0F0F0F0u, 0x08080808u, 0xEA);
     uint2 e[4][4];
 #pragma unroll
@@ -81,6 +84,48 @@ __device__ __forceinline__ void mac_input_v1(const uint4 &L, const uint4 &H, uin
       const int s = d * 4 + b;
       acc_lo[s] = xor3(xor3(acc_lo[s], e[b][0].x, e[b][1].x), e[b][2].x, e[b][3].x);
       acc_hi[s] = xor3(xor3(acc_hi[s], e[b][0].y, e[b][1].y), e[b][2].y, e[b][3].y);
+    }
+  }
+}
+
+__device__ __forceinline__ uint32_t lds_entry32(uint32_t byte_addr) {
+  return *(const AS_LDS uint32_t *)(uintptr_t)byte_addr;
+}
+
+// mac_input_v1 for passes whose coefficients all lie in the GF(2^8) subfield
+// (every RS(k<=30, 3) encode and decode; PlanPass::subfield).  There the
+// product of a symbol's low byte has a zero high byte (the high
+// output byte depends on the high input bytes only), so the two low-byte
+// lookups read only the 4-byte low half of their entries and the high
+// accumulator takes one 3-input XOR per symbol instead of two: 3 XORs per
+// symbol and input instead of 4 (-16 VALU per input and lane; the kernel is
+// VALU-bound, profiles/r02/).  Same table layout and addresses.
+__device__ __forceinline__ void mac_input_sub(const uint4 &L, const uint4 &H, uint32_t base_hi,
+                                              uint32_t base_lo, uint32_t (&acc_lo)[16],
+                                              uint32_t (&acc_hi)[16]) {
+  const uint32_t l[4] = {L.x, L.y, L.z, L.w};
+  const uint32_t h[4] = {H.x, H.y, H.z, H.w};
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const uint32_t ll = (l[d] << 4) & 0xF0F0F0F0u;
+    const uint32_t lh = l[d] & 0xF0F0F0F0u;
+    const uint32_t hl = __builtin_amdgcn_bitop3_b32(h[d] << 4, 0xF0F0F0F0u, 0x08080808u, 0xEA);
+    const uint32_t hh = __builtin_amdgcn_bitop3_b32(h[d], 0xF0F0F0F0u, 0x08080808u, 0xEA);
+    uint32_t a[4], b[4];
+    uint2 e2[4], e3[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t sel = 0x0C050400u | uint32_t(k);
+      a[k] = lds_entry32(__builtin_amdgcn_perm(base_lo, ll, sel));
+      b[k] = lds_entry32(__builtin_amdgcn_perm(base_hi, lh, sel));
+      e2[k] = lds_entry(nullptr, __builtin_amdgcn_perm(base_lo, hl, sel));
+      e3[k] = lds_entry(nullptr, __builtin_amdgcn_perm(base_hi, hh, sel));
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int s = d * 4 + k;
+      acc_lo[s] = xor3(xor3(acc_lo[s], a[k], b[k]), e2[k].x, e3[k].x);
+      acc_hi[s] = xor3(acc_hi[s], e2[k].y, e3[k].y);
     }
   }
 }
@@ -107,6 +152,25 @@ __device__ __forceinline__ uint32_t gather_byte(const uint32_t (&acc)[16], int d
 }
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// In-place 4x4 byte transpose of every group acc[4d..4d+3]: afterwards
+// acc[4d + t] holds byte t (output t) of the four symbols 4d..4d+3, i.e. the
+// dword gather_byte(acc, d, t) builds.  8 v_perm per group instead of ~28
+// shift/mask/or ops of the four gather_byte calls.
+__device__ __forceinline__ void transpose_outputs(uint32_t (&acc)[16]) {
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    uint32_t *a = acc + 4 * d;
+    const uint32_t x0 = __builtin_amdgcn_perm(a[1], a[0], 0x05010400u);  // a0.0 a1.0 a0.1 a1.1
+    const uint32_t x1 = __builtin_amdgcn_perm(a[1], a[0], 0x07030602u);  // a0.2 a1.2 a0.3 a1.3
+    const uint32_t y0 = __builtin_amdgcn_perm(a[3], a[2], 0x05010400u);
+    const uint32_t y1 = __builtin_amdgcn_perm(a[3], a[2], 0x07030602u);
+    a[0] = __builtin_amdgcn_perm(y0, x0, 0x05040100u);  // byte 0 of a0..a3
+    a[1] = __builtin_amdgcn_perm(y0, x0, 0x07060302u);  // byte 1
+    a[2] = __builtin_amdgcn_perm(y1, x1, 0x05040100u);  // byte 2
+    a[3] = __builtin_amdgcn_perm(y1, x1, 0x07060302u);  // byte 3
+  }
+}
 
 __device__ __forceinline__ uint4 load16(uint64_t a) {
   const u32x4 v = *(const AS_GLOBAL u32x4 *)(uintptr_t)a;
@@ -334,7 +398,9 @@ __device__ __forceinline__ CtLane ct_lane(uint64_t wchunk0, uint64_t full_chunks
 // vmcnt arithmetic constant, never consumed) read the last input's first
 // chunk -- one hot 64-B line -- instead of re-reading 2 KiB of its columns,
 // which with non-temporal loads costs real HBM traffic (2 of 30 inputs).
-template <int LPOL, int ROT = 0, bool PROBE = false, int TAIL = 0>
+// SLOTS: the tables sit in read order (stage_tables_rotated), so step x uses
+// slot x instead of input idx(x).
+template <int LPOL, int ROT = 0, bool PROBE = false, int TAIL = 0, int SUB = 0, bool SLOTS = false>
 __device__ __forceinline__ bool ring_acc_ct(const KernArgs &args, const PassDesc &P, uint32_t tile,
                                             uint32_t wave_id, uint32_t (&acc_lo)[16],
                                             uint32_t (&acc_hi)[16], CtLane &ln) {
@@ -364,12 +430,15 @@ __device__ __forceinline__ bool ring_acc_ct(const KernArgs &args, const PassDesc
         gload_ct<LPOL>(A, B, in[idx(x)], past ? ln.fb : offA, past ? ln.fb : offB);
       },
       [&](const u32x4 &Av, const u32x4 &Bv, uint32_t x) {
-        const uint32_t r = idx(x);
+        const uint32_t r = SLOTS ? x : idx(x);
         u32x4 L = Av, H = Bv;
         halves_swap(L, H);
         if constexpr (PROBE)  // traffic-only probe (measurement, NOT a codec)
           mac_input_stream(make_uint4(L.x, L.y, L.z, L.w), make_uint4(H.x, H.y, H.z, H.w), acc_lo,
                            acc_hi);
+        else if constexpr (SUB)
+          mac_input_sub(make_uint4(L.x, L.y, L.z, L.w), make_uint4(H.x, H.y, H.z, H.w), 2 * r,
+                        2 * r + 1, acc_lo, acc_hi);
         else
           mac_input_v1(make_uint4(L.x, L.y, L.z, L.w), make_uint4(H.x, H.y, H.z, H.w), 2 * r,
                        2 * r + 1, acc_lo, acc_hi);
@@ -377,20 +446,24 @@ __device__ __forceinline__ bool ring_acc_ct(const KernArgs &args, const PassDesc
   return true;
 }
 
-template <int LPOL, int SPOL, int ROT = 0, bool PROBE = false, int TAIL = 0>
+template <int LPOL, int SPOL, int ROT = 0, bool PROBE = false, int TAIL = 0, int SUB = 0,
+          bool SLOTS = false>
 __device__ __forceinline__ void ring_tile_ct(const KernArgs &args, const PassDesc &P, uint32_t tile,
                                              uint32_t wave_id) {
   uint32_t acc_lo[16], acc_hi[16];
   CtLane ln;
-  if (!ring_acc_ct<LPOL, ROT, PROBE, TAIL>(args, P, tile, wave_id, acc_lo, acc_hi, ln)) return;
+  if (!ring_acc_ct<LPOL, ROT, PROBE, TAIL, SUB, SLOTS>(args, P, tile, wave_id, acc_lo, acc_hi, ln))
+    return;
   const uint32_t n_out = P.n_out;
   const uint64_t *outp = args.ptrs + P.out;
   const bool accumulate = P.accumulate != 0;
-  for (uint32_t t = 0; t < n_out; ++t) {
-    u32x4 ol = {gather_byte(acc_lo, 0, t), gather_byte(acc_lo, 1, t), gather_byte(acc_lo, 2, t),
-                gather_byte(acc_lo, 3, t)};
-    u32x4 oh = {gather_byte(acc_hi, 0, t), gather_byte(acc_hi, 1, t), gather_byte(acc_hi, 2, t),
-                gather_byte(acc_hi, 3, t)};
+  transpose_outputs(acc_lo);
+  transpose_outputs(acc_hi);
+#pragma unroll
+  for (uint32_t t = 0; t < kMaxPassOutputs; ++t) {
+    if (t >= n_out) break;
+    u32x4 ol = {acc_lo[t], acc_lo[4 + t], acc_lo[8 + t], acc_lo[12 + t]};
+    u32x4 oh = {acc_hi[t], acc_hi[4 + t], acc_hi[8 + t], acc_hi[12 + t]};
     halves_swap(ol, oh);  // back to the contiguous layout: ol -> run A, oh -> run B
     const uint64_t dst = outp[t];
     if (accumulate) {
@@ -450,7 +523,8 @@ __device__ __forceinline__ uint32_t xcd_group_remap(uint32_t b, uint32_t n) {
 // LAY 0: half-chunk lanes (round 1); LAY 1: contiguous lines + lane-half
 // swaps (ring_acc_ct).  LPOL 1: non-temporal loads (only sound with LAY 1,
 // where every line is read by one instruction).
-template <int ROT, bool PROBE = false, uint32_t XG = 0, int LAY = 0, int LPOL = 0, int TAIL = 0>
+template <int ROT, bool PROBE = false, uint32_t XG = 0, int LAY = 0, int LPOL = 0, int TAIL = 0,
+          int SUB = 0>
 __global__ __launch_bounds__(256, 5) void gf_apply_ring_kernel(const KernArgs args) {
   uint32_t wg = blockIdx.x;
   if constexpr (XG > 0) wg = xcd_group_remap<XG>(blockIdx.x, gridDim.x);
@@ -460,10 +534,258 @@ __global__ __launch_bounds__(256, 5) void gf_apply_ring_kernel(const KernArgs ar
   const uint32_t wave_id = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   for (uint32_t tile = t_begin; tile < t_end; ++tile) {
     if constexpr (LAY == 1)
-      ring_tile_ct<LPOL, 1, ROT, PROBE, TAIL>(args, P, tile, wave_id);
+      ring_tile_ct<LPOL, 1, ROT, PROBE, TAIL, SUB>(args, P, tile, wave_id);
     else
       ring_tile_halfchunk<0, 1, ROT, PROBE>(args, P, tile, wave_id);
   }
+}
+
+// ---- fully unrolled path (v76) ------------------------------------------------
+// For the pass sizes BlockFrame runs (n_in = 30: every full RS(30,3) block,
+// encode or 3-erasure decode; 8: the bench's last block), the input loop is
+// unrolled at compile time.  The table of the input consumed at step x then
+// sits at a compile-time LDS offset (the workgroup stages its tables in its
+// own rotated read order: slot x <- input (rot + x) mod n_in), so a lookup
+// address is ONE SDWA op straight from the data byte -- no mask/shift prep,
+// no v_perm splice -- with slot, half and byte in the ds_read immediate:
+//   high nibble of byte k: v_and_b32_sdwa (byte k) & 0xF0        = 16*v
+//   low nibble of byte k : v_lshlrev_b32_sdwa (byte k) << 4, BYTE_0 = 16*v
+// Per symbol and input: 4 SDWA + 4 ds_read + 3 v_bitop3 (GF(2^8)-subfield
+// passes only; the host selects this kernel when every pass is), 7 VALU vs
+// ~9 of mac_input_sub.  The ring is the same 4-buffer, 3-in-flight ring with
+// compile-time buffers and vmcnt.
+
+// (byte K of x) & mask, mask = 0xF0 in an SGPR
+template <int K>
+__device__ __forceinline__ uint32_t sdwa_hi_nib16(uint32_t x, uint32_t mask) {
+  uint32_t r;
+  asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_%c3 src1_sel:DWORD"
+      : "=v"(r)
+      : "v"(x), "s"(mask), "i"(K));
+  return r;
+}
+// ((byte K of x) << 4) & 0xFF
+template <int K>
+__device__ __forceinline__ uint32_t sdwa_lo_nib16(uint32_t x) {
+  uint32_t r;
+  asm("v_lshlrev_b32_sdwa %0, 4, %1 dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_%c2"
+      : "=v"(r)
+      : "v"(x), "i"(K));
+  return r;
+}
+
+template <int N>
+__device__ __forceinline__ void vm_wait_n(u32x4 &A, u32x4 &B) {
+  if constexpr (N <= 0) vm_wait<0>(A, B);
+  else if constexpr (N == 2) vm_wait<2>(A, B);
+  else if constexpr (N == 4) vm_wait<4>(A, B);
+  else vm_wait<6>(A, B);
+}
+
+// 3-input XOR as a volatile asm: in the fully unrolled tile the compiler
+// would otherwise reorder the accumulator chains across inputs and keep
+// hundreds of lookup results live (3451 spilled VGPRs in the first build).
+__device__ __forceinline__ uint32_t xor3_ordered(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm volatile("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+// a ^ lo32(b) ^ lo32(c) where b, c are whole 8-byte LDS entries: naming the
+// 64-bit values as (unprinted) operands keeps the compiler from narrowing
+// their ds_read_b64 to ds_read_b32.  A wave64 ds_read_b32 runs at 128 B/clk,
+// i.e. in 32-bank mode, where the stride-16 tables put nibbles v and v + 8 in
+// one bank (2-way conflicts: SQ_LDS_BANK_CONFLICT = 32% of the cycles,
+// profiles/r02/); a ds_read_b64 takes the same 2 cycles conflict free.
+__device__ __forceinline__ uint32_t xor3_lo64(uint32_t a, uint64_t b, uint64_t c) {
+  uint32_t r;
+  asm volatile("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96 ; %4 %5"
+               : "=v"(r)
+               : "v"(a), "v"(uint32_t(b)), "v"(uint32_t(c)), "v"(b), "v"(c));
+  return r;
+}
+
+// One input's 16 symbols (L = low bytes, H = high bytes) into the
+// accumulators with the tables of slot SLOT (compile-time LDS offsets).
+// B64: the low-byte lookups read whole 8-byte entries (conflict free);
+// else 4-byte reads (32-bank mode: 2-way conflicts on the stride-16 tables).
+template <uint32_t SLOT, bool B64>
+__device__ __forceinline__ void mac_slot(const u32x4 &L, const u32x4 &H, uint32_t mask,
+                                         uint32_t (&acc_lo)[16], uint32_t (&acc_hi)[16]) {
+  const AS_LDS uint8_t *t = (const AS_LDS uint8_t *)(uintptr_t)(SLOT * 512u);
+  const uint32_t l[4] = {L.x, L.y, L.z, L.w};
+  const uint32_t h[4] = {H.x, H.y, H.z, H.w};
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    uint64_t a[4], b[4];
+    uint2 e2[4], e3[4];
+#define BFRS_LOOKUPS(K)                                                                  \
+  if constexpr (B64) {                                                                   \
+    a[K] = *(const AS_LDS uint64_t *)(t + 256 + sdwa_lo_nib16<K>(l[d]));                 \
+    b[K] = *(const AS_LDS uint64_t *)(t + sdwa_hi_nib16<K>(l[d], mask));                 \
+  } else {                                                                               \
+    a[K] = *(const AS_LDS uint32_t *)(t + 256 + sdwa_lo_nib16<K>(l[d]));                 \
+    b[K] = *(const AS_LDS uint32_t *)(t + sdwa_hi_nib16<K>(l[d], mask));                 \
+  }                                                                                      \
+  {                                                                                      \
+    const uint64_t v2 = *(const AS_LDS uint64_t *)(t + 256 + 8 + sdwa_lo_nib16<K>(h[d])); \
+    const uint64_t v3 = *(const AS_LDS uint64_t *)(t + 8 + sdwa_hi_nib16<K>(h[d], mask)); \
+    e2[K] = make_uint2(uint32_t(v2), uint32_t(v2 >> 32));                                \
+    e3[K] = make_uint2(uint32_t(v3), uint32_t(v3 >> 32));                                \
+  }
+    // two symbols (8 lookups) per group, a scheduling barrier after each
+    // group's XORs: letting the compiler hoist more lookups costs live VGPRs
+    // and spills at the 96-VGPR (5 waves/SIMD) budget
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      if (g == 0) {
+        BFRS_LOOKUPS(0)
+        BFRS_LOOKUPS(1)
+      } else {
+        BFRS_LOOKUPS(2)
+        BFRS_LOOKUPS(3)
+      }
+#pragma unroll
+      for (int k = 2 * g; k < 2 * g + 2; ++k) {
+        const int s = d * 4 + k;
+        const uint32_t lo2 = B64 ? xor3_lo64(acc_lo[s], a[k], b[k])
+                                 : xor3_ordered(acc_lo[s], uint32_t(a[k]), uint32_t(b[k]));
+        acc_lo[s] = xor3_ordered(lo2, e2[k].x, e3[k].x);
+        acc_hi[s] = xor3_ordered(acc_hi[s], e2[k].y, e3[k].y);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#undef BFRS_LOOKUPS
+  }
+}
+
+template <int N, int LPOL, bool B64, uint32_t C>
+__device__ __forceinline__ void unrolled_step(const uint64_t *in, uint32_t rot, const CtLane &ln,
+                                              uint32_t mask, u32x4 (&A)[N], u32x4 (&B)[N],
+                                              uint32_t (&acc_lo)[16], uint32_t (&acc_hi)[16]) {
+  constexpr int D = 3;  // inputs in flight ahead of the one consumed
+  if constexpr (C < uint32_t(N)) {  // issue input C
+    uint32_t src = rot + C;
+    src = src >= uint32_t(N) ? src - N : src;
+    gload_ct<LPOL>(A[C], B[C], in[src], ln.offA, ln.offB);
+  }
+  if constexpr (C >= uint32_t(D) && C - D < uint32_t(N)) {  // consume input C - D
+    constexpr uint32_t c = C - D;
+    constexpr int after = (N - 1 - int(c)) < D ? (N - 1 - int(c)) : D;
+    vm_wait_n<2 * after>(A[c], B[c]);
+    u32x4 L = A[c], H = B[c];
+    halves_swap(L, H);
+    mac_slot<c, B64>(L, H, mask, acc_lo, acc_hi);
+  }
+}
+
+template <int N, int LPOL, bool B64, uint32_t... Cs>
+__device__ __forceinline__ void unrolled_ring(const uint64_t *in, uint32_t rot, const CtLane &ln,
+                                              uint32_t mask, u32x4 (&A)[N], u32x4 (&B)[N],
+                                              uint32_t (&acc_lo)[16], uint32_t (&acc_hi)[16],
+                                              std::integer_sequence<uint32_t, Cs...>) {
+  (unrolled_step<N, LPOL, B64, Cs>(in, rot, ln, mask, A, B, acc_lo, acc_hi), ...);
+}
+
+template <int N, int LPOL, bool B64>
+__device__ __forceinline__ void tile_unrolled(const KernArgs &args, const PassDesc &P,
+                                              uint32_t tile, uint32_t wave_id, uint32_t rot) {
+  const uint64_t wchunk0 = (uint64_t(tile) * 4 + wave_id) * 32;
+  if (wchunk0 >= P.full_chunks) return;  // wave-uniform
+  const CtLane ln = ct_lane(wchunk0, P.full_chunks);
+  const uint64_t *in = args.ptrs + P.in;
+  const uint32_t mask = __builtin_amdgcn_readfirstlane(0xF0u);
+  uint32_t acc_lo[16], acc_hi[16];
+#pragma unroll
+  for (int s = 0; s < 16; ++s) acc_lo[s] = acc_hi[s] = 0;
+  u32x4 A[N], B[N];
+  unrolled_ring<N, LPOL, B64>(in, rot, ln, mask, A, B, acc_lo, acc_hi,
+                         std::make_integer_sequence<uint32_t, N + 3>{});
+  const uint32_t n_out = P.n_out;
+  const uint64_t *outp = args.ptrs + P.out;
+  const bool accumulate = P.accumulate != 0;
+  transpose_outputs(acc_lo);
+  transpose_outputs(acc_hi);
+#pragma unroll
+  for (uint32_t t = 0; t < kMaxPassOutputs; ++t) {
+    if (t >= n_out) break;
+    u32x4 ol = {acc_lo[t], acc_lo[4 + t], acc_lo[8 + t], acc_lo[12 + t]};
+    u32x4 oh = {acc_hi[t], acc_hi[4 + t], acc_hi[8 + t], acc_hi[12 + t]};
+    halves_swap(ol, oh);
+    const uint64_t dst = outp[t];
+    if (accumulate) {
+      if (ln.okA) {
+        const uint4 p = load16(dst + ln.offA);
+        ol ^= u32x4{p.x, p.y, p.z, p.w};
+      }
+      if (ln.okB) {
+        const uint4 p = load16(dst + ln.offB);
+        oh ^= u32x4{p.x, p.y, p.z, p.w};
+      }
+    }
+    if (ln.okA) store16_nt(dst + ln.offA, ol);
+    if (ln.okB) store16_nt(dst + ln.offB, oh);
+  }
+}
+
+// Pass lookup (binary search over wg_begin) without staging.
+__device__ __forceinline__ const PassDesc &find_pass(const KernArgs &args, uint32_t wg) {
+  const PassDesc *passes = args.passes;
+  uint32_t lo = 0, hi = args.n_passes;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (passes[mid].wg_begin <= wg)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  return passes[lo];
+}
+
+// Stages the pass tables in LDS in read order: slot x <- input (rot + x) mod n_in.
+__device__ __forceinline__ void stage_tables_rotated(const PassDesc &P, uint32_t rot) {
+  extern __shared__ __attribute__((aligned(16))) uint2 lds_table[];
+  const uint32_t n_in = P.n_in;
+  const AS_GLOBAL u32x4 *tab = (const AS_GLOBAL u32x4 *)(uintptr_t)P.table;
+  u32x4 *dst = reinterpret_cast<u32x4 *>(lds_table);
+  const uint32_t n16 = n_in * 32;  // 32 x 16 B per input
+  u32x4 v[kMaxPassInputs * 32 / 256];
+#pragma unroll
+  for (int r = 0; r < int(kMaxPassInputs * 32 / 256); ++r) {
+    const uint32_t e = threadIdx.x + 256u * r;
+    v[r] = e < n16 ? tab[e] : u32x4{0, 0, 0, 0};
+  }
+#pragma unroll
+  for (int r = 0; r < int(kMaxPassInputs * 32 / 256); ++r) {
+    const uint32_t e = threadIdx.x + 256u * r;
+    if (e < n16) {
+      const uint32_t i = e >> 5;  // source input
+      const uint32_t x = i >= rot ? i - rot : i + n_in - rot;  // its slot
+      dst[x * 32 + (e & 31)] = v[r];
+    }
+  }
+  __syncthreads();
+}
+
+// v76: unrolled SDWA-addressed path for n_in in {30, 8}, the looped
+// subfield path (slot-indexed tables) for any other pass of the launch.
+// Host contract: every pass subfield, tiles_per_wg == 1.
+template <bool B64>
+__global__ __launch_bounds__(256, 5) void gf_apply_unrolled_kernel(const KernArgs args) {
+  const uint32_t wg = xcd_group_remap<16>(blockIdx.x, gridDim.x);
+  const PassDesc &P = find_pass(args, wg);
+  const uint32_t tile = wg - P.wg_begin;
+  const uint32_t n_in = P.n_in;
+  const uint32_t rot = P.rotate ? ((tile >> 4) * 4) % n_in : 0;  // read order of v41/v58
+  stage_tables_rotated(P, rot);
+  if (tile >= P.n_tiles) return;
+  const uint32_t wave_id = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (n_in == 30)
+    tile_unrolled<30, 1, B64>(args, P, tile, wave_id, rot);
+  else if (n_in == 8)
+    tile_unrolled<8, 1, B64>(args, P, tile, wave_id, rot);
+  else
+    ring_tile_ct<1, 1, 6, false, 1, 1, true>(args, P, tile, wave_id);
 }
 
 // Tail chunk (shard_bytes % 64 = tb != 0): tb/2 symbols, low bytes at
@@ -502,7 +824,15 @@ __global__ __launch_bounds__(64) void gf_tail_kernel(const KernArgs args) {
 }  // namespace
 
 // Kernel variant selector for A/B measurement (tools/kbench.py).
-// 58 (default): 41 with each read group's 16 workgroups on one XCD.
+// 76 (default, round 2): contiguous-line loads/stores with lane-half swaps,
+// non-temporal loads, and for GF(2^8)-subfield launches (every RS(k<=30,3)
+// encode/decode) the fully unrolled SDWA-addressed kernel for n_in 30 / 8;
+// other launches fall back to 75 (looped, subfield) or 73 (looped, general).
+// 77: 76 with 4-byte low-byte lookups (2-way LDS bank conflicts).
+// 70-75: the round-2 steps: 70 contiguous lines, 71 + nt loads,
+// 73 + hot-line past-the-end loads, 75 + subfield arithmetic; 72 / 74:
+// traffic-only probes of 71 / 73.
+// Round 1: 58: 41 with each read group's 16 workgroups on one XCD.
 // 41: one input rotation per group of 16 consecutive tiles (the 16
 // workgroups stream one shard's 128 KiB together); 36 / 40 / 42: groups of
 // 1 / 8 / 32 tiles; 5: one rotation per wave (each wave of a tile on its own
@@ -511,14 +841,14 @@ __global__ __launch_bounds__(64) void gf_tail_kernel(const KernArgs args) {
 // in the git history and their results in DESIGN.md §9.
 int kernel_variant() {
   const char *e = std::getenv("BFRS_KERNEL_VARIANT");
-  int v = e ? atoi(e) : 58;
-  if ((v == 44 || v == 72 || v == 74) && !std::getenv("BFRS_ALLOW_PROBE")) v = 58;
+  int v = e ? atoi(e) : 76;
+  if ((v == 44 || v == 72 || v == 74) && !std::getenv("BFRS_ALLOW_PROBE")) v = 76;
   return v;
 }
 
 uint32_t tile_bytes() { return kTileHalfChunks * 32; }
 
-hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in,
+hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in, bool subfield,
                            hipStream_t stream) {
   if (n_wgs == 0) return hipSuccess;
   const size_t lds = size_t(max_in) * 64 * sizeof(uint2);
@@ -555,6 +885,26 @@ hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in
       break;
     case 73:  // 71 with the ring's past-the-end loads on one hot line
       hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16, 1, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
+      break;
+    case 75:  // 73 with the GF(2^8)-subfield arithmetic when every pass allows it
+      if (subfield)
+        hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16, 1, 1, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
+      else
+        hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16, 1, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
+      break;
+    case 77:  // 76 with 4-byte low-byte lookups
+      if (subfield && args.tiles_per_wg == 1) {
+        hipLaunchKernelGGL(gf_apply_unrolled_kernel<false>, dim3(n_wgs), dim3(256), lds, stream, args);
+        break;
+      }
+      [[fallthrough]];
+    case 76:  // unrolled SDWA-addressed kernel where the launch allows it, else 75
+      if (subfield && args.tiles_per_wg == 1)
+        hipLaunchKernelGGL(gf_apply_unrolled_kernel<true>, dim3(n_wgs), dim3(256), lds, stream, args);
+      else if (subfield)
+        hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16, 1, 1, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
+      else
+        hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16, 1, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
       break;
     case 74:  // traffic-only probe of 73
       hipLaunchKernelGGL((gf_apply_ring_kernel<6, true, 16, 1, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);

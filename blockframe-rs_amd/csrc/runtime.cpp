@@ -72,6 +72,13 @@ static int upload_plan(Plan *p) {
       offs.push_back(all.size());
       all.insert(all.end(), t.begin(), t.end());
       PlanPass pp;
+      pp.subfield = true;
+      for (size_t r = r0; r < r1 && pp.subfield; ++r)
+        for (size_t cc = c0; cc < c1; ++cc)
+          if (c.at(r, cc) >= 256) {
+            pp.subfield = false;
+            break;
+          }
       pp.r0 = uint32_t(r0);
       pp.r1 = uint32_t(r1);
       pp.c0 = uint32_t(c0);
@@ -321,6 +328,7 @@ int Context::run_window(const std::vector<BlockIO> &blocks, size_t shard_bytes,
       ka.n_passes = uint32_t(last - first);
       ka.tiles_per_wg = tpw;
       uint32_t pi = 0, wg = 0, max_in = 0;
+      bool subfield = true;
       for (size_t it = first; it < last; ++it) {
         const BlockIO &b = *items[it].b;
         const PlanPass &p = *items[it].p;
@@ -333,6 +341,7 @@ int Context::run_window(const std::vector<BlockIO> &blocks, size_t shard_bytes,
         d.out = pi;
         for (uint32_t r = p.r0; r < p.r1; ++r) ka.ptrs[pi++] = reinterpret_cast<uint64_t>(b.out[r]);
         d.table = reinterpret_cast<uint64_t>(p.d_table);
+        subfield = subfield && p.subfield;
         d.n_in = n_pad;
         d.n_out = p.r1 - p.r0;
         d.wg_begin = wg;
@@ -345,7 +354,7 @@ int Context::run_window(const std::vector<BlockIO> &blocks, size_t shard_bytes,
         wg += wgs_per_pass;
         max_in = std::max(max_in, n_pad);
       }
-      if (n_tiles) HIP_TRY(launch_gf_apply(ka, wg, max_in, s));
+      if (n_tiles) HIP_TRY(launch_gf_apply(ka, wg, max_in, subfield, s));
       if (tail) HIP_TRY(launch_gf_tail(ka, s));
       first = last;
     }

@@ -61,6 +61,10 @@ struct PlanPass {
   uint32_t r0, r1, c0, c1;
   uint32_t phase;  // input-group index; phase > 0 accumulates
   const uint2 *d_table = nullptr;
+  // every coefficient lies in the GF(2^8) subfield (values < 256):
+  // the products of a symbol's low byte then have a zero high byte, so the
+  // kernel reads those table entries as 4 bytes and skips their high XORs
+  bool subfield = false;
 };
 
 // A coefficient plan for one (k, m, erasure pattern), tables on device.
