@@ -3,11 +3,19 @@
 // reference uses it (src/chunker/generate.rs:37-49,84-96;
 // src/filestore/recovery.rs:58-69,152-170; src/filestore/health.rs:733-752).
 //
-// Shards added from host memory are copied straight into device memory (the
-// crate likewise copies each added shard into its work area); encode()/decode()
-// run the HIP pass and bring the results back to host buffers owned by the
-// object, valid until the next call on it.
+// Each object holds a CodecSlot from its context's cache (runtime.hpp): k + m
+// shard rows of HBM, the same rows of pinned host memory, and a stream of its
+// own.  add_*_shard copies the caller's bytes into the pinned row (the crate
+// likewise copies each added shard into its work area, so the caller may
+// reuse its buffer at once) and queues the row's H2D copy, so the copy of
+// shard i+1 overlaps the DMA of shard i.  encode()/decode() queue the HIP
+// pass and the D2H of the results into pinned rows; results stay valid until
+// the next call on the object.  Objects are used by one thread at a time;
+// objects of one context may live on different threads.
+#include <algorithm>
+#include <cstring>
 #include <sstream>
+#include <thread>
 
 #include "runtime.hpp"
 
@@ -15,39 +23,63 @@ using namespace bfrs;
 
 namespace {
 
-struct DevBuf {
-  void *p = nullptr;
-  ~DevBuf() {
-    if (p) (void)hipFree(p);
-  }
-};
-
-size_t stride_of(size_t shard_bytes) { return (shard_bytes + 255) / 256 * 256; }
-
 int shard_size_error(size_t expected, size_t got) {
   std::ostringstream os;
   os << "different shard size: expected " << expected << " bytes, got " << got << " bytes";
   return set_error(BFRS_E_DIFFERENT_SHARD_SIZE, os.str());
 }
 
-}  // namespace
+// Host copy into pinned memory: a few threads for large shards (one core
+// copies ~10-20 GB/s; the PCIe link takes ~50 GB/s).
+void copy_in(uint8_t *dst, const uint8_t *src, size_t n) {
+  constexpr size_t kPart = 8u << 20;
+  const size_t parts = std::min<size_t>(4, n / kPart);
+  if (parts < 2) {
+    std::memcpy(dst, src, n);
+    return;
+  }
+  const size_t per = (n / parts + 63) / 64 * 64;
+  std::thread th[4];
+  for (size_t t = 1; t < parts; ++t) {
+    const size_t a = t * per, b = std::min(n, a + per);
+    th[t] = std::thread([=] { std::memcpy(dst + a, src + a, b - a); });
+  }
+  std::memcpy(dst, src, std::min(n, per));
+  for (size_t t = 1; t < parts; ++t) th[t].join();
+}
 
-struct bfrs_encoder {
+struct CodecObject {
   bfrs_ctx *ctx;
   size_t k, m, shard_bytes;
-  size_t received = 0;
-  bool encoded = false;
-  DevBuf dev;                              // (k + m) shard slots
-  std::vector<std::vector<uint8_t>> recovery;
+  std::unique_ptr<CodecSlot> slot;
+  uint8_t *d_row(size_t i) const { return static_cast<uint8_t *>(slot->d) + i * slot->stride; }
+  uint8_t *h_row(size_t i) const { return slot->h + i * slot->stride; }
+  // stage a host shard into row i (pinned copy + async H2D on the slot stream)
+  int stage(size_t i, const uint8_t *src, size_t len) {
+    HIP_TRY(hipSetDevice(ctx->impl.device));
+    // the row's previous H2D (an earlier round on this object) must be done
+    // before its pinned bytes are overwritten: rows are reused only after
+    // encode()/decode() synchronised the stream, so no wait is needed here
+    copy_in(h_row(i), src, len);
+    HIP_TRY(hipMemcpyAsync(d_row(i), h_row(i), len, hipMemcpyHostToDevice, slot->stream));
+    return BFRS_OK;
+  }
+  ~CodecObject() {
+    if (slot) ctx->impl.codec_release(std::move(slot));
+  }
 };
 
-struct bfrs_decoder {
-  bfrs_ctx *ctx;
-  size_t k, m, shard_bytes;
+}  // namespace
+
+struct bfrs_encoder : CodecObject {
+  size_t received = 0;
+  bool encoded = false;
+};
+
+struct bfrs_decoder : CodecObject {
   std::vector<uint8_t> orig_present, rec_present;
+  std::vector<uint8_t> restored;  // 1 = row i holds a restored original (pinned)
   bool decoded = false;
-  DevBuf dev;                              // (k + m) shard slots
-  std::vector<std::vector<uint8_t>> restored;  // index by original; empty = not restored
 };
 
 extern "C" {
@@ -58,13 +90,15 @@ int bfrs_encoder_new(bfrs_ctx *ctx, size_t k, size_t m, size_t shard_bytes, bfrs
   *out = nullptr;
   int rc = check_shape(k, m, shard_bytes);
   if (rc) return rc;
-  auto *e = new (std::nothrow) bfrs_encoder{ctx, k, m, shard_bytes};
+  auto *e = new (std::nothrow) bfrs_encoder;
   if (!e) return set_error(BFRS_E_NOMEM, "encoder allocation failed");
-  hipError_t he = hipSetDevice(ctx->impl.device);
-  if (he == hipSuccess) he = hipMalloc(&e->dev.p, stride_of(shard_bytes) * (k + m));
-  if (he != hipSuccess) {
+  e->ctx = ctx;
+  e->k = k;
+  e->m = m;
+  e->shard_bytes = shard_bytes;
+  if ((rc = ctx->impl.codec_acquire(k + m, shard_bytes, &e->slot))) {
     delete e;
-    return hip_error(he, "bfrs_encoder_new: hipMalloc");
+    return rc;
   }
   *out = e;
   return BFRS_OK;
@@ -84,11 +118,8 @@ int bfrs_encoder_add_original_shard(bfrs_encoder *e, const uint8_t *shard, size_
     return set_error(BFRS_E_TOO_MANY_ORIGINAL_SHARDS, os.str());
   }
   if (len != e->shard_bytes) return shard_size_error(e->shard_bytes, len);
-  hipError_t he = hipSetDevice(e->ctx->impl.device);
-  if (he == hipSuccess)
-    he = hipMemcpy(static_cast<uint8_t *>(e->dev.p) + e->received * stride_of(e->shard_bytes),
-                   shard, len, hipMemcpyHostToDevice);
-  if (he != hipSuccess) return hip_error(he, "add_original_shard: hipMemcpy");
+  int rc = e->stage(e->received, shard, len);
+  if (rc) return rc;
   ++e->received;
   return BFRS_OK;
   BFRS_API_END
@@ -103,25 +134,17 @@ int bfrs_encoder_encode(bfrs_encoder *e) {
        << " shards while original_count is " << e->k;
     return set_error(BFRS_E_TOO_FEW_ORIGINAL_SHARDS, os.str());
   }
-  const size_t st = stride_of(e->shard_bytes);
-  auto *d = static_cast<uint8_t *>(e->dev.p);
   std::vector<const uint8_t *> din(e->k);
   std::vector<uint8_t *> dout(e->m);
-  for (size_t i = 0; i < e->k; ++i) din[i] = d + i * st;
-  for (size_t j = 0; j < e->m; ++j) dout[j] = d + (e->k + j) * st;
-  uint32_t kk = uint32_t(e->k);
-  int rc = encode_batch_on(e->ctx, 1, &kk, e->m, e->shard_bytes, din.data(), dout.data(),
-                           e->ctx->impl.stream);
+  for (size_t i = 0; i < e->k; ++i) din[i] = e->d_row(i);
+  for (size_t j = 0; j < e->m; ++j) dout[j] = e->d_row(e->k + j);
+  const uint32_t kk = uint32_t(e->k);
+  hipStream_t st = e->slot->stream;
+  int rc = encode_batch_on(e->ctx, 1, &kk, e->m, e->shard_bytes, din.data(), dout.data(), st);
   if (rc) return rc;
-  e->recovery.assign(e->m, std::vector<uint8_t>(e->shard_bytes));
-  Context &c = e->ctx->impl;
-  for (size_t j = 0; j < e->m; ++j) {
-    hipError_t he = hipMemcpyAsync(e->recovery[j].data(), dout[j], e->shard_bytes,
-                                   hipMemcpyDeviceToHost, c.stream);
-    if (he != hipSuccess) return hip_error(he, "encode: D2H");
-  }
-  hipError_t he = hipStreamSynchronize(c.stream);
-  if (he != hipSuccess) return hip_error(he, "encode: sync");
+  for (size_t j = 0; j < e->m; ++j)
+    HIP_TRY(hipMemcpyAsync(e->h_row(e->k + j), dout[j], e->shard_bytes, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
   e->encoded = true;
   return BFRS_OK;
   BFRS_API_END
@@ -130,13 +153,13 @@ int bfrs_encoder_encode(bfrs_encoder *e) {
 int bfrs_encoder_recovery(bfrs_encoder *e, size_t index, const uint8_t **data, size_t *len) {
   BFRS_API_BEGIN
   if (!e || !data || !len) return set_error(BFRS_E_INVALID_ARGUMENT, "recovery: NULL argument");
-  if (!e->encoded || index >= e->recovery.size()) {
+  if (!e->encoded || index >= e->m) {
     std::ostringstream os;
     os << "invalid recovery shard index: " << index << " >= recovery_count " << e->m;
     return set_error(BFRS_E_INVALID_RECOVERY_SHARD_INDEX, os.str());
   }
-  *data = e->recovery[index].data();
-  *len = e->recovery[index].size();
+  *data = e->h_row(e->k + index);
+  *len = e->shard_bytes;
   return BFRS_OK;
   BFRS_API_END
 }
@@ -149,15 +172,17 @@ int bfrs_decoder_new(bfrs_ctx *ctx, size_t k, size_t m, size_t shard_bytes, bfrs
   *out = nullptr;
   int rc = check_shape(k, m, shard_bytes);
   if (rc) return rc;
-  auto *d = new (std::nothrow) bfrs_decoder{ctx, k, m, shard_bytes};
+  auto *d = new (std::nothrow) bfrs_decoder;
   if (!d) return set_error(BFRS_E_NOMEM, "decoder allocation failed");
+  d->ctx = ctx;
+  d->k = k;
+  d->m = m;
+  d->shard_bytes = shard_bytes;
   d->orig_present.assign(k, 0);
   d->rec_present.assign(m, 0);
-  hipError_t he = hipSetDevice(ctx->impl.device);
-  if (he == hipSuccess) he = hipMalloc(&d->dev.p, stride_of(shard_bytes) * (k + m));
-  if (he != hipSuccess) {
+  if ((rc = ctx->impl.codec_acquire(k + m, shard_bytes, &d->slot))) {
     delete d;
-    return hip_error(he, "bfrs_decoder_new: hipMalloc");
+    return rc;
   }
   *out = d;
   return BFRS_OK;
@@ -189,11 +214,8 @@ int bfrs_decoder_add_original_shard(bfrs_decoder *d, size_t index, const uint8_t
     return set_error(BFRS_E_DUPLICATE_ORIGINAL_SHARD_INDEX, os.str());
   }
   if (len != d->shard_bytes) return shard_size_error(d->shard_bytes, len);
-  hipError_t he = hipSetDevice(d->ctx->impl.device);
-  if (he == hipSuccess)
-    he = hipMemcpy(static_cast<uint8_t *>(d->dev.p) + index * stride_of(d->shard_bytes), shard,
-                   len, hipMemcpyHostToDevice);
-  if (he != hipSuccess) return hip_error(he, "add_original_shard: hipMemcpy");
+  int rc = d->stage(index, shard, len);
+  if (rc) return rc;
   d->orig_present[index] = 1;
   return BFRS_OK;
   BFRS_API_END
@@ -215,11 +237,8 @@ int bfrs_decoder_add_recovery_shard(bfrs_decoder *d, size_t index, const uint8_t
     return set_error(BFRS_E_DUPLICATE_RECOVERY_SHARD_INDEX, os.str());
   }
   if (len != d->shard_bytes) return shard_size_error(d->shard_bytes, len);
-  hipError_t he = hipSetDevice(d->ctx->impl.device);
-  if (he == hipSuccess)
-    he = hipMemcpy(static_cast<uint8_t *>(d->dev.p) + (d->k + index) * stride_of(d->shard_bytes),
-                   shard, len, hipMemcpyHostToDevice);
-  if (he != hipSuccess) return hip_error(he, "add_recovery_shard: hipMemcpy");
+  int rc = d->stage(d->k + index, shard, len);
+  if (rc) return rc;
   d->rec_present[index] = 1;
   return BFRS_OK;
   BFRS_API_END
@@ -237,37 +256,34 @@ int bfrs_decoder_decode(bfrs_decoder *d) {
        << d->k << " original_count";
     return set_error(BFRS_E_NOT_ENOUGH_SHARDS, os.str());
   }
-  d->restored.assign(d->k, {});
+  d->restored.assign(d->k, 0);
   d->decoded = true;
-  if (orig_recv == d->k) return BFRS_OK;
-
-  const size_t st = stride_of(d->shard_bytes);
-  auto *base = static_cast<uint8_t *>(d->dev.p);
-  // Restored shards are written over the erased originals' own slots.
+  hipStream_t st = d->slot->stream;
+  if (orig_recv == d->k) {  // nothing to restore; the staged copies still have to land
+    HIP_TRY(hipStreamSynchronize(st));
+    return BFRS_OK;
+  }
+  // Restored shards are written over the erased originals' own rows.
   std::vector<const uint8_t *> dorig(d->k), drec(d->m);
   std::vector<uint8_t *> drest(d->k, nullptr);
   for (size_t i = 0; i < d->k; ++i) {
     if (d->orig_present[i])
-      dorig[i] = base + i * st;
+      dorig[i] = d->d_row(i);
     else
-      drest[i] = base + i * st;
+      drest[i] = d->d_row(i);
   }
   for (size_t j = 0; j < d->m; ++j)
-    if (d->rec_present[j]) drec[j] = base + (d->k + j) * st;
-  uint32_t kk = uint32_t(d->k);
+    if (d->rec_present[j]) drec[j] = d->d_row(d->k + j);
+  const uint32_t kk = uint32_t(d->k);
   int rc = decode_batch_on(d->ctx, 1, &kk, d->m, d->shard_bytes, dorig.data(), drec.data(),
-                           drest.data(), d->ctx->impl.stream);
+                           drest.data(), st);
   if (rc) return rc;
-  Context &c = d->ctx->impl;
   for (size_t i = 0; i < d->k; ++i)
     if (!d->orig_present[i]) {
-      d->restored[i].resize(d->shard_bytes);
-      hipError_t he = hipMemcpyAsync(d->restored[i].data(), drest[i], d->shard_bytes,
-                                     hipMemcpyDeviceToHost, c.stream);
-      if (he != hipSuccess) return hip_error(he, "decode: D2H");
+      HIP_TRY(hipMemcpyAsync(d->h_row(i), drest[i], d->shard_bytes, hipMemcpyDeviceToHost, st));
+      d->restored[i] = 1;
     }
-  hipError_t he = hipStreamSynchronize(c.stream);
-  if (he != hipSuccess) return hip_error(he, "decode: sync");
+  HIP_TRY(hipStreamSynchronize(st));
   return BFRS_OK;
   BFRS_API_END
 }
@@ -279,10 +295,10 @@ int bfrs_decoder_restored_original(bfrs_decoder *d, size_t index, const uint8_t 
     return set_error(BFRS_E_INVALID_ARGUMENT, "restored_original: NULL argument");
   *data = nullptr;
   *len = 0;
-  if (!d->decoded || index >= d->restored.size() || d->restored[index].empty())
+  if (!d->decoded || index >= d->restored.size() || !d->restored[index])
     return set_error(BFRS_E_NOT_RESTORED, "original shard was not restored");
-  *data = d->restored[index].data();
-  *len = d->restored[index].size();
+  *data = d->h_row(index);
+  *len = d->shard_bytes;
   return BFRS_OK;
   BFRS_API_END
 }

@@ -403,7 +403,8 @@ __device__ __forceinline__ CtLane ct_lane(uint64_t wchunk0, uint64_t full_chunks
 template <int LPOL, int ROT = 0, bool PROBE = false, int TAIL = 0, int SUB = 0, bool SLOTS = false>
 __device__ __forceinline__ bool ring_acc_ct(const KernArgs &args, const PassDesc &P, uint32_t tile,
                                             uint32_t wave_id, uint32_t (&acc_lo)[16],
-                                            uint32_t (&acc_hi)[16], CtLane &ln) {
+                                            uint32_t (&acc_hi)[16], CtLane &ln,
+                                            uint32_t slots_rot = 0) {
   const uint32_t n_in = P.n_in;
   const uint64_t *in = args.ptrs + P.in;
   const uint64_t wchunk0 = (uint64_t(tile) * 4 + wave_id) * 32;
@@ -412,7 +413,9 @@ __device__ __forceinline__ bool ring_acc_ct(const KernArgs &args, const PassDesc
   const uint32_t offA = ln.offA, offB = ln.offB;
 #pragma unroll
   for (int s = 0; s < 16; ++s) acc_lo[s] = acc_hi[s] = 0;
-  const uint32_t rot = !P.rotate || ROT == 2 ? 0
+  // SLOTS: the caller staged the tables in its read order and passes it
+  const uint32_t rot = SLOTS                ? slots_rot
+                       : !P.rotate || ROT == 2 ? 0
                        : ROT == 1           ? (tile * 4) % n_in
                        : ROT >= 3           ? ((tile >> (ROT - 2)) * 4) % n_in
                                             : (tile * 4 + wave_id) % n_in;
@@ -449,10 +452,11 @@ __device__ __forceinline__ bool ring_acc_ct(const KernArgs &args, const PassDesc
 template <int LPOL, int SPOL, int ROT = 0, bool PROBE = false, int TAIL = 0, int SUB = 0,
           bool SLOTS = false>
 __device__ __forceinline__ void ring_tile_ct(const KernArgs &args, const PassDesc &P, uint32_t tile,
-                                             uint32_t wave_id) {
+                                             uint32_t wave_id, uint32_t slots_rot = 0) {
   uint32_t acc_lo[16], acc_hi[16];
   CtLane ln;
-  if (!ring_acc_ct<LPOL, ROT, PROBE, TAIL, SUB, SLOTS>(args, P, tile, wave_id, acc_lo, acc_hi, ln))
+  if (!ring_acc_ct<LPOL, ROT, PROBE, TAIL, SUB, SLOTS>(args, P, tile, wave_id, acc_lo, acc_hi, ln,
+                                                       slots_rot))
     return;
   const uint32_t n_out = P.n_out;
   const uint64_t *outp = args.ptrs + P.out;
@@ -770,13 +774,15 @@ __device__ __forceinline__ void stage_tables_rotated(const PassDesc &P, uint32_t
 // v76: unrolled SDWA-addressed path for n_in in {30, 8}, the looped
 // subfield path (slot-indexed tables) for any other pass of the launch.
 // Host contract: every pass subfield, tiles_per_wg == 1.
-template <bool B64>
+// GL: log2 of the read group (consecutive tiles sharing one starting input,
+// placed on one XCD); STEP: how far consecutive groups' starting inputs move.
+template <bool B64, int GL = 6, int STEP = 4>
 __global__ __launch_bounds__(256, 5) void gf_apply_unrolled_kernel(const KernArgs args) {
-  const uint32_t wg = xcd_group_remap<16>(blockIdx.x, gridDim.x);
+  const uint32_t wg = xcd_group_remap<(1u << GL)>(blockIdx.x, gridDim.x);
   const PassDesc &P = find_pass(args, wg);
   const uint32_t tile = wg - P.wg_begin;
   const uint32_t n_in = P.n_in;
-  const uint32_t rot = P.rotate ? ((tile >> 4) * 4) % n_in : 0;  // read order of v41/v58
+  const uint32_t rot = P.rotate ? ((tile >> GL) * STEP) % n_in : 0;  // read order of v41/v58
   stage_tables_rotated(P, rot);
   if (tile >= P.n_tiles) return;
   const uint32_t wave_id = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -785,7 +791,7 @@ __global__ __launch_bounds__(256, 5) void gf_apply_unrolled_kernel(const KernArg
   else if (n_in == 8)
     tile_unrolled<8, 1, B64>(args, P, tile, wave_id, rot);
   else
-    ring_tile_ct<1, 1, 6, false, 1, 1, true>(args, P, tile, wave_id);
+    ring_tile_ct<1, 1, 6, false, 1, 1, true>(args, P, tile, wave_id, rot);
 }
 
 // Tail chunk (shard_bytes % 64 = tb != 0): tb/2 symbols, low bytes at
@@ -826,9 +832,12 @@ __global__ __launch_bounds__(64) void gf_tail_kernel(const KernArgs args) {
 // Kernel variant selector for A/B measurement (tools/kbench.py).
 // 76 (default, round 2): contiguous-line loads/stores with lane-half swaps,
 // non-temporal loads, and for GF(2^8)-subfield launches (every RS(k<=30,3)
-// encode/decode) the fully unrolled SDWA-addressed kernel for n_in 30 / 8;
-// other launches fall back to 75 (looped, subfield) or 73 (looped, general).
-// 77: 76 with 4-byte low-byte lookups (2-way LDS bank conflicts).
+// encode/decode) the fully unrolled SDWA-addressed kernel for n_in 30 / 8,
+// read groups of 64 consecutive tiles (512 KiB of every shard's columns) on
+// one XCD; other launches fall back to 75 (looped, subfield) or 73 (looped,
+// general).  77: 76 with 4-byte low-byte lookups (2-way LDS bank conflicts);
+// 78-80: read groups of 16 / 32 / 128 tiles; 81-83: group start moving by
+// 1 / 2 / 8 inputs instead of 4.
 // 70-75: the round-2 steps: 70 contiguous lines, 71 + nt loads,
 // 73 + hot-line past-the-end loads, 75 + subfield arithmetic; 72 / 74:
 // traffic-only probes of 71 / 73.
@@ -892,6 +901,29 @@ hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in
       else
         hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16, 1, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
       break;
+    case 78:  // 76 with read groups of 16 tiles (the round-1 grouping)
+    case 79:  // 76 with read groups of 32 tiles
+    case 80:  // 76 with read groups of 128 tiles
+    case 81:  // 76 with the group start moving by 1 input
+    case 82:  // 76 with the group start moving by 2 inputs
+    case 83:  // 76 with the group start moving by 8 inputs
+      if (subfield && args.tiles_per_wg == 1) {
+        const int v = kernel_variant();
+        if (v == 78)
+          hipLaunchKernelGGL((gf_apply_unrolled_kernel<true, 4, 4>), dim3(n_wgs), dim3(256), lds, stream, args);
+        else if (v == 79)
+          hipLaunchKernelGGL((gf_apply_unrolled_kernel<true, 5, 4>), dim3(n_wgs), dim3(256), lds, stream, args);
+        else if (v == 80)
+          hipLaunchKernelGGL((gf_apply_unrolled_kernel<true, 7, 4>), dim3(n_wgs), dim3(256), lds, stream, args);
+        else if (v == 81)
+          hipLaunchKernelGGL((gf_apply_unrolled_kernel<true, 6, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
+        else if (v == 82)
+          hipLaunchKernelGGL((gf_apply_unrolled_kernel<true, 6, 2>), dim3(n_wgs), dim3(256), lds, stream, args);
+        else
+          hipLaunchKernelGGL((gf_apply_unrolled_kernel<true, 6, 8>), dim3(n_wgs), dim3(256), lds, stream, args);
+        break;
+      }
+      [[fallthrough]];
     case 77:  // 76 with 4-byte low-byte lookups
       if (subfield && args.tiles_per_wg == 1) {
         hipLaunchKernelGGL(gf_apply_unrolled_kernel<false>, dim3(n_wgs), dim3(256), lds, stream, args);

@@ -98,9 +98,61 @@ static int upload_plan(Plan *p) {
   return BFRS_OK;
 }
 
+CodecSlot::~CodecSlot() {
+  if (stream) {
+    (void)hipStreamSynchronize(stream);
+    (void)hipStreamDestroy(stream);
+  }
+  if (d) (void)hipFree(d);
+  if (h) (void)hipHostFree(h);
+}
+
+int Context::codec_acquire(size_t nshards, size_t shard_bytes, std::unique_ptr<CodecSlot> *out) {
+  const size_t stride = (shard_bytes + 255) / 256 * 256;
+  {
+    std::lock_guard<std::mutex> g(codec_mu);
+    for (size_t i = 0; i < codec_free.size(); ++i)
+      if (codec_free[i]->stride >= stride && codec_free[i]->nshards >= nshards &&
+          codec_free[i]->stride * codec_free[i]->nshards <= 2 * stride * nshards) {
+        *out = std::move(codec_free[i]);
+        codec_free.erase(codec_free.begin() + long(i));
+        return BFRS_OK;
+      }
+  }
+  auto s = std::make_unique<CodecSlot>();
+  s->stride = stride;
+  s->nshards = nshards;
+  HIP_TRY(hipSetDevice(device));
+  HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+  HIP_TRY(hipMalloc(&s->d, stride * nshards));
+  HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&s->h), stride * nshards, hipHostMallocDefault));
+  *out = std::move(s);
+  return BFRS_OK;
+}
+
+void Context::codec_release(std::unique_ptr<CodecSlot> slot) {
+  if (!slot) return;
+  (void)hipStreamSynchronize(slot->stream);
+  std::unique_ptr<CodecSlot> drop;
+  std::lock_guard<std::mutex> g(codec_mu);
+  if (codec_free.size() < codec_cached) {
+    codec_free.push_back(std::move(slot));
+  } else {  // keep the larger slot
+    size_t small = 0;
+    for (size_t i = 1; i < codec_free.size(); ++i)
+      if (codec_free[i]->stride * codec_free[i]->nshards <
+          codec_free[small]->stride * codec_free[small]->nshards)
+        small = i;
+    if (codec_free[small]->stride * codec_free[small]->nshards < slot->stride * slot->nshards)
+      std::swap(codec_free[small], slot);
+    drop = std::move(slot);  // freed outside... after the lock guard (declared first)
+  }
+}
+
 Context::~Context() {
   if (device >= 0) (void)hipSetDevice(device);
   if (stream) (void)hipStreamSynchronize(stream);
+  codec_free.clear();
   staging.reset();  // archive staging arenas (pinned + device)
   plans.clear();
   if (d_scratch) (void)hipFree(d_scratch);
@@ -122,6 +174,7 @@ int Context::init(int dev) {
   if (dev < 0 || dev >= n) return set_error(BFRS_E_NO_DEVICE, "HIP device id out of range");
   device = dev;
   if (const char *e = std::getenv("BFRS_PLAN_CACHE")) max_plans = std::max(1, atoi(e));
+  if (const char *e = std::getenv("BFRS_CODEC_SLOTS")) codec_cached = size_t(std::max(0, atoi(e)));
   HIP_TRY(hipSetDevice(dev));
   HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
   for (auto &ps : pipe_stream) HIP_TRY(hipStreamCreateWithFlags(&ps, hipStreamNonBlocking));

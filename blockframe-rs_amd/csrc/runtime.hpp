@@ -87,6 +87,19 @@ struct BlockIO {
   std::vector<uint8_t *> out;       // plan.coef.rows device pointers
 };
 
+// Device + pinned-host shard slots of the streaming codec objects
+// (bfrs_encoder / bfrs_decoder), each with its own stream so objects on
+// different threads overlap.  Cached per context (Context::codec_*), so an
+// encoder per block -- BlockFrame's pattern, generate.rs:84 -- allocates and
+// pins nothing after the first few blocks.
+struct CodecSlot {
+  void *d = nullptr;     // nshards x stride bytes of HBM
+  uint8_t *h = nullptr;  // nshards x stride bytes of pinned host memory
+  size_t stride = 0, nshards = 0;
+  hipStream_t stream = nullptr;
+  ~CodecSlot();
+};
+
 struct Context {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -121,6 +134,16 @@ struct Context {
   size_t d_hash_cap = 0;
   void *h_hash = nullptr;
   size_t h_hash_cap = 0;
+
+  // Codec-object slot cache: at most codec_cached idle slots are kept
+  // (BFRS_CODEC_SLOTS, default 2), which bounds a context's idle pinned +
+  // HBM footprint to 2 x (k + m) x shard_bytes each; slots beyond that are
+  // freed on release.  Any number of objects may be alive at once.
+  std::mutex codec_mu;
+  std::vector<std::unique_ptr<CodecSlot>> codec_free;
+  size_t codec_cached = 2;
+  int codec_acquire(size_t nshards, size_t shard_bytes, std::unique_ptr<CodecSlot> *out);
+  void codec_release(std::unique_ptr<CodecSlot> slot);
 
   ~Context();
   int init(int dev);

@@ -26,38 +26,17 @@ def _isa(src, tmp_path):
     return out.read_text().split("\n")
 
 
-def _sgpr_dest(line):
-    """SGPRs an instruction writes through its first operand (s7 or s[6:7]), else ()."""
-    m = re.match(r"\s*([sv]_\w+)\s+s(?:(\d+)|\[(\d+):(\d+)\])\s*,", line)
-    if not m:
-        return ()
-    if m.group(2) is not None:
-        return (int(m.group(2)),)
-    return tuple(range(int(m.group(3)), int(m.group(4)) + 1))
+def _gate():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("isa_gate",
+                                                  os.path.join(ROOT, "tools", "isa_gate.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
 
 
 def _hazards(lines, window=6):
-    """(line, VALU writer, VMEM) triples where a VALU instruction's SGPR result is
-    still the value a saddr VMEM instruction reads, fewer than `window`
-    instructions later with no s_nop between (an SMEM/SALU rewrite of the
-    register in between ends the hazard)."""
-    hits = []
-    for i, l in enumerate(lines):
-        m = re.search(r"global_(load|store)_dwordx\d+ .*?, s\[(\d+):(\d+)\]", l)
-        if not m:
-            continue
-        lo, hi = int(m.group(2)), int(m.group(3))
-        prev = [x for x in lines[max(0, i - 3 * window):i]
-                if x.strip() and not x.strip().startswith((";", "."))][-window:]
-        if any("s_nop" in x for x in prev):
-            continue
-        for r in range(lo, hi + 1):
-            for w in reversed(prev):  # the most recent writer of s<r> decides
-                if r in _sgpr_dest(w):
-                    if w.strip().startswith("v_"):
-                        hits.append((i, w.strip(), l.strip()))
-                    break
-    return hits
+    return _gate().sgpr_hazards(lines, window)
 
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
@@ -119,3 +98,45 @@ def test_inflight_checker_flags_a_copy():
     reuse = ["\t;;#ASMSTART", "\tglobal_load_dwordx4 v[10:13], v2, s[4:5]", "\t;;#ASMEND",
              "\tglobal_load_dwordx4 v[30:33], v11, s[4:5]", "\ts_endpgm"]
     assert len(ic.check(reuse)) == 1
+
+
+BROKEN_KERNEL = r"""
+#include <hip/hip_runtime.h>
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__global__ void broken(const uint8_t *base, uint32_t *out) {
+  u32x4 x;
+  const uint32_t off = threadIdx.x * 16;
+  asm volatile("global_load_dwordx4 %0, %1, %2" : "=&v"(x) : "v"(off), "s"(base) : "memory");
+  uint32_t y;
+  // uses a register of the load above as an address before any s_waitcnt
+  asm volatile("global_load_dword %0, %1, %2" : "=&v"(y) : "v"(x.x), "s"(base) : "memory");
+  asm volatile("s_waitcnt vmcnt(0)" : "+v"(y), "+v"(x) :: "memory");
+  out[threadIdx.x] = y + x.y;
+}
+"""
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+def test_build_gate_rejects_a_broken_kernel(tmp_path):
+    """the gate build() runs (Makefile -> tools/isa_gate.py)
+    fails on a kernel that uses an in-flight asm-load register as an address,
+    and passes the product kernels."""
+    import subprocess
+    import sys
+    src = tmp_path / "broken.hip"
+    src.write_text(BROKEN_KERNEL)
+    lst = tmp_path / "broken.s"
+    subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "--cuda-device-only", "-S", str(src),
+                    "-o", str(lst)], check=True, capture_output=True)
+    gate = os.path.join(ROOT, "tools", "isa_gate.py")
+    r = subprocess.run([sys.executable, gate, str(lst)], capture_output=True, text=True)
+    assert r.returncode == 1 and "in-flight" in r.stderr, r.stderr
+    ok = tmp_path / "blake3.s"
+    ok.write_text("\n".join(_isa(os.path.join(CSRC, "blake3_kernels.hip"), tmp_path)))
+    r = subprocess.run([sys.executable, gate, str(ok)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+
+
+def test_makefile_runs_the_gate():
+    mk = open(os.path.join(CSRC, "Makefile")).read()
+    assert "all: $(OUT) $(GATE)" in mk and "tools/isa_gate.py $(ISA)" in mk
