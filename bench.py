@@ -540,8 +540,9 @@ def pmc_traffic(alg_bytes):
     if rec.get("algorithmic_read_bytes", 0) + rec.get("algorithmic_write_bytes", 0) != alg_bytes:
         return None, None
     src = {"file": os.path.relpath(PMC_FILE, ROOT), "round": rec.get("round"),
-           "kernel": rec.get("kernel"), "how": rec.get("source"),
-           "ratio_to_algorithmic": rec.get("ratio_to_algorithmic")}
+           "box": rec.get("box"), "kernel": rec.get("kernel"), "how": rec.get("source"),
+           "ratio_to_algorithmic": rec.get("ratio_to_algorithmic"),
+           "rocprof_trace_mean_launch_ms": (rec.get("trace") or {}).get("mean_ms")}
     return rec.get("hbm_bytes_per_launch"), src
 
 
@@ -850,7 +851,11 @@ def main():
         line["encode_GiBps_per_gpu"] = round(data_bytes / 2**30 / (enc_ms * 1e-3), 2)
         line["decode_GiBps_per_gpu"] = round(data_bytes / 2**30 / (dec_ms * 1e-3), 2)
         line["roofline"] = {
-            "bound": "hbm", "kernel": "gf_apply_ring_kernel",
+            "bound": "hbm",
+            "kernel": ("gf_apply_unrolled_kernel (variant 76: unrolled SDWA-addressed GF(2^8)-"
+                       "subfield pass, contiguous-line nt loads)"
+                       if os.environ.get("BFRS_KERNEL_VARIANT", "76") == "76" else
+                       f"gf_apply (variant {os.environ.get('BFRS_KERNEL_VARIANT')})"),
             "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
             "traffic_source": traffic_src,
