@@ -255,8 +255,10 @@ CoefMatrix plan_decode(size_t k, size_t m, const std::vector<uint8_t> &orig_pres
     n = pow2_at_least(end);
     fft_trunc = k;
     erased.assign(n, 0);
+    // [k, c) holds the encoder's zero padding: a known zero, not an erasure
+    // (its product with the locator is zero either way, but an erased pad
+    // would spend c-k of the m correctable erasures)
     for (size_t i = 0; i < k; ++i) erased[i] = !orig_present[i];
-    for (size_t i = k; i < c; ++i) erased[i] = 1;
     for (size_t j = 0; j < m; ++j) erased[c + j] = !rec_present[j];
     for (size_t i = end; i < n; ++i) erased[i] = 1;
   }

@@ -40,6 +40,12 @@ int oracle_encode_engine(int engine, uint32_t k, uint32_t m, size_t shard_bytes,
 int oracle_decode_engine(int engine, uint32_t k, uint32_t m, size_t shard_bytes,
                          const uint8_t *const *originals, const uint8_t *const *recovery,
                          uint8_t *const *restored);
+/* rate: -1 DefaultRate, 0 LowRate, 1 HighRate (risk r2 fixtures only) */
+int oracle_encode_rate(int engine, int rate, uint32_t k, uint32_t m, size_t shard_bytes,
+                       const uint8_t *const *originals, uint8_t *const *recovery);
+int oracle_decode_rate(int engine, int rate, uint32_t k, uint32_t m, size_t shard_bytes,
+                       const uint8_t *const *originals, const uint8_t *const *recovery,
+                       uint8_t *const *restored);
 int oracle_batch(int engine, int decode, int threads, uint32_t nblocks, const uint32_t *k,
                  uint32_t m, size_t shard_bytes, const uint8_t *const *const *orig,
                  const uint8_t *const *const *rec, uint8_t *const *const *out);

@@ -37,6 +37,8 @@ def lib() -> ctypes.CDLL:
                                            ctypes.c_size_t, P, P]
         L.oracle_decode_engine.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32,
                                            ctypes.c_size_t, P, P, P]
+        L.oracle_encode_rate.argtypes = [ctypes.c_int] + L.oracle_encode_engine.argtypes
+        L.oracle_decode_rate.argtypes = [ctypes.c_int] + L.oracle_decode_engine.argtypes
         L.oracle_batch.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint32,
                                    ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32,
                                    ctypes.c_size_t, P, P, P]
@@ -72,19 +74,23 @@ def _as_u8(b):
     return a
 
 
-def encode(originals, m=3, engine=ENGINE_SCALAR):
-    """RS(k,m) encode of k equal-length shards -> list of m recovery arrays."""
+RATE_DEFAULT, RATE_LOW, RATE_HIGH = -1, 0, 1
+
+
+def encode(originals, m=3, engine=ENGINE_SCALAR, rate=RATE_DEFAULT):
+    """RS(k,m) encode of k equal-length shards -> list of m recovery arrays.
+    rate: DefaultRate (the crate's choice) or a forced Low/HighRate (r2 fixtures)."""
     orig = [_as_u8(o) for o in originals]
     k = len(orig)
     n = orig[0].size if k else 0
     rec = [np.zeros(n, dtype=np.uint8) for _ in range(m)]
-    rc = lib().oracle_encode_engine(engine, k, m, n, _ptrs(orig), _ptrs(rec))
+    rc = lib().oracle_encode_rate(engine, rate, k, m, n, _ptrs(orig), _ptrs(rec))
     if rc != 0:
         raise ValueError(f"oracle_encode rc={rc}")
     return rec
 
 
-def decode(originals, recovery, engine=ENGINE_SCALAR):
+def decode(originals, recovery, engine=ENGINE_SCALAR, rate=RATE_DEFAULT):
     """originals: k entries (None = missing); recovery: m entries (None = missing).
     Returns {index: restored array} for each missing original."""
     orig = [_as_u8(o) for o in originals]
@@ -96,7 +102,7 @@ def decode(originals, recovery, engine=ENGINE_SCALAR):
     outp = (ctypes.c_void_p * k)()
     for i, a in enumerate(out):
         outp[i] = None if a is None else a.ctypes.data
-    rc = lib().oracle_decode_engine(engine, k, m, n, _ptrs(orig), _ptrs(rec), outp)
+    rc = lib().oracle_decode_rate(engine, rate, k, m, n, _ptrs(orig), _ptrs(rec), outp)
     if rc != 0:
         raise ValueError(f"oracle_decode rc={rc}")
     return {i: a for i, a in enumerate(out) if a is not None}

@@ -374,12 +374,19 @@ static void encode_low(const work_t *w, uint32_t k, uint32_t m) {
   if (last) fft(w, p, c, last, p + c);
 }
 
-int oracle_encode_engine(int engine, uint32_t k, uint32_t m, size_t shard_bytes,
-                         const uint8_t *const *originals, uint8_t *const *recovery) {
+/* rate < 0: DefaultRate (oracle_use_high_rate); 0: LowRate; 1: HighRate.  The
+ * forced rates exist only to write the RS(3,3)/RS(4,3) fixtures of risk r2
+ * under both rates (tests/golden/make_golden.py). */
+static int pick_rate(int rate, uint32_t k, uint32_t m) {
+  return rate < 0 ? oracle_use_high_rate(k, m) : rate != 0;
+}
+
+int oracle_encode_rate(int engine, int rate, uint32_t k, uint32_t m, size_t shard_bytes,
+                       const uint8_t *const *originals, uint8_t *const *recovery) {
   int rc = check_args(k, m, shard_bytes);
   if (rc) return rc;
   ensure_tables();
-  int high = oracle_use_high_rate(k, m);
+  int high = pick_rate(rate, k, m);
   size_t count;
   if (high) {
     size_t c = next_pow2(m);
@@ -401,6 +408,11 @@ int oracle_encode_engine(int engine, uint32_t k, uint32_t m, size_t shard_bytes,
   return 0;
 }
 
+int oracle_encode_engine(int engine, uint32_t k, uint32_t m, size_t shard_bytes,
+                         const uint8_t *const *originals, uint8_t *const *recovery) {
+  return oracle_encode_rate(engine, -1, k, m, shard_bytes, originals, recovery);
+}
+
 int oracle_encode(uint32_t k, uint32_t m, size_t shard_bytes, const uint8_t *const *originals,
                   uint8_t *const *recovery) {
   return oracle_encode_engine(ORACLE_ENGINE_SCALAR, k, m, shard_bytes, originals, recovery);
@@ -409,9 +421,9 @@ int oracle_encode(uint32_t k, uint32_t m, size_t shard_bytes, const uint8_t *con
 /* Decode (A.4).  originals[i]/recovery[j] == NULL marks a missing shard.
  * restored[i] is written only for missing originals.  Mirrors the crate's
  * ReedSolomonDecoder: all received shards take part. */
-int oracle_decode_engine(int engine, uint32_t k, uint32_t m, size_t shard_bytes,
-                         const uint8_t *const *originals, const uint8_t *const *recovery,
-                         uint8_t *const *restored) {
+int oracle_decode_rate(int engine, int rate, uint32_t k, uint32_t m, size_t shard_bytes,
+                       const uint8_t *const *originals, const uint8_t *const *recovery,
+                       uint8_t *const *restored) {
   int rc = check_args(k, m, shard_bytes);
   if (rc) return rc;
   ensure_tables();
@@ -421,7 +433,7 @@ int oracle_decode_engine(int engine, uint32_t k, uint32_t m, size_t shard_bytes,
   if (orig_recv == k) return 0; /* nothing to restore */
   if (orig_recv + rec_recv < k) return ORACLE_E_NOT_ENOUGH_SHARDS;
 
-  int high = oracle_use_high_rate(k, m);
+  int high = pick_rate(rate, k, m);
   uint16_t *E = (uint16_t *)calloc(GF_ORDER, sizeof(uint16_t));
   if (!E) return ORACLE_E_NOMEM;
   work_t w;
@@ -466,9 +478,11 @@ int oracle_decode_engine(int engine, uint32_t k, uint32_t m, size_t shard_bytes,
       free(E);
       return ORACLE_E_NOMEM;
     }
+    /* originals' zero padding [k, c) is a known zero of the codeword (encode_low
+     * zero-fills it before the IFFT), so it is not an erasure: marking it
+     * would cost c-k of the m erasures the code corrects */
     for (uint32_t i = 0; i < k; ++i)
       if (!originals[i]) E[i] = 1;
-    for (size_t i = k; i < c; ++i) E[i] = 1;
     for (uint32_t j = 0; j < m; ++j)
       if (!recovery[j]) E[c + j] = 1;
     for (size_t i = rend; i < GF_ORDER; ++i) E[i] = 1;
@@ -497,6 +511,12 @@ int oracle_decode_engine(int engine, uint32_t k, uint32_t m, size_t shard_bytes,
   free(w.base);
   free(E);
   return 0;
+}
+
+int oracle_decode_engine(int engine, uint32_t k, uint32_t m, size_t shard_bytes,
+                         const uint8_t *const *originals, const uint8_t *const *recovery,
+                         uint8_t *const *restored) {
+  return oracle_decode_rate(engine, -1, k, m, shard_bytes, originals, recovery, restored);
 }
 
 int oracle_decode(uint32_t k, uint32_t m, size_t shard_bytes, const uint8_t *const *originals,

@@ -7,6 +7,7 @@ tests/test_oracle.py before these fixtures are trusted).
 
   python tests/golden/make_golden.py            # small vectors (seconds)
   python tests/golden/make_golden.py --large    # config-size digests (minutes)
+  python tests/golden/make_golden.py --r2       # RS(3,3)/RS(4,3) under both rates
 """
 import argparse
 import hashlib
@@ -30,6 +31,8 @@ SMALL_CASES = [
     (30, 3, 128), (30, 3, 64), (8, 3, 64), (20, 3, 192), (1, 3, 64), (2, 3, 128),
     (3, 3, 64), (4, 3, 64), (5, 3, 64), (29, 3, 64), (30, 3, 70), (7, 3, 2), (30, 3, 1000),
     (1, 3, 8000002 % 4096 + 2), (16, 4, 128), (10, 1, 64), (64, 3, 64), (65, 5, 128),
+    # LowRate with zero-padded originals (k not a power of two): round 2
+    (3, 5, 64), (7, 5, 128), (5, 9, 64),
 ]
 
 
@@ -94,12 +97,52 @@ def large(threads):
                    "synth": "blockframe-rs_amd/bfrs/synth.py splitmix64", **out}, f, indent=1)
 
 
+def r2():
+    """Risk r2 (SURVEY §7, A.4): which rate DefaultRate picks for k in {3, 4}
+    at m = 3 decides the parity bytes of a tier-3 file whose last block holds
+    3 or 4 segments.  No reference-held vector settles it, so these fixtures
+    carry BOTH rates' parity and decodes, labelled, plus the rate this build
+    chose (plan.cpp choose_rate): a run of the real crate on the same inputs
+    settles the question by matching exactly one of them."""
+    rng = np.random.default_rng(0x52)
+    cases = []
+    for k in (3, 4):
+        for n in (128, 70):
+            orig = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(k)]
+            # the bench's 3-erasure pattern: originals 0..2 missing
+            er = list(range(min(3, k)))
+            per = {}
+            for name, rate in (("low", O.RATE_LOW), ("high", O.RATE_HIGH)):
+                rec = O.encode(orig, 3, rate=rate)
+                o = [None if i in er else orig[i] for i in range(k)]
+                out = O.decode(o, rec, rate=rate)
+                assert all(np.array_equal(out[i], orig[i]) for i in er)
+                per[name] = {"recovery": [r.tobytes().hex() for r in rec]}
+            cases.append({
+                "k": k, "m": 3, "shard_bytes": n,
+                "originals": [x.tobytes().hex() for x in orig],
+                "erased": er,
+                "rates": per,
+                "this_build_default": "high" if O.use_high_rate(k, 3) else "low",
+            })
+    with open(os.path.join(HERE, "rs_r2.json"), "w") as f:
+        json.dump({"generator": "tests/golden/make_golden.py --r2",
+                   "rng": "numpy PCG64 seed 0x52",
+                   "label": "r2-dependent: parity of RS(3,3) and RS(4,3) under LowRate and HighRate; "
+                            "which one the reed-solomon-simd 3.1.0 DefaultRate produces is unpinned "
+                            "here (no crate, no reference vector)",
+                   "cases": cases}, f, indent=1)
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--large", action="store_true")
+    ap.add_argument("--r2", action="store_true")
     ap.add_argument("--threads", type=int, default=8)
     a = ap.parse_args()
     if a.large:
         large(a.threads)
+    elif a.r2:
+        r2()
     else:
         small()

@@ -1,5 +1,6 @@
 """CPU: the C-ABI library loads, exports exactly what include/bfrs.h declares,
 and its host-side planner reproduces the oracle (no GPU compute here)."""
+import itertools
 import json
 import os
 import re
@@ -100,6 +101,26 @@ def test_planner_decode_matrices_reproduce_oracle(bfrs, gf_tables):
                 assert a.tobytes().hex() == d["restored"][str(i)], (k, m, d["erased"])
             checked += 1
     assert checked >= 30
+
+
+@pytest.mark.parametrize("k,m", [(3, 5), (7, 5), (5, 9)])
+def test_planner_lowrate_padding_round_trip(bfrs, oracle, gf_tables, k, m):
+    """bfrs_plan_decode for LowRate shapes with zero-padded originals restores
+    every pattern of m erasures (the pad is a known zero, not an erasure)."""
+    exp, log = gf_tables
+    rng = np.random.default_rng(k + 16 * m)
+    data = [rng.integers(0, 256, 64, dtype=np.uint8) for _ in range(k)]
+    par = oracle.encode(data, m)
+    for er in itertools.islice(itertools.combinations(range(k + m), m), 0, 25):
+        op = [i not in er for i in range(k)]
+        rp = [(k + j) not in er for j in range(m)]
+        if all(op):
+            continue
+        mat = bfrs.plan_decode(k, m, op, rp)
+        inputs = [par[j] for j in range(m) if rp[j]] + [data[i] for i in range(k) if op[i]]
+        outs = apply_matrix(mat, inputs, exp, log)
+        for i, a in zip([i for i in range(k) if not op[i]], outs):
+            assert np.array_equal(a, data[i]), (k, m, er, i)
 
 
 def test_archive_entry_points_reject_null_arguments(bfrs):

@@ -46,6 +46,21 @@ def test_host_decode_golden(ctx, case):
         assert {str(i): a.tobytes().hex() for i, a in out.items()} == d["restored"]
 
 
+def test_r2_fixture_rate_invariant(ctx):
+    """RS(3,3)/RS(4,3) (a 3- or 4-segment last tier-3 block): the product's
+    parity equals the labelled LowRate AND HighRate fixture entries, which are
+    identical (tests/test_oracle.py::test_rates_agree_in_the_default_rate_tie),
+    and the 3-erasure decode restores the originals."""
+    g = json.load(open(os.path.join(GOLDEN, "rs_r2.json")))
+    for c in g["cases"]:
+        orig = [_np(h) for h in c["originals"]]
+        rec = [r.tobytes().hex() for r in ctx.encode(orig, c["m"])]
+        assert rec == c["rates"]["low"]["recovery"] == c["rates"]["high"]["recovery"]
+        o = [None if i in c["erased"] else orig[i] for i in range(c["k"])]
+        out = ctx.decode(o, [_np(h) for h in rec])
+        assert all(np.array_equal(out[i], orig[i]) for i in c["erased"])
+
+
 # ---------------------------------------------------------------- device batch API vs oracle
 def _dev_shards(arrs, dev="cuda"):
     return [torch.from_numpy(a.copy()).to(dev) for a in arrs]

@@ -126,6 +126,85 @@ def test_decode_all_erasure_patterns(oracle, k):
             assert np.array_equal(a, data[i]), (k, er, i)
 
 
+def _pow2(x):
+    p = 1
+    while p < x:
+        p <<= 1
+    return p
+
+
+@pytest.mark.parametrize("k,m", [(3, 3), (4, 3), (2, 2), (7, 5), (8, 8), (6, 8)])
+def test_rates_agree_in_the_default_rate_tie(oracle, k, m):
+    """Risk r2: DefaultRate's tie-break (next_pow2(k) == next_pow2(m)) picks
+    between two rates that give the SAME bytes: both place the k originals in
+    one coset of the size-c evaluation subspace and the m recovery shards in
+    the neighbouring one, and the additive FFT's translation invariance maps
+    one placement onto the other.  Encodes and decodes (including a decode of
+    a corrupted, non-codeword recovery shard) agree byte for byte, so the tie
+    rule cannot change BlockFrame's parity for a 3- or 4-segment last block."""
+    assert _pow2(k) == _pow2(m)
+    rng = np.random.default_rng(k * 100 + m)
+    data = [rng.integers(0, 256, 192, dtype=np.uint8) for _ in range(k)]
+    lo = oracle.encode(data, m, rate=oracle.RATE_LOW)
+    hi = oracle.encode(data, m, rate=oracle.RATE_HIGH)
+    assert all(np.array_equal(a, b) for a, b in zip(lo, hi))
+    bad = [r.copy() for r in lo]
+    bad[-1][::5] ^= 0x33
+    for er in itertools.islice(itertools.combinations(range(k), min(k, m)), 0, 20):
+        o = [None if i in er else data[i] for i in range(k)]
+        for rec in (lo, bad):
+            a = oracle.decode(o, rec, rate=oracle.RATE_LOW)
+            b = oracle.decode(o, rec, rate=oracle.RATE_HIGH)
+            assert all(np.array_equal(a[i], b[i]) for i in a), (er,)
+
+
+def test_rates_differ_outside_the_tie(oracle):
+    """The fixture above discriminates: off the tie the two rates' parity
+    differs (so agreement in the tie is a property, not a no-op)."""
+    rng = np.random.default_rng(9)
+    for k, m in ((2, 3), (5, 3), (30, 3), (3, 5)):
+        data = [rng.integers(0, 256, 64, dtype=np.uint8) for _ in range(k)]
+        lo = oracle.encode(data, m, rate=oracle.RATE_LOW)
+        hi = oracle.encode(data, m, rate=oracle.RATE_HIGH)
+        assert not all(np.array_equal(a, b) for a, b in zip(lo, hi)), (k, m)
+
+
+def test_r2_fixture_reproduces_under_both_rates(oracle):
+    """tests/golden/rs_r2.json (labelled r2-dependent) holds RS(3,3) and RS(4,3)
+    parity under LowRate and HighRate; the oracle reproduces both, and the
+    default rate's bytes are the labelled entry."""
+    g = json.load(open(os.path.join(GOLDEN, "rs_r2.json")))
+    assert "r2-dependent" in g["label"]
+    for c in g["cases"]:
+        orig = [np.frombuffer(bytes.fromhex(h), np.uint8) for h in c["originals"]]
+        for name, rate in (("low", oracle.RATE_LOW), ("high", oracle.RATE_HIGH)):
+            rec = oracle.encode(orig, c["m"], rate=rate)
+            assert [r.tobytes().hex() for r in rec] == c["rates"][name]["recovery"]
+        dflt = oracle.encode(orig, c["m"])
+        assert [r.tobytes().hex() for r in dflt] == c["rates"][c["this_build_default"]]["recovery"]
+
+
+@pytest.mark.parametrize("k,m", [(3, 5), (7, 5), (5, 9), (3, 6), (6, 16)])
+def test_lowrate_zero_padding_is_not_an_erasure(oracle, k, m):
+    """LowRate with k not a power of two zero-pads the originals to c; the pad
+    is a known zero of the codeword.  Every pattern of up to m erasures must
+    round-trip (round 1 marked the pad as erased and lost c-k of the m)."""
+    assert not oracle.use_high_rate(k, m) and _pow2(k) != k
+    rng = np.random.default_rng(k * 7 + m)
+    data = [rng.integers(0, 256, 128, dtype=np.uint8) for _ in range(k)]
+    par = oracle.encode(data, m)
+    for e in range(1, m + 1):
+        for er in itertools.islice(itertools.combinations(range(k + m), e), 0, 60):
+            o = [None if i in er else data[i] for i in range(k)]
+            if all(x is not None for x in o):
+                continue
+            r = [None if (k + j) in er else par[j] for j in range(m)]
+            if sum(x is not None for x in o + r) < k:
+                continue
+            for i, a in oracle.decode(o, r).items():
+                assert np.array_equal(a, data[i]), (k, m, er, i)
+
+
 def test_decode_not_enough_shards(oracle):
     data = [np.zeros(64, np.uint8) for _ in range(30)]
     par = oracle.encode(data, 3)
