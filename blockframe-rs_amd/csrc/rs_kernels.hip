@@ -794,215 +794,6 @@ __global__ __launch_bounds__(256, 5) void gf_apply_unrolled_kernel(const KernArg
     ring_tile_ct<1, 1, 6, false, 1, 1, true>(args, P, tile, wave_id, rot);
 }
 
-// ---- 8 symbols per lane (v86-v88, round 2 A/B) -------------------------------
-// The v76 lane owns 16 symbols, so its accumulators (32 VGPRs) and the
-// 3-deep ring of 2 KiB per input (24-32 VGPRs) cap it at 96 VGPRs = 5 waves
-// per SIMD, while the LDS lookups and the VALU are each ~88% busy: the
-// question is whether more waves overlap the two pipes better.  Here a wave
-// reads ONE 1 KiB run per input (16 chunks: lanes 0-31 the low halves, 32-63
-// the high halves, 16 B each) and two v_permlane32_swap (dwords 0<->2 and
-// 1<->3 across the lane halves) give every lane the low bytes (X0, X1) and
-// high bytes (X2, X3) of 8 symbols: lanes 0-31 symbols 0-7 of their 16-B
-// slice, lanes 32-63 symbols 8-15.  The same swaps map the transposed
-// outputs back to the stored layout.  WAVES waves per workgroup cover the
-// same 8 KiB tile as v76 (WAVES = 8), so the host's tiling is unchanged.
-__device__ __forceinline__ void quarter_swap(u32x4 &X) {
-  auto r = __builtin_amdgcn_permlane32_swap(X[0], X[2], false, false);
-  X[0] = r[0];
-  X[2] = r[1];
-  r = __builtin_amdgcn_permlane32_swap(X[1], X[3], false, false);
-  X[1] = r[0];
-  X[3] = r[1];
-}
-
-template <int N>
-__device__ __forceinline__ void vm_wait1(u32x4 &X) {
-  asm volatile("s_waitcnt vmcnt(%1)" : "+v"(X) : "n"(N) : "memory");
-}
-
-__device__ __forceinline__ void gload1_nt(u32x4 &X, uint64_t base, uint32_t off) {
-  asm volatile("global_load_dwordx4 %0, %1, %2 nt" : "=&v"(X) : "v"(off), "s"(base) : "memory");
-}
-
-template <int N>
-__device__ __forceinline__ void vm_wait1_n(u32x4 &X) {
-  if constexpr (N <= 0) vm_wait1<0>(X);
-  else if constexpr (N == 1) vm_wait1<1>(X);
-  else if constexpr (N == 2) vm_wait1<2>(X);
-  else if constexpr (N == 3) vm_wait1<3>(X);
-  else if constexpr (N == 4) vm_wait1<4>(X);
-  else if constexpr (N == 5) vm_wait1<5>(X);
-  else vm_wait1<6>(X);
-}
-
-// mac_slot for the 8-symbol lane: L = (X0, X1), H = (X2, X3).
-template <uint32_t SLOT>
-__device__ __forceinline__ void mac_slot8(const u32x4 &X, uint32_t mask, uint32_t (&acc_lo)[8],
-                                          uint32_t (&acc_hi)[8]) {
-  const AS_LDS uint8_t *t = (const AS_LDS uint8_t *)(uintptr_t)(SLOT * 512u);
-  const uint32_t l[2] = {X.x, X.y};
-  const uint32_t h[2] = {X.z, X.w};
-#pragma unroll
-  for (int d = 0; d < 2; ++d) {
-    uint64_t a[4], b[4];
-    uint2 e2[4], e3[4];
-#define BFRS_LOOKUPS8(K)                                                                 \
-  a[K] = *(const AS_LDS uint64_t *)(t + 256 + sdwa_lo_nib16<K>(l[d]));                   \
-  b[K] = *(const AS_LDS uint64_t *)(t + sdwa_hi_nib16<K>(l[d], mask));                   \
-  {                                                                                      \
-    const uint64_t v2 = *(const AS_LDS uint64_t *)(t + 256 + 8 + sdwa_lo_nib16<K>(h[d])); \
-    const uint64_t v3 = *(const AS_LDS uint64_t *)(t + 8 + sdwa_hi_nib16<K>(h[d], mask)); \
-    e2[K] = make_uint2(uint32_t(v2), uint32_t(v2 >> 32));                                \
-    e3[K] = make_uint2(uint32_t(v3), uint32_t(v3 >> 32));                                \
-  }
-#pragma unroll
-    for (int g = 0; g < 2; ++g) {
-      if (g == 0) {
-        BFRS_LOOKUPS8(0)
-        BFRS_LOOKUPS8(1)
-      } else {
-        BFRS_LOOKUPS8(2)
-        BFRS_LOOKUPS8(3)
-      }
-#pragma unroll
-      for (int k = 2 * g; k < 2 * g + 2; ++k) {
-        const int s = d * 4 + k;
-        const uint32_t lo2 = xor3_lo64(acc_lo[s], a[k], b[k]);
-        acc_lo[s] = xor3_ordered(lo2, e2[k].x, e3[k].x);
-        acc_hi[s] = xor3_ordered(acc_hi[s], e2[k].y, e3[k].y);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-#undef BFRS_LOOKUPS8
-  }
-}
-
-// In-place 4x4 byte transposes of acc[0..3] and acc[4..7] (transpose_outputs for 8).
-__device__ __forceinline__ void transpose_outputs8(uint32_t (&acc)[8]) {
-#pragma unroll
-  for (int d = 0; d < 2; ++d) {
-    uint32_t *a = acc + 4 * d;
-    const uint32_t x0 = __builtin_amdgcn_perm(a[1], a[0], 0x05010400u);
-    const uint32_t x1 = __builtin_amdgcn_perm(a[1], a[0], 0x07030602u);
-    const uint32_t y0 = __builtin_amdgcn_perm(a[3], a[2], 0x05010400u);
-    const uint32_t y1 = __builtin_amdgcn_perm(a[3], a[2], 0x07030602u);
-    a[0] = __builtin_amdgcn_perm(y0, x0, 0x05040100u);
-    a[1] = __builtin_amdgcn_perm(y0, x0, 0x07060302u);
-    a[2] = __builtin_amdgcn_perm(y1, x1, 0x05040100u);
-    a[3] = __builtin_amdgcn_perm(y1, x1, 0x07060302u);
-  }
-}
-
-template <int N, int D, uint32_t C>
-__device__ __forceinline__ void unrolled_step8(const uint64_t *in, uint32_t rot, uint32_t off,
-                                               uint32_t mask, u32x4 (&X)[N], uint32_t (&acc_lo)[8],
-                                               uint32_t (&acc_hi)[8]) {
-  if constexpr (C < uint32_t(N)) {  // issue input C
-    uint32_t src = rot + C;
-    src = src >= uint32_t(N) ? src - N : src;
-    gload1_nt(X[C], in[src], off);
-  }
-  if constexpr (C >= uint32_t(D) && C - D < uint32_t(N)) {  // consume input C - D
-    constexpr uint32_t c = C - D;
-    constexpr int after = (N - 1 - int(c)) < D ? (N - 1 - int(c)) : D;
-    vm_wait1_n<after>(X[c]);
-    u32x4 Y = X[c];
-    quarter_swap(Y);
-    mac_slot8<c>(Y, mask, acc_lo, acc_hi);
-  }
-}
-
-template <int N, int D, uint32_t... Cs>
-__device__ __forceinline__ void unrolled_ring8(const uint64_t *in, uint32_t rot, uint32_t off,
-                                               uint32_t mask, u32x4 (&X)[N], uint32_t (&acc_lo)[8],
-                                               uint32_t (&acc_hi)[8],
-                                               std::integer_sequence<uint32_t, Cs...>) {
-  (unrolled_step8<N, D, Cs>(in, rot, off, mask, X, acc_lo, acc_hi), ...);
-}
-
-template <int N, int WAVES, int D>
-__device__ __forceinline__ void tile_unrolled8(const KernArgs &args, const PassDesc &P,
-                                               uint32_t tile, uint32_t wave_id, uint32_t rot) {
-  const uint64_t wchunk0 = (uint64_t(tile) * WAVES + wave_id) * 16;
-  if (wchunk0 >= P.full_chunks) return;  // wave-uniform
-  const uint32_t l = threadIdx.x & 63;
-  const uint32_t slice = (l >> 5) * 32 + (l & 1) * 16;  // 16-B slice of the chunk
-  const bool ok = wchunk0 + ((l & 31) >> 1) < P.full_chunks;
-  // a lane past the last full chunk reads chunk 0 (never stored) so every
-  // lane takes part in the swaps
-  const uint32_t off = ok ? uint32_t(wchunk0 * 64) + ((l & 31) >> 1) * 64 + slice : slice;
-  const uint64_t *in = args.ptrs + P.in;
-  const uint32_t mask = __builtin_amdgcn_readfirstlane(0xF0u);
-  uint32_t acc_lo[8], acc_hi[8];
-#pragma unroll
-  for (int s = 0; s < 8; ++s) acc_lo[s] = acc_hi[s] = 0;
-  u32x4 X[N];
-  unrolled_ring8<N, D>(in, rot, off, mask, X, acc_lo, acc_hi,
-                       std::make_integer_sequence<uint32_t, N + D>{});
-  const uint32_t n_out = P.n_out;
-  const uint64_t *outp = args.ptrs + P.out;
-  const bool accumulate = P.accumulate != 0;
-  transpose_outputs8(acc_lo);
-  transpose_outputs8(acc_hi);
-#pragma unroll
-  for (uint32_t t = 0; t < kMaxPassOutputs; ++t) {
-    if (t >= n_out) break;
-    u32x4 Y = {acc_lo[t], acc_lo[4 + t], acc_hi[t], acc_hi[4 + t]};
-    quarter_swap(Y);
-    const uint64_t dst = outp[t];
-    if (accumulate && ok) {
-      const uint4 p = load16(dst + off);
-      Y ^= u32x4{p.x, p.y, p.z, p.w};
-    }
-    if (ok) store16_nt(dst + off, Y);
-  }
-}
-
-// stage_tables_rotated for NT threads.
-template <int NT>
-__device__ __forceinline__ void stage_tables_rotated_nt(const PassDesc &P, uint32_t rot) {
-  extern __shared__ __attribute__((aligned(16))) uint2 lds_table[];
-  const uint32_t n_in = P.n_in;
-  const AS_GLOBAL u32x4 *tab = (const AS_GLOBAL u32x4 *)(uintptr_t)P.table;
-  u32x4 *dst = reinterpret_cast<u32x4 *>(lds_table);
-  const uint32_t n16 = n_in * 32;
-  constexpr int R = int(kMaxPassInputs * 32 / NT);
-  u32x4 v[R];
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const uint32_t e = threadIdx.x + uint32_t(NT) * r;
-    v[r] = e < n16 ? tab[e] : u32x4{0, 0, 0, 0};
-  }
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const uint32_t e = threadIdx.x + uint32_t(NT) * r;
-    if (e < n16) {
-      const uint32_t i = e >> 5;
-      const uint32_t x = i >= rot ? i - rot : i + n_in - rot;
-      dst[x * 32 + (e & 31)] = v[r];
-    }
-  }
-  __syncthreads();
-}
-
-// Host contract: every pass subfield with n_in 30 or 8, tiles_per_wg == 1.
-template <int WAVES, int D, int MINB>
-__global__ __launch_bounds__(64 * WAVES, MINB) void gf_apply_unrolled8_kernel(const KernArgs args) {
-  constexpr int GL = 6, STEP = 4;
-  const uint32_t wg = xcd_group_remap<(1u << GL)>(blockIdx.x, gridDim.x);
-  const PassDesc &P = find_pass(args, wg);
-  const uint32_t tile = wg - P.wg_begin;
-  const uint32_t n_in = P.n_in;
-  const uint32_t rot = P.rotate ? ((tile >> GL) * STEP) % n_in : 0;
-  stage_tables_rotated_nt<64 * WAVES>(P, rot);
-  if (tile >= P.n_tiles) return;
-  const uint32_t wave_id = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (n_in == 30)
-    tile_unrolled8<30, WAVES, D>(args, P, tile, wave_id, rot);
-  else
-    tile_unrolled8<8, WAVES, D>(args, P, tile, wave_id, rot);
-}
-
 // Tail chunk (shard_bytes % 64 = tb != 0): tb/2 symbols, low bytes at
 // [base, base+tb/2), high bytes at [base+tb/2, base+tb) — the crate's tail rule.
 // One workgroup per pass, one lane per symbol; rare and tiny.
@@ -1070,34 +861,7 @@ hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in
                            hipStream_t stream) {
   if (n_wgs == 0) return hipSuccess;
   const size_t lds = size_t(max_in) * 64 * sizeof(uint2);
-  bool n30_8 = true;  // every pass 30 or 8 inputs (the 8-symbol variants' contract)
-  for (uint32_t p = 0; p < args.n_passes; ++p)
-    n30_8 = n30_8 && (args.passes[p].n_in == 30 || args.passes[p].n_in == 8);
-  const bool lane8 = subfield && args.tiles_per_wg == 1 && n30_8;
   switch (kernel_variant()) {
-    case 86:  // 8 symbols per lane, 8 waves per workgroup, 3 inputs in flight per wave
-    case 87:  // ... 4 inputs in flight
-    case 88:  // ... 5 inputs in flight
-    case 89:  // ... 6 inputs in flight
-      if (lane8) {
-        const int v = kernel_variant();
-        if (v == 86)
-          hipLaunchKernelGGL((gf_apply_unrolled8_kernel<8, 3, 4>), dim3(n_wgs), dim3(512), lds, stream, args);
-        else if (v == 87)
-          hipLaunchKernelGGL((gf_apply_unrolled8_kernel<8, 4, 4>), dim3(n_wgs), dim3(512), lds, stream, args);
-        else if (v == 88)
-          hipLaunchKernelGGL((gf_apply_unrolled8_kernel<8, 5, 4>), dim3(n_wgs), dim3(512), lds, stream, args);
-        else
-          hipLaunchKernelGGL((gf_apply_unrolled8_kernel<8, 6, 4>), dim3(n_wgs), dim3(512), lds, stream, args);
-        break;
-      }
-      if (subfield && args.tiles_per_wg == 1)
-        hipLaunchKernelGGL(gf_apply_unrolled_kernel<true>, dim3(n_wgs), dim3(256), lds, stream, args);
-      else if (subfield)
-        hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16, 1, 1, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
-      else
-        hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16, 1, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
-      break;
     case 5:
       hipLaunchKernelGGL((gf_apply_ring_kernel<0>), dim3(n_wgs), dim3(256), lds, stream, args);
       break;

@@ -155,7 +155,6 @@ Context::~Context() {
   codec_free.clear();
   staging.reset();  // archive staging arenas (pinned + device)
   plans.clear();
-  if (d_scratch) (void)hipFree(d_scratch);
   for (auto &ps : pipe_stream)
     if (ps) {
       (void)hipStreamSynchronize(ps);
@@ -178,21 +177,6 @@ int Context::init(int dev) {
   HIP_TRY(hipSetDevice(dev));
   HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
   for (auto &ps : pipe_stream) HIP_TRY(hipStreamCreateWithFlags(&ps, hipStreamNonBlocking));
-  return BFRS_OK;
-}
-
-int Context::scratch(size_t bytes, void **out) {
-  if (bytes > scratch_cap) {
-    if (d_scratch) {
-      HIP_TRY(hipStreamSynchronize(stream));
-      HIP_TRY(hipFree(d_scratch));
-      d_scratch = nullptr;
-      scratch_cap = 0;
-    }
-    HIP_TRY(hipMalloc(&d_scratch, bytes));
-    scratch_cap = bytes;
-  }
-  *out = d_scratch;
   return BFRS_OK;
 }
 

@@ -103,14 +103,10 @@ struct CodecSlot {
 struct Context {
   int device = 0;
   hipStream_t stream = nullptr;
-  std::mutex mu;  // guards the plan cache (contexts are single-threaded otherwise)
+  std::mutex mu;  // guards the plan cache (shared by every thread using the context)
   std::map<std::string, std::shared_ptr<Plan>> plans;
   uint64_t plan_tick = 0;
   size_t max_plans = 4096;  // BFRS_PLAN_CACHE overrides at bfrs_open (tests)
-
-  // Scratch device memory for the host-memory API.
-  void *d_scratch = nullptr;
-  size_t scratch_cap = 0;
 
   // Host-path pipeline: slots of device slab buffers, one stream each.
   // pipe_mu serialises run_host: archive prefetch threads, repair and the
@@ -163,7 +159,6 @@ struct Context {
   static constexpr size_t kMaxWindowBytes = size_t(1) << 31;
   int run_blocks(const std::vector<BlockIO> &blocks, size_t shard_bytes, hipStream_t stream);
   int run_window(const std::vector<BlockIO> &blocks, size_t shard_bytes, hipStream_t stream);
-  int scratch(size_t bytes, void **out);
   // Streams host-memory blocks through HBM (see bfrs_encode_host_batch).
   // orig/rec/out are per-block host pointer lists (decode: NULL = missing).
   int run_host(bool decode, size_t nblocks, const uint32_t *ks, size_t m, size_t shard_bytes,

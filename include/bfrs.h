@@ -16,12 +16,16 @@
  * the calling thread's last failure, using the reference's own strings where
  * the reference has them (src/filestore/recovery.rs:48,55,124,128,132,138).
  *
- * Threading: a context may be used by one thread at a time; distinct
- * contexts may be used concurrently (also on the same device), mirroring
- * rayon's one-encoder-per-block use at src/chunker/commit.rs:391-466.
- * Exceptions, serialised inside the library: the archive calls (commit,
- * repair, health check) and an open archive handle, whose prefetch threads
- * and readers share its context; a handle may be read from several threads.
+ * Threading: one context per device may be shared by all threads, which is
+ * how rayon's one-encoder-per-block use (src/chunker/commit.rs:391-466) maps
+ * onto it.  Encoder/decoder objects and the batch calls may run concurrently
+ * on one context: each codec object owns a pooled slot (device rows, pinned
+ * rows, its own HIP stream), the plan cache and the slot pool are locked, the
+ * host-batch pipeline and the BLAKE3 work area are serialised.  A single
+ * encoder or decoder object is used by one thread at a time (as the crate's
+ * &mut self API implies).  The archive calls (commit, repair, health check)
+ * and an open archive handle are serialised inside the library; a handle may
+ * be read from several threads.  Distinct contexts are independent.
  */
 #ifndef BFRS_H
 #define BFRS_H

@@ -279,6 +279,49 @@ def test_streaming_encoder_decoder(ctx, bfrs, oracle):
     assert dec.restored_original(1) is None  # crate: Option::None for present shards
 
 
+def test_codec_objects_share_one_context_across_threads(ctx, bfrs, oracle):
+    """rayon workers share ONE context per device.  Encoders
+    and decoders created concurrently on it (pooled codec slots, each with its
+    own stream; plan cache under the context lock) give the oracle's bytes."""
+    import threading
+    rng = np.random.default_rng(11)
+    n = 64 * 512 + 64
+    blocks = [[rng.integers(0, 256, n, dtype=np.uint8) for _ in range(k)] for k in (30, 8, 20, 30)]
+    want = [[r.tobytes() for r in oracle.encode(b, 3)] for b in blocks]
+    errors = []
+
+    def worker(w):
+        try:
+            for rep in range(3):
+                b = (w + rep) % len(blocks)
+                data = blocks[b]
+                enc = bfrs.ReedSolomonEncoder(ctx, len(data), 3, n)
+                for d in data:
+                    enc.add_original_shard(d)
+                rec = list(enc.encode().recovery_iter())
+                assert rec == want[b], (w, rep, b)
+                del enc
+                dec = bfrs.ReedSolomonDecoder(ctx, len(data), 3, n)
+                lost = {(w + rep) % len(data), (w + rep + 1) % len(data)}
+                for i, d in enumerate(data):
+                    if i not in lost:
+                        dec.add_original_shard(i, d)
+                for j in range(3):
+                    dec.add_recovery_shard(j, rec[j])
+                dec.decode()
+                for i in lost:
+                    assert dec.restored_original(i) == data[i].tobytes(), (w, rep, i)
+        except Exception as e:  # noqa: BLE001 - reported below
+            errors.append(repr(e))
+
+    ts = [threading.Thread(target=worker, args=(w,)) for w in range(6)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    assert not errors, errors
+
+
 def test_codec_argument_errors(ctx, bfrs):
     E = bfrs.BfrsError
     for args, code in (((30, 3, 0), bfrs.E_INVALID_SHARD_SIZE), ((30, 3, 63), bfrs.E_INVALID_SHARD_SIZE),
