@@ -303,6 +303,13 @@ def run_c4_strong(rt, ctx, args, stream_handle):
     _, t_dec = timed(rt, lambda: dec(stream_handle), steps)
     rt.sync()
     sets.check_restored()
+    pcie = None
+    if args.pcie == "auto" and not rt.stub:
+        # device-resident AND incl. pinned H2D/D2H; every
+        # rank streams its own stripes over its own PCIe link
+        pcie = pcie_inclusive(ctx, sets, steps=1, rt=rt, job_bytes=sum(shapes) * S_full)
+        pcie["note"] = ("whole-job GiB/s, max over ranks; each rank's stripes from pinned host "
+                        "buffers through bfrs_*_host_batch")
     if args.dump_dir:
         import numpy as np
         os.makedirs(args.dump_dir, exist_ok=True)
@@ -321,6 +328,7 @@ def run_c4_strong(rt, ctx, args, stream_handle):
         "value": round(2 * job * steps / 2**30 / (t_enc + t_dec), 2),
         "unit": "GiB/s",
         "ms_per_encode": round(t_enc / steps * 1e3, 4), "ms_per_decode": round(t_dec / steps * 1e3, 4),
+        "pcie_inclusive": pcie,
     }
     del sets
     return out
@@ -483,11 +491,12 @@ def crate_api(ctx, sets, reps=3):
     }
 
 
-def pcie_inclusive(ctx, sets, steps=2):
+def pcie_inclusive(ctx, sets, steps=2, rt=None, job_bytes=None):
     """The reference path starts and ends in host memory: time the same batch
     through bfrs_encode_host_batch / bfrs_decode_host_batch from pinned host
     buffers (H2D + kernel + D2H pipelined over 3 streams).  Reported beside
-    `value`, never as `value`."""
+    `value`, never as `value`.  With rt (c4_strong): every rank times its own
+    stripes between barriers and the job rate uses the max over ranks."""
     import torch
     shapes, S = sets.shapes, sets.S
     nseg, nb = sum(shapes), len(shapes)
@@ -504,22 +513,24 @@ def pcie_inclusive(ctx, sets, steps=2):
             dec_in_h.append(None if i in er else h_data[seg + i])
             dec_out_h.append(h_rest[3 * b + er.index(i)] if i in er else None)
         seg += k
-    ctx.encode_host_batch(shapes, 3, S, enc_in, enc_out)  # warm
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        ctx.encode_host_batch(shapes, 3, S, enc_in, enc_out)
-    t_enc = (time.perf_counter() - t0) / steps
-    ctx.decode_host_batch(shapes, 3, S, dec_in_h, enc_out, dec_out_h)
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        ctx.decode_host_batch(shapes, 3, S, dec_in_h, enc_out, dec_out_h)
-    t_dec = (time.perf_counter() - t0) / steps
+    def clock(call):
+        call()  # warm
+        if rt:
+            rt.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            call()
+        t = (time.perf_counter() - t0) / steps
+        return rt.max_over_ranks(t) if rt else t
+
+    t_enc = clock(lambda: ctx.encode_host_batch(shapes, 3, S, enc_in, enc_out))
+    t_dec = clock(lambda: ctx.decode_host_batch(shapes, 3, S, dec_in_h, enc_out, dec_out_h))
     seg = 0
     for b, k in enumerate(shapes):
         for t, i in enumerate(sets.erased[b]):
             assert torch.equal(h_rest[3 * b + t], h_data[seg + i]), "host-path decode mismatch"
         seg += k
-    gib = nseg * S / 2**30
+    gib = (job_bytes or nseg * S) / 2**30
     return {
         "encode_GiBps": round(gib / t_enc, 2), "decode_GiBps": round(gib / t_dec, 2),
         "encode_ms": round(t_enc * 1e3, 2), "decode_ms": round(t_dec * 1e3, 2),

@@ -42,6 +42,7 @@ E_HIP = -31
 E_NO_DEVICE = -32
 E_NOMEM = -33
 E_NOT_RESTORED = -34
+E_NOT_FOUND = -35
 
 # Every symbol include/bfrs.h declares (tests check the library exports them).
 EXPORTS = (
@@ -54,7 +55,8 @@ EXPORTS = (
     "bfrs_encode_batch_dev", "bfrs_decode_batch_dev", "bfrs_encode_host_batch",
     "bfrs_decode_host_batch", "bfrs_generate_parity",
     "bfrs_generate_parity_segmented", "bfrs_recover_segment_rs13", "bfrs_recover_segment_rs30_3",
-    "bfrs_blake3_hex", "bfrs_blake3_batch_dev", "bfrs_blake3_combine", "bfrs_merkle_root_hex", "bfrs_manifest_check", "bfrs_commit", "bfrs_repair", "bfrs_health_check", "bfrs_archive_open",
+    "bfrs_blake3_hex", "bfrs_blake3_batch_dev", "bfrs_blake3_combine", "bfrs_merkle_root_hex", "bfrs_manifest_check", "bfrs_commit", "bfrs_repair", "bfrs_health_check",
+    "bfrs_store_list", "bfrs_store_find", "bfrs_batch_health_check", "bfrs_archive_open",
     "bfrs_archive_size", "bfrs_archive_read", "bfrs_archive_stats_get", "bfrs_archive_close",
 )
 
@@ -174,6 +176,12 @@ def lib() -> ctypes.CDLL:
             "bfrs_health_check": ([_vp, ctypes.c_char_p, ctypes.c_char_p, _sz, ctypes.POINTER(_sz)],
                                   ctypes.c_int),
             "bfrs_repair": ([_vp, ctypes.c_char_p, ctypes.POINTER(RepairReport)], ctypes.c_int),
+            "bfrs_store_list": ([ctypes.c_char_p, ctypes.c_char_p, _sz, ctypes.POINTER(_sz)],
+                                ctypes.c_int),
+            "bfrs_store_find": ([ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, _sz,
+                                 ctypes.POINTER(_sz)], ctypes.c_int),
+            "bfrs_batch_health_check": ([_vp, ctypes.c_char_p, ctypes.c_char_p, _sz,
+                                         ctypes.POINTER(_sz)], ctypes.c_int),
             "bfrs_archive_open": ([_vp, ctypes.c_char_p, _sz, ctypes.c_int, ctypes.POINTER(_vp)],
                                   ctypes.c_int),
             "bfrs_archive_size": ([_vp, ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
@@ -635,6 +643,38 @@ def health_check(ctx: Context, archive_dir: str) -> dict:
     _check(lib().bfrs_health_check(ctx.handle, os.fsencode(archive_dir), out, len(out),
                                    ctypes.byref(need)))
     return json.loads(out.value.decode())
+
+
+def _json_call(f, *args) -> str:
+    """Two-call JSON output convention (*needed = length + 1)."""
+    need = _sz()
+    _check(f(*args, None, 0, ctypes.byref(need)))
+    out = ctypes.create_string_buffer(need.value)
+    _check(f(*args, out, len(out), ctypes.byref(need)))
+    return out.value.decode()
+
+
+class FileStore:
+    """FileStore's discovery over an archive root (src/filestore/mod.rs:81-154,
+    health.rs:45-74): get_all / find / batch_health_check."""
+
+    def __init__(self, store_path: str):
+        self.store_path = store_path
+
+    def get_all(self) -> list:
+        import json
+        return json.loads(_json_call(lib().bfrs_store_list, os.fsencode(self.store_path)))
+
+    def find(self, file_name: str) -> dict:
+        """The first archived file named file_name (with its archive "dir");
+        BfrsError(E_NOT_FOUND, "File '<name>' not found") otherwise."""
+        d = _json_call(lib().bfrs_store_find, os.fsencode(self.store_path), file_name.encode())
+        return next(f for f in self.get_all() if f["dir"] == d)
+
+    def batch_health_check(self, ctx: Context) -> dict:
+        import json
+        return json.loads(_json_call(lib().bfrs_batch_health_check, ctx.handle,
+                                     os.fsencode(self.store_path)))
 
 
 class Archive:

@@ -9,6 +9,7 @@
 // back to its in-block index; reads map offsets with `%`, not `&`
 // (filesystem_unix.rs:216), and tier-3 recovery decodes RS(k,3), not RS(1,3)
 // (:112-113).
+#include <dirent.h>
 #include <fcntl.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
@@ -902,10 +903,8 @@ int bfrs_repair(bfrs_ctx *ctx, const char *archive_dir, bfrs_repair_report *repo
 // but whose parity is not is Degraded (the reference tier-3 check only tests
 // existence, :363-411).  Report: JSON with HealthReport's fields
 // (src/filestore/models.rs:67-82) plus per-tier counts.
-int bfrs_health_check(bfrs_ctx *ctx, const char *archive_dir, char *json_out, size_t cap,
-                      size_t *needed) {
-  BFRS_API_BEGIN
-  if (!ctx || !archive_dir) return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_health_check: NULL argument");
+namespace {
+int health_report(bfrs_ctx *ctx, const char *archive_dir, Json *out) {
   Geometry g;
   int rc = load_geometry(archive_dir, &g);
   if (rc) return rc;
@@ -1000,13 +999,143 @@ int bfrs_health_check(bfrs_ctx *ctx, const char *archive_dir, char *json_out, si
       << degraded << " degraded, " << recoverable << " recoverable, " << unrecoverable
       << " unrecoverable";
   r["details"] = Json::str(det.str());
-  const std::string js = r.dump();
+  *out = std::move(r);
+  return BFRS_OK;
+}
+
+// JSON text into a caller buffer: *needed = length + 1, truncated copy.
+void put_json(const Json &j, char *json_out, size_t cap, size_t *needed) {
+  const std::string js = j.dump();
   if (needed) *needed = js.size() + 1;
   if (json_out && cap) {
     const size_t n = std::min(cap - 1, js.size());
     std::memcpy(json_out, js.data(), n);
     json_out[n] = 0;
   }
+}
+
+// FileStore::all_files + get_all (src/filestore/mod.rs:81-112): every entry of
+// the store root is taken as an archive directory whose manifest.json must
+// parse (the reference fails the whole listing otherwise).  read_dir order is
+// unspecified there; here entries are sorted by name.
+struct StoreFile {
+  std::string name, hash, manifest_path, dir;
+};
+int store_files(const char *root, std::vector<StoreFile> *out) {
+  DIR *d = opendir(root);
+  if (!d) return io_error(std::string("read_dir ") + root);
+  std::vector<std::string> entries;
+  while (const dirent *e = readdir(d)) {
+    const std::string n = e->d_name;
+    if (n != "." && n != "..") entries.push_back(n);
+  }
+  closedir(d);
+  std::sort(entries.begin(), entries.end());
+  for (const std::string &n : entries) {
+    StoreFile f;
+    f.dir = std::string(root) + "/" + n;
+    f.manifest_path = f.dir + "/manifest.json";
+    std::vector<uint8_t> text;
+    if (!read_file(f.manifest_path, &text)) return io_error("read manifest " + f.manifest_path);
+    Manifest mf;
+    std::string err;
+    if (!Manifest::from_json(std::string(text.begin(), text.end()), &mf, &err))
+      return set_error(BFRS_E_WRAPPER, f.manifest_path + ": " + err);
+    f.name = mf.name;
+    f.hash = mf.original_hash;
+    out->push_back(std::move(f));
+  }
+  return BFRS_OK;
+}
+
+Json file_json(const StoreFile &f) {
+  Json j = Json::obj(), data = Json::obj();
+  j["file_name"] = Json::str(f.name);
+  data["hash"] = Json::str(f.hash);
+  data["path"] = Json::str(f.manifest_path);
+  j["file_data"] = data;
+  j["dir"] = Json::str(f.dir);
+  return j;
+}
+}  // namespace
+
+int bfrs_health_check(bfrs_ctx *ctx, const char *archive_dir, char *json_out, size_t cap,
+                      size_t *needed) {
+  BFRS_API_BEGIN
+  if (!ctx || !archive_dir) return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_health_check: NULL argument");
+  Json r;
+  int rc = health_report(ctx, archive_dir, &r);
+  if (rc) return rc;
+  put_json(r, json_out, cap, needed);
+  return BFRS_OK;
+  BFRS_API_END
+}
+
+int bfrs_store_list(const char *store_root, char *json_out, size_t cap, size_t *needed) {
+  BFRS_API_BEGIN
+  if (!store_root) return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_store_list: NULL argument");
+  std::vector<StoreFile> files;
+  int rc = store_files(store_root, &files);
+  if (rc) return rc;
+  Json a = Json::arr();
+  for (const StoreFile &f : files) a.a.push_back(file_json(f));
+  put_json(a, json_out, cap, needed);
+  return BFRS_OK;
+  BFRS_API_END
+}
+
+int bfrs_store_find(const char *store_root, const char *file_name, char *dir_out, size_t cap,
+                    size_t *needed) {
+  BFRS_API_BEGIN
+  if (!store_root || !file_name)
+    return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_store_find: NULL argument");
+  std::vector<StoreFile> files;
+  int rc = store_files(store_root, &files);
+  if (rc) return rc;
+  for (const StoreFile &f : files)
+    if (f.name == file_name) {  // first match, as FileStore::find (mod.rs:137-146)
+      if (needed) *needed = f.dir.size() + 1;
+      if (dir_out && cap) {
+        const size_t n = std::min(cap - 1, f.dir.size());
+        std::memcpy(dir_out, f.dir.data(), n);
+        dir_out[n] = 0;
+      }
+      return BFRS_OK;
+    }
+  return set_error(BFRS_E_NOT_FOUND, std::string("File '") + file_name + "' not found");  // mod.rs:150-153
+  BFRS_API_END
+}
+
+int bfrs_batch_health_check(bfrs_ctx *ctx, const char *store_root, char *json_out, size_t cap,
+                            size_t *needed) {
+  BFRS_API_BEGIN
+  if (!ctx || !store_root)
+    return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_batch_health_check: NULL argument");
+  std::vector<StoreFile> files;
+  int rc = store_files(store_root, &files);
+  if (rc) return rc;
+  int64_t counts[4] = {0, 0, 0, 0};
+  static const char *kNames[] = {"Healthy", "Degraded", "Recoverable", "Unrecoverable"};
+  Json reports = Json::arr();
+  for (const StoreFile &f : files) {
+    Json r;
+    if ((rc = health_report(ctx, f.dir.c_str(), &r))) return rc;  // `?` in health.rs:53
+    const Json *st = r.get("status");
+    for (int i = 0; i < 4; ++i)
+      if (st && st->s == kNames[i]) ++counts[i];
+    Json pair = Json::arr();  // (String, HealthReport) serialises as a 2-array
+    pair.a.push_back(Json::str(f.name));
+    pair.a.push_back(std::move(r));
+    reports.a.push_back(std::move(pair));
+  }
+  Json b = Json::obj();
+  b["total_files"] = Json::num(int64_t(files.size()));
+  b["healthy"] = Json::num(counts[0]);
+  b["degraded"] = Json::num(counts[1]);
+  b["recoverable"] = Json::num(counts[2]);
+  b["unrecoverable"] = Json::num(counts[3]);
+  b["reports"] = std::move(reports);
+  put_json(b, json_out, cap, needed);
   return BFRS_OK;
   BFRS_API_END
 }

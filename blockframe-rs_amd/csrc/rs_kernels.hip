@@ -546,8 +546,8 @@ __global__ __launch_bounds__(256, 5) void gf_apply_ring_kernel(const KernArgs ar
 
 // ---- fully unrolled path (v76) ------------------------------------------------
 // For the pass sizes BlockFrame runs (n_in = 30: every full RS(30,3) block,
-// encode or 3-erasure decode; 8: the bench's last block), the input loop is
-// unrolled at compile time.  The table of the input consumed at step x then
+// encode or 3-erasure decode; 8 and 20: the last blocks of configs 2 and 4),
+// the input loop is unrolled at compile time.  The table of the input consumed at step x then
 // sits at a compile-time LDS offset (the workgroup stages its tables in its
 // own rotated read order: slot x <- input (rot + x) mod n_in), so a lookup
 // address is ONE SDWA op straight from the data byte -- no mask/shift prep,
@@ -771,7 +771,7 @@ __device__ __forceinline__ void stage_tables_rotated(const PassDesc &P, uint32_t
   __syncthreads();
 }
 
-// v76: unrolled SDWA-addressed path for n_in in {30, 8}, the looped
+// v76: unrolled SDWA-addressed path for n_in in {30, 20, 8}, the looped
 // subfield path (slot-indexed tables) for any other pass of the launch.
 // Host contract: every pass subfield, tiles_per_wg == 1.
 // GL: log2 of the read group (consecutive tiles sharing one starting input,
@@ -790,6 +790,8 @@ __global__ __launch_bounds__(256, 5) void gf_apply_unrolled_kernel(const KernArg
     tile_unrolled<30, 1, B64>(args, P, tile, wave_id, rot);
   else if (n_in == 8)
     tile_unrolled<8, 1, B64>(args, P, tile, wave_id, rot);
+  else if (n_in == 20)  // config 4's last block, RS(20,3)
+    tile_unrolled<20, 1, B64>(args, P, tile, wave_id, rot);
   else
     ring_tile_ct<1, 1, 6, false, 1, 1, true>(args, P, tile, wave_id, rot);
 }

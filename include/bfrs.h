@@ -60,6 +60,7 @@ enum {
   BFRS_E_NO_DEVICE = -32,        /* no usable gfx950 device / device id out of range */
   BFRS_E_NOMEM = -33,
   BFRS_E_NOT_RESTORED = -34,     /* restored_original(i): index was not restored (None) */
+  BFRS_E_NOT_FOUND = -35,        /* bfrs_store_find: no archived file of that name */
 };
 
 typedef struct bfrs_ctx bfrs_ctx;
@@ -265,6 +266,24 @@ int bfrs_repair(bfrs_ctx *ctx, const char *archive_dir, bfrs_repair_report *repo
  * details) plus corrupt_parity and per-unit counts; *needed = length + 1. */
 int bfrs_health_check(bfrs_ctx *ctx, const char *archive_dir, char *json_out, size_t cap,
                       size_t *needed);
+
+/* Archive discovery (FileStore, src/filestore/mod.rs:81-154, health.rs:45-74).
+ * Every entry of store_root is an archive directory {name}_{hash} whose
+ * manifest.json must parse (as FileStore::all_files/get_all; an unreadable
+ * one fails the call).  Entries are visited in name order.
+ * bfrs_store_list: JSON array of {"file_name", "file_data": {"hash", "path"
+ * (the manifest path)}, "dir"} (models.rs File).
+ * bfrs_store_find: the archive directory of the first file named file_name;
+ * BFRS_E_NOT_FOUND with "File '<name>' not found" otherwise (mod.rs:150-153).
+ * bfrs_batch_health_check: BatchHealthReport (models.rs:84-92) as JSON:
+ * total_files, healthy, degraded, recoverable, unrecoverable and reports =
+ * [[file_name, <bfrs_health_check report>], ...].
+ * Output convention as bfrs_health_check: *needed = length + 1. */
+int bfrs_store_list(const char *store_root, char *json_out, size_t cap, size_t *needed);
+int bfrs_store_find(const char *store_root, const char *file_name, char *dir_out, size_t cap,
+                    size_t *needed);
+int bfrs_batch_health_check(bfrs_ctx *ctx, const char *store_root, char *json_out, size_t cap,
+                            size_t *needed);
 
 /* Read-path core of the FUSE mount (src/mount/filesystem_unix.rs:176-305,
  * src/mount/cache.rs): offset->segment mapping, LRU segment cache,

@@ -349,6 +349,36 @@ def test_health_check_tier1_tier2(ctx, bfrs, tmp_path):
     assert len(h["missing_parity"]) == 3
 
 
+def test_batch_health_check_over_a_store(ctx, bfrs, tmp_path):
+    """FileStore::batch_health_check (health.rs:45-74) over an archive root
+    holding a tier-1, a tier-2 and a tier-3 file: counts by status and one
+    (name, report) pair per file."""
+    root = str(tmp_path / "archive")
+    p1, _ = _file(tmp_path, 3000, seed=31, name="one.bin")
+    a1 = bfrs.commit(ctx, p1, root)
+    p2, _ = _file(tmp_path, 2 * SEG + 5, seed=32, name="two.bin")
+    a2 = bfrs.commit(ctx, p2, root, segment_size=SEG, tier=2)
+    p3, _ = _file(tmp_path, 61 * SEG + 7, seed=33, name="three.bin")
+    a3 = bfrs.commit(ctx, p3, root, segment_size=SEG, tier=3)
+    store = bfrs.FileStore(root)
+    assert sorted(f["file_name"] for f in store.get_all()) == ["one.bin", "three.bin", "two.bin"]
+    assert store.find("three.bin")["dir"] == a3
+    b = store.batch_health_check(ctx)
+    assert (b["total_files"], b["healthy"], b["degraded"], b["recoverable"], b["unrecoverable"]) == (3, 3, 0, 0, 0)
+    _flip(os.path.join(a1, "parity_0.dat"))                              # tier 1: Degraded
+    _flip(os.path.join(a3, "blocks", "block_2", "segments", "segment_0.dat"))  # tier 3: Recoverable
+    for p in range(3):                                                     # tier 2: Unrecoverable
+        os.remove(os.path.join(a2, "parity", f"segment_0_parity_{p}.dat"))
+    os.remove(os.path.join(a2, "segments", "segment_0.dat"))
+    b = store.batch_health_check(ctx)
+    assert (b["total_files"], b["healthy"], b["degraded"], b["recoverable"], b["unrecoverable"]) == (3, 0, 1, 1, 1)
+    by_name = {name: rep for name, rep in b["reports"]}
+    assert by_name["one.bin"]["status"] == "Degraded"
+    assert by_name["two.bin"]["status"] == "Unrecoverable"
+    assert by_name["three.bin"]["corrupt_segments"] == ["block_2/segment_0.dat"]
+    assert by_name["three.bin"] == bfrs.health_check(ctx, a3)
+
+
 # ---------------------------------------------------------------- src/chunker/tests.rs, mirrored
 def _const_file(tmp_path, name, size, byte=None):
     # chunker/tests.rs:19-27: content = the name's first byte, repeated
