@@ -66,7 +66,7 @@ int bfrs_generate_parity(bfrs_ctx *ctx, const uint8_t *const *segments, const si
     size_t len;
     if ((rc = bfrs_encoder_recovery(enc.p, j, &data, &len))) return rc;
     if (!parity_out[j]) return set_error(BFRS_E_INVALID_ARGUMENT, "parity buffer is NULL");
-    std::memcpy(parity_out[j], data, len);
+    host_copy(parity_out[j], data, len);
   }
   return BFRS_OK;
   BFRS_API_END
@@ -127,7 +127,7 @@ int bfrs_recover_segment_rs13(bfrs_ctx *ctx, const uint8_t *const *parity,
   // recovery.rs:71-76 — truncate to Some(expected_size) if shorter
   if (expected_size != SIZE_MAX && len > expected_size) len = expected_size;
   if (!out) return set_error(BFRS_E_INVALID_ARGUMENT, "out is NULL");
-  std::memcpy(out, data, len);
+  host_copy(out, data, len);
   *out_len = len;
   return BFRS_OK;
   BFRS_API_END
@@ -176,7 +176,7 @@ int bfrs_recover_segment_rs30_3(bfrs_ctx *ctx, const uint8_t *const *segments,
   if (bfrs_decoder_restored_original(dec.p, target_index, &data, &len))
     return wrapper_error("Failed to restore target segment");
   if (!out) return set_error(BFRS_E_INVALID_ARGUMENT, "out is NULL");
-  std::memcpy(out, data, len);
+  host_copy(out, data, len);
   *out_len = len;
   return BFRS_OK;
   BFRS_API_END

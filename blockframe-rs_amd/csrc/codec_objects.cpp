@@ -29,25 +29,6 @@ int shard_size_error(size_t expected, size_t got) {
   return set_error(BFRS_E_DIFFERENT_SHARD_SIZE, os.str());
 }
 
-// Host copy into pinned memory: a few threads for large shards (one core
-// copies ~10-20 GB/s; the PCIe link takes ~50 GB/s).
-void copy_in(uint8_t *dst, const uint8_t *src, size_t n) {
-  constexpr size_t kPart = 8u << 20;
-  const size_t parts = std::min<size_t>(4, n / kPart);
-  if (parts < 2) {
-    std::memcpy(dst, src, n);
-    return;
-  }
-  const size_t per = (n / parts + 63) / 64 * 64;
-  std::thread th[4];
-  for (size_t t = 1; t < parts; ++t) {
-    const size_t a = t * per, b = std::min(n, a + per);
-    th[t] = std::thread([=] { std::memcpy(dst + a, src + a, b - a); });
-  }
-  std::memcpy(dst, src, std::min(n, per));
-  for (size_t t = 1; t < parts; ++t) th[t].join();
-}
-
 struct CodecObject {
   bfrs_ctx *ctx;
   size_t k, m, shard_bytes;
@@ -60,7 +41,7 @@ struct CodecObject {
     // the row's previous H2D (an earlier round on this object) must be done
     // before its pinned bytes are overwritten: rows are reused only after
     // encode()/decode() synchronised the stream, so no wait is needed here
-    copy_in(h_row(i), src, len);
+    host_copy(h_row(i), src, len);
     HIP_TRY(hipMemcpyAsync(d_row(i), h_row(i), len, hipMemcpyHostToDevice, slot->stream));
     return BFRS_OK;
   }

@@ -7,6 +7,7 @@
 #include "runtime.hpp"
 
 #include <algorithm>
+#include <thread>
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
@@ -105,6 +106,26 @@ CodecSlot::~CodecSlot() {
   }
   if (d) (void)hipFree(d);
   if (h) (void)hipHostFree(h);
+}
+
+// Host copy into pinned memory: up to 8 threads of >= 4 MiB for large shards
+// (one core copies ~10-20 GB/s from pageable memory; the PCIe link takes
+// ~50 GB/s, and the crate-shaped path is bound by these copies).
+void host_copy(uint8_t *dst, const uint8_t *src, size_t n) {
+  constexpr size_t kPart = 4u << 20, kMaxParts = 8;
+  const size_t parts = std::min<size_t>(kMaxParts, n / kPart);
+  if (parts < 2) {
+    std::memcpy(dst, src, n);
+    return;
+  }
+  const size_t per = (n / parts + 63) / 64 * 64;
+  std::thread th[kMaxParts];
+  for (size_t t = 1; t < parts; ++t) {
+    const size_t a = t * per, b = std::min(n, a + per);
+    th[t] = std::thread([=] { std::memcpy(dst + a, src + a, b - a); });
+  }
+  std::memcpy(dst, src, std::min(n, per));
+  for (size_t t = 1; t < parts; ++t) th[t].join();
 }
 
 int Context::codec_acquire(size_t nshards, size_t shard_bytes, std::unique_ptr<CodecSlot> *out) {

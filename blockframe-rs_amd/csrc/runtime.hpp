@@ -100,6 +100,9 @@ struct CodecSlot {
   ~CodecSlot();
 };
 
+// memcpy on up to 8 threads for large buffers (pageable <-> pinned staging).
+void host_copy(uint8_t *dst, const uint8_t *src, size_t n);
+
 struct Context {
   int device = 0;
   hipStream_t stream = nullptr;

@@ -16,7 +16,7 @@ for v in ${PMC_VARIANTS:-73}; do
   for set in "${SETS[@]}"; do
     i=$((i+1))
     BFRS_KERNEL_VARIANT=$v timeout -s KILL 90 rocprofv3 --pmc $set --output-format csv \
-        -d "$PWD/$OUT/pmc_${TAG}_v${v}_$i" -o pmc -- python3 tools/pmc_kernel.py --n 10 \
+        -d "$PWD/$OUT/pmc_${TAG}_v${v}_$i" -o pmc -- python3 tools/pmc_kernel.py --n ${PMC_N:-10} \
         > "$OUT/pmc_${TAG}_v${v}_$i.log" 2>&1
     rc=$?; echo "v$v pass $i ($set) rc=$rc"; [ $rc -eq 0 ] || exit $rc
   done

@@ -12,10 +12,10 @@ for v in ${VARIANTS:-}; do
   rc=$?; echo "variant $v parity rc=$rc: $(tail -1 "$OUT/pytest_v${v}_$TAG.log")"; [ $rc -eq 0 ] || exit $rc
 done
 if [ -n "${KB:-}" ]; then
-  timeout -k 10 300 python3 tools/kbench.py --variants "$KB" --stagger 12288 --rounds "${ROUNDS:-3}" --tpw "${TPW:-0}" \
+  timeout -k 10 300 python3 tools/kbench.py --variants "$KB" --stagger "${STAGGER:-12288}" --rounds "${ROUNDS:-3}" --tpw "${TPW:-0}" \
       --iters 10 > "$OUT/kb_${TAG}_enc.log" 2>&1
   rc=$?; echo "kbench enc rc=$rc"; [ $rc -eq 0 ] || exit $rc
-  timeout -k 10 300 python3 tools/kbench.py --decode --variants "$KB" --stagger 12288 \
+  timeout -k 10 300 python3 tools/kbench.py --decode --variants "$KB" --stagger "${STAGGER:-12288}" \
       --rounds "${ROUNDS:-3}" --tpw "${TPW:-0}" --segments "${SEGS:-128}" --iters 10 > "$OUT/kb_${TAG}_dec.log" 2>&1
   rc=$?; echo "kbench dec rc=$rc"; [ $rc -eq 0 ] || exit $rc
 fi

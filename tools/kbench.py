@@ -26,7 +26,9 @@ def main():
     ap.add_argument("--settle-ms", type=float, default=200.0,
                     help="untimed launches of the same config right before each timed run")
     ap.add_argument("--stagger", default="0",
-                    help="comma list: extra bytes between consecutive shards (row pitch S + x)")
+                    help="comma list: extra bytes between consecutive shards (row pitch S + x); "
+                         "suffix b = block-interleaved rows (each block's k data, 3 parity and "
+                         "3 restored rows consecutive in one buffer, as the archive arenas)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -41,12 +43,22 @@ def main():
         buf = torch.empty(n * pitch, dtype=torch.uint8, device="cuda")
         return [buf[i * pitch:i * pitch + S] for i in range(n)]
 
-    def build(stagger):
-        data = rows(a.segments, S + stagger)
+    def build(x):
+        stagger = int(x.rstrip("b"))
+        if x.endswith("b"):
+            allr = rows(sum(k + 6 for k in shapes), S + stagger)
+            data, par, rest, r = [], [], [], 0
+            for k in shapes:
+                data += allr[r:r + k]
+                par += allr[r + k:r + k + 3]
+                rest += allr[r + k + 3:r + k + 6]
+                r += k + 6
+        else:
+            data = rows(a.segments, S + stagger)
+            par = rows(3 * nb, S + stagger)
+            rest = rows(3 * nb, S + stagger)
         for s_ in range(a.segments):
             synth.fill_segment_torch(data[s_], 0xB10C, s_)
-        par = rows(3 * nb, S + stagger)
-        rest = rows(3 * nb, S + stagger)
         dec_in, dec_out, seg, erased = [], [], 0, []
         for b, k in enumerate(shapes):
             er = [1, k // 2, k - 1]
@@ -58,7 +70,7 @@ def main():
             seg += k
         return dict(data=data, par=par, rest=rest, dec_in=dec_in, dec_out=dec_out, erased=erased)
 
-    layouts = {int(x): build(int(x)) for x in a.stagger.split(",")}
+    layouts = {x: build(x) for x in a.stagger.split(",")}
     ctx = bfrs.Context(0)
     stream = torch.cuda.current_stream()
     alg = sum(k + 3 for k in shapes) * S
@@ -145,7 +157,7 @@ def main():
     out = {}
     for (v, t, x), ms in res.items():
         m = float(np.median(ms))
-        out[f"v{v}_tpw{t}" + (f"_stagger{x}" if x else "")] = {"ms": round(m, 4), "GBps": round(alg / m / 1e6, 1), "all_ms": [round(x, 4) for x in ms]}
+        out[f"v{v}_tpw{t}" + (f"_stagger{x}" if x != "0" else "")] = {"ms": round(m, 4), "GBps": round(alg / m / 1e6, 1), "all_ms": [round(x, 4) for x in ms]}
     cm = float(np.median(copy_ms))
     out["torch_copy_same_bytes"] = {"ms": round(cm, 4), "GBps": round(alg / cm / 1e6, 1)}
     print(json.dumps({"decode": a.decode, "alg_bytes": alg, **out}, indent=1))
