@@ -115,8 +115,8 @@ __device__ __forceinline__ uint32_t lane_off(uint32_t col0, uint32_t lane, int j
 // PRO = 1: the product kernel's prologue first (enter_pass: 30 inputs x 512 B
 // of nibble tables from a global buffer into LDS, then a barrier).
 
-template <int K, int O, int NL, int HC, int NTL, int NTS, int D, int XG, int PRO = 0>
-__global__ __launch_bounds__(256) void probe(Args a) {
+template <int K, int O, int NL, int HC, int NTL, int NTS, int D, int XG, int PRO = 0, int WAVES = 4>
+__global__ __launch_bounds__(64 * WAVES) void probe(Args a) {
   if constexpr (PRO) {
     extern __shared__ __attribute__((aligned(16))) u32x4 tab_lds[];
     const u32x4 *tab = (const u32x4 *)a.out;  // any resident bytes: 960 x 16 B
@@ -136,7 +136,7 @@ __global__ __launch_bounds__(256) void probe(Args a) {
   const uint32_t wg = XG ? xcd_remap16(blockIdx.x, gridDim.x) : blockIdx.x;
   const uint32_t blk = wg / a.tiles_per_block, tile = wg % a.tiles_per_block;
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint32_t col0 = (tile * 4 + wave) * NL * 1024;
+  const uint32_t col0 = (tile * WAVES + wave) * NL * 1024;
   const AS_CONST uint64_t *in = (const AS_CONST uint64_t *)(uintptr_t)(a.in + size_t(blk) * K);
   const uint32_t rot = K > 1 ? ((tile >> 4) * 4) % K : 0;
   u32x4 buf[K][NL];
@@ -317,19 +317,19 @@ void timeit(const char *name, F launch, double bytes) {
 
 // occ > 0: reserve 160 KiB / (occ) of LDS per 4-wave workgroup so at most
 // `occ` waves per SIMD run (the product kernel runs 5 at 96 VGPRs)
-template <int K, int O, int NL, int HC, int NTL, int NTS, int D, int XG, int PRO = 0>
+template <int K, int O, int NL, int HC, int NTL, int NTS, int D, int XG, int PRO = 0, int WAVES = 4>
 void run(const char *tag, int occ = 0) {
   constexpr uint32_t B = kShards / K;
-  const uint32_t wg_bytes = 4 * NL * 1024;
+  const uint32_t wg_bytes = WAVES * NL * 1024;
   Args a = make_args<K, O>(wg_bytes);
   const double bytes = double(kS) * B * (K + O);
   size_t lds = occ > 0 ? (size_t(160) << 10) / occ / 1024 * 1024 : 0;
   if (PRO && lds < 960 * 16) lds = 960 * 16;
   char name[160];
-  snprintf(name, sizeof name, "%s_k%d_o%d_nl%d_%s_ntl%d_nts%d_d%d_xg%d_occ%d_pro%d", tag, K, O, NL,
-           HC == 2 ? "ctperm" : HC ? "hc" : "ct", NTL, NTS, D, XG, occ, PRO);
-  timeit(name, [&] { hipLaunchKernelGGL((probe<K, O, NL, HC, NTL, NTS, D, XG, PRO>), dim3(a.total_tiles),
-                                         dim3(256), lds, 0, a); }, bytes);
+  snprintf(name, sizeof name, "%s_k%d_o%d_nl%d_%s_ntl%d_nts%d_d%d_xg%d_occ%d_pro%d_w%d", tag, K, O, NL,
+           HC == 2 ? "ctperm" : HC ? "hc" : "ct", NTL, NTS, D, XG, occ, PRO, WAVES);
+  timeit(name, [&] { hipLaunchKernelGGL((probe<K, O, NL, HC, NTL, NTS, D, XG, PRO, WAVES>), dim3(a.total_tiles),
+                                         dim3(64 * WAVES), lds, 0, a); }, bytes);
 }
 
 template <int K, int O, int NL, int NTL, int NTS, int D>
@@ -425,6 +425,15 @@ int main(int argc, char **argv) {
       run<30, 0, 2, 2, 1, 1, 2, 1>("rsro", 5);
       run<30, 3, 2, 0, 0, 1, 2, 1>("rs", 5);
       run<30, 3, 2, 2, 0, 1, 2, 1>("rs", 5);
+    }
+    if (all || !strcmp(only, "wg")) {
+      // per-wave vs per-workgroup contiguity at the product's settings (ct, nt
+      // loads + stores, 3 in flight, XCD grouping, 96-VGPR occupancy)
+      run<30, 3, 2, 0, 1, 1, 2, 1, 0, 4>("rs", 5);   // product: 2 KiB/wave, 8 KiB/WG
+      run<30, 3, 2, 0, 1, 1, 2, 1, 0, 8>("rs", 5);   // 2 KiB/wave, 16 KiB/WG
+      run<30, 3, 4, 0, 1, 1, 2, 1, 0, 4>("rs", 4);   // 4 KiB/wave, 16 KiB/WG
+      run<30, 3, 1, 0, 1, 1, 2, 1, 0, 8>("rs", 5);   // 1 KiB/wave, 8 KiB/WG
+      run<30, 3, 2, 0, 1, 1, 2, 1, 0, 16>("rs", 5);  // 2 KiB/wave, 32 KiB/WG
     }
     if (all || !strcmp(only, "mix")) {
       run<10, 1, 4, 0, 0, 1, 2, 1>("mix");
