@@ -416,23 +416,33 @@ def cpu_baseline(args, sets, info):
             assert all(np.array_equal(par[b][j], want[j]) for j in range(3)), "cpu parity check"
         for i in sets.erased[b]:
             assert np.array_equal(rest[b][i], blocks[b][i]), "cpu decode check"
-    # column stripes over all cores: 16 stripes per shard (64-B aligned)
-    nst = 16
-    sw = S // nst
-    ks, so, sr, sp, sd, sdo = [], [], [], [], [], []
-    for b, k in enumerate(shapes):
-        for t in range(nst):
-            sl = slice(t * sw, (t + 1) * sw)
-            ks.append(k)
-            so.append([blocks[b][i][sl] for i in range(k)])
-            sp.append([par[b][j][sl] for j in range(3)])
-            sd.append([None if x is None else x[sl] for x in dec_in[b]])
-            sdo.append([None if x is None else x[sl] for x in rest[b]])
-    t_e = run(threads, ks, so, [[None] * 3] * len(ks), sp, False)
-    t_d = run(threads, ks, sd, sp, sdo, True)
-    res["striped"] = {"threads": threads, "stripes_per_shard": nst,
-                      "encode_GiBps": round(data_gib / t_e, 3), "decode_GiBps": round(data_gib / t_d, 3),
-                      "value": round(2 * data_gib / (t_e + t_d), 3)}
+    # column stripes over all cores (64-B aligned)
+    def striped(nthreads, nst):
+        sw = S // nst
+        ks, so, sp, sd, sdo = [], [], [], [], []
+        for b, k in enumerate(shapes):
+            for t in range(nst):
+                sl = slice(t * sw, (t + 1) * sw)
+                ks.append(k)
+                so.append([blocks[b][i][sl] for i in range(k)])
+                sp.append([par[b][j][sl] for j in range(3)])
+                sd.append([None if x is None else x[sl] for x in dec_in[b]])
+                sdo.append([None if x is None else x[sl] for x in rest[b]])
+        t_e = run(nthreads, ks, so, [[None] * 3] * len(ks), sp, False)
+        t_d = run(nthreads, ks, sd, sp, sdo, True)
+        return {"threads": nthreads, "stripes_per_shard": nst,
+                "encode_GiBps": round(data_gib / t_e, 3), "decode_GiBps": round(data_gib / t_d, 3),
+                "value": round(2 * data_gib / (t_e + t_d), 3)}
+
+    res["striped"] = striped(threads, 16)
+    # T = nproc, as SURVEY 8(d) words it; on a box whose cgroup grants fewer
+    # CPUs than nproc this oversubscribes the quota (reported, not the value)
+    nproc = os.cpu_count() or threads
+    if nproc != threads:
+        nst = 16
+        while nst * nb < nproc and nst < 256:  # power-of-two stripes stay 64-B aligned
+            nst *= 2
+        res["striped_nproc_threads"] = striped(nproc, nst)
     # one core, one RS(30,3) block
     b0 = [blocks[0]]
     p0 = [[np.empty(S, np.uint8) for _ in range(3)]]
