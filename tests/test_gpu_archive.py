@@ -150,6 +150,29 @@ def test_commit_tier3_single_segment_last_block(ctx, bfrs, oracle, tmp_path):
     assert np.array_equal(got, oracle.encode([d[30 * SEG:]], 3, oracle.ENGINE_AVX2)[0])
 
 
+@pytest.mark.parametrize("last", [3, 4])
+def test_commit_tier3_r2_last_block(ctx, bfrs, oracle, tmp_path, last):
+    """Risk r2 end to end: a tier-3 file of 30 + `last` segments ends in an
+    RS(3,3) / RS(4,3) block, where DefaultRate's tie-break picks the rate.  The
+    parity files equal the oracle's under BOTH forced rates (identical bytes,
+    DESIGN §3), and a repair of 3 deleted segments of that block restores them."""
+    adir, d = _tier3(ctx, bfrs, tmp_path, nseg_full=30 + last - 1, tail=SEG // 2, seed=40 + last)
+    segs = _segments(d)[30:]
+    assert len(segs) == last
+    padded = [_pad(s, SEG) for s in segs]
+    for rate in (oracle.RATE_LOW, oracle.RATE_HIGH):
+        want = oracle.encode(padded, 3, rate=rate)
+        for p in range(3):
+            got = _read(os.path.join(adir, "blocks", "block_1", "parity", f"block_parity_{p}.dat"))
+            assert np.array_equal(got, want[p]), (rate, p)
+    for s in range(3):
+        os.remove(os.path.join(adir, "blocks", "block_1", "segments", f"segment_{s}.dat"))
+    assert bfrs.repair(ctx, adir)["segments_repaired"] == 3
+    for s in range(3):
+        got = _read(os.path.join(adir, "blocks", "block_1", "segments", f"segment_{s}.dat"))
+        assert np.array_equal(got, segs[s])
+
+
 def test_commit_auto_tier_and_overwrite(ctx, bfrs, tmp_path):
     path, d = _file(tmp_path, 4096, seed=5)
     a1 = bfrs.commit(ctx, path, str(tmp_path / "archive"))
