@@ -85,6 +85,23 @@ def test_exp8_subfield(oracle):
                                                            0x4e, 0x15, 0x56]
 
 
+def test_tower_identity_for_subfield_coefficients(oracle):
+    """SURVEY A.5, used by the subfield kernel form and DESIGN §10's cost
+    model: for c < 256 and x = L | H << 8,
+    c*x = (m8(c, L ^ G(H)) ^ G(m8(c, H))) | m8(c, H) << 8, with
+    G(h) = lo8((h << 8) ^ (h * 0x0100)) (whose high byte is 0)."""
+    mul = oracle.gf_mul
+    gamma = [((h << 8) ^ mul(h, 0x0100)) for h in range(256)]
+    assert all(g >> 8 == 0 for g in gamma)
+    rng = np.random.default_rng(5)
+    for c in [1, 0x0c, 0x0f, 0x0a, 0x08, 0x9b, 0xd6, 0xf8, 0xff] + rng.integers(2, 256, 8).tolist():
+        for x in rng.integers(0, 65536, 400).tolist() + [0, 0xFFFF, 0x0100, 0x00FF]:
+            L, H = x & 0xFF, x >> 8
+            hi = mul(c, H)
+            lo = mul(c, L ^ gamma[H]) ^ gamma[hi]
+            assert mul(c, x) == lo | hi << 8, (c, x)
+
+
 def test_cantor_basis_recurrence(oracle):
     basis = [0x0001, 0xACCA, 0x3C0E, 0x163E, 0xC582, 0xED2E, 0x914C, 0x4012, 0x6C98, 0x10D8,
              0x6A72, 0xB900, 0xFDB8, 0xFB34, 0xFF38, 0x991E]
