@@ -13,7 +13,7 @@ for f in sys.argv[1:]:
     per = collections.defaultdict(lambda: collections.defaultdict(float))
     dur = {}
     for r in csv.DictReader(open(f)):
-        if "gf_apply" not in r["Kernel_Name"] or int(r["Grid_Size"]) < 1000000:
+        if ("gf_apply" not in r["Kernel_Name"] and "gf_encode" not in r["Kernel_Name"]) or int(r["Grid_Size"]) < 1000000:
             continue
         per[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
         dur[r["Dispatch_Id"]] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
