@@ -68,11 +68,9 @@ uint32_t tile_bytes();
 int kernel_variant();
 
 // subfield: every pass of the launch has GF(2^8)-subfield coefficients
-// (PlanPass::subfield), so the subfield kernel form may run.  g30: every pass
-// is a whole RS(30,3) or RS(8,3) encode (G_30's first n_in columns, 3
-// outputs, no accumulate: PlanPass::g30), for the bit-sliced variant 96.
+// (PlanPass::subfield), so the subfield kernel form may run.
 hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in, bool subfield,
-                           bool g30, hipStream_t stream);
+                           hipStream_t stream);
 hipError_t launch_gf_tail(const KernArgs &args, hipStream_t stream);
 
 }  // namespace bfrs

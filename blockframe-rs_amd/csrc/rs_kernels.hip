@@ -796,147 +796,6 @@ __global__ __launch_bounds__(256, 5) void gf_apply_unrolled_kernel(const KernArg
     ring_tile_ct<1, 1, 6, false, 1, 1, true>(args, P, tile, wave_id, rot);
 }
 
-// ---- bit-sliced encode (v96, round 2 A/B) ---------------------
-// Encode launches whose every pass is the RS(30,3) / RS(8,3) encode matrix
-// (G_30 or its first 8 columns, PassDesc::g30): no LDS tables, the XOR
-// networks of bitslice_g30.inc (generated from plan.cpp by
-// tools/gen_bitslice.cpp).  A lane's 16 symbols become 8 packed planes:
-// Q[p] bit s = bit p of L_s (low half, s < 16) / of H_s (high half).
-// Source rows W[r] = (L_2r, L_2r+1, H_2r, H_2r+1) are 32x8 bit matrices
-// transposed by 3 delta swaps (row bit i <-> column bit i); the symbol order
-// inside a plane is whatever the swaps leave, undone by the same swaps.
-
-// x ^ (u >> 16): one SDWA op (src1 = the high half of u, zero-extended)
-__device__ __forceinline__ uint32_t bs_xor_hi(uint32_t x, uint32_t u) {
-  uint32_t r;
-  asm("v_xor_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1"
-      : "=v"(r)
-      : "v"(x), "v"(u));
-  return r;
-}
-
-#include "bitslice_g30.inc"
-
-// rows a (row bit i = 0) and b (= 1): swap a's columns with column bit i set
-// and b's with it clear (S = 2^i; M = columns with bit i clear)
-template <int S, uint32_t M>
-__device__ __forceinline__ void bs_delta(uint32_t &a, uint32_t &b) {
-  const uint32_t na = __builtin_amdgcn_bitop3_b32(M, a, b << S, 0xCA);  // M ? a : b<<S
-  const uint32_t nb = __builtin_amdgcn_bitop3_b32(M, a >> S, b, 0xCA);  // M ? a>>S : b
-  a = na;
-  b = nb;
-}
-
-__device__ __forceinline__ void bs_transpose(uint32_t (&W)[8]) {
-#pragma unroll
-  for (int r = 0; r < 8; r += 2) bs_delta<1, 0x55555555u>(W[r], W[r + 1]);
-#pragma unroll
-  for (int r = 0; r < 8; r += 4) {
-    bs_delta<2, 0x33333333u>(W[r], W[r + 2]);
-    bs_delta<2, 0x33333333u>(W[r + 1], W[r + 3]);
-  }
-#pragma unroll
-  for (int r = 0; r < 4; ++r) bs_delta<4, 0x0F0F0F0Fu>(W[r], W[r + 4]);
-}
-
-// L/H (4 dwords each, symbol s = byte s%4 of dword s/4) -> packed planes
-__device__ __forceinline__ void bs_planes(const u32x4 &L, const u32x4 &H, uint32_t (&Q)[8]) {
-#pragma unroll
-  for (int d = 0; d < 4; ++d) {
-    Q[2 * d] = __builtin_amdgcn_perm(H[d], L[d], 0x05040100u);      // L_4d, L_4d+1, H_4d, H_4d+1
-    Q[2 * d + 1] = __builtin_amdgcn_perm(H[d], L[d], 0x07060302u);  // L_4d+2, L_4d+3, H_.., H_..
-  }
-  bs_transpose(Q);
-}
-
-// packed planes -> L/H bytes (inverse of bs_planes)
-__device__ __forceinline__ void bs_bytes(uint32_t (&Q)[8], u32x4 &L, u32x4 &H) {
-  bs_transpose(Q);
-#pragma unroll
-  for (int d = 0; d < 4; ++d) {
-    L[d] = __builtin_amdgcn_perm(Q[2 * d + 1], Q[2 * d], 0x05040100u);
-    H[d] = __builtin_amdgcn_perm(Q[2 * d + 1], Q[2 * d], 0x07060302u);
-  }
-}
-
-// One ring step of the unrolled bit-sliced tile: issue input C, consume
-// input C - 3 (no read rotation: the input index must be a compile-time
-// constant to select its XOR network; a runtime switch over 30 networks in
-// the 4-way unrolled ring was outlined by the compiler into a call with
-// its accumulators in scratch).
-template <int N, uint32_t C>
-__device__ __forceinline__ void bs_step(const uint64_t *in, const CtLane &ln, u32x4 (&A)[N],
-                                        u32x4 (&B)[N], uint32_t (&acc)[24]) {
-  constexpr int D = 3;
-  if constexpr (C < uint32_t(N)) gload_ct<1>(A[C], B[C], in[C], ln.offA, ln.offB);
-  if constexpr (C >= uint32_t(D) && C - D < uint32_t(N)) {
-    constexpr uint32_t c = C - D;
-    constexpr int after = (N - 1 - int(c)) < D ? (N - 1 - int(c)) : D;
-    vm_wait_n<2 * after>(A[c], B[c]);
-    u32x4 L = A[c], H = B[c];
-    halves_swap(L, H);
-    uint32_t Q[8];
-    bs_planes(L, H, Q);
-    bs_gamma(Q);  // low halves: T = L ^ G(H)
-    bs_mac<c>(Q, acc);
-    // opaque per input: the IR reassociation pass would otherwise rebalance
-    // the 30 inputs' XOR chains into one tree and keep every partial live
-#pragma unroll
-    for (int r = 0; r < 24; ++r) asm volatile("" : "+v"(acc[r]));
-    __builtin_amdgcn_sched_barrier(0);
-  }
-}
-
-template <int N, uint32_t... Cs>
-__device__ __forceinline__ void bs_ring(const uint64_t *in, const CtLane &ln, u32x4 (&A)[N],
-                                        u32x4 (&B)[N], uint32_t (&acc)[24],
-                                        std::integer_sequence<uint32_t, Cs...>) {
-  (bs_step<N, Cs>(in, ln, A, B, acc), ...);
-}
-
-template <int N>
-__device__ __forceinline__ void bs_tile(const KernArgs &args, const PassDesc &P, uint32_t tile,
-                                        uint32_t wave_id) {
-  const uint64_t wchunk0 = (uint64_t(tile) * 4 + wave_id) * 32;
-  if (wchunk0 >= P.full_chunks) return;  // wave-uniform
-  const CtLane ln = ct_lane(wchunk0, P.full_chunks);
-  const uint64_t *in = args.ptrs + P.in;
-  uint32_t acc[24];
-#pragma unroll
-  for (int r = 0; r < 24; ++r) acc[r] = 0;
-  u32x4 A[N], B[N];
-  bs_ring<N>(in, ln, A, B, acc, std::make_integer_sequence<uint32_t, N + 3>{});
-  const uint64_t *outp = args.ptrs + P.out;
-#pragma unroll
-  for (uint32_t t = 0; t < 3; ++t) {
-    uint32_t Q[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) Q[q] = acc[8 * t + q];
-    bs_gamma(Q);  // lo_out ^= G(hi_out)
-    u32x4 ol, oh;
-    bs_bytes(Q, ol, oh);
-    halves_swap(ol, oh);
-    const uint64_t dst = outp[t];
-    if (ln.okA) store16_nt(dst + ln.offA, ol);
-    if (ln.okB) store16_nt(dst + ln.offB, oh);
-  }
-}
-
-// Host contract: every pass is an encode pass with PassDesc::g30 (inputs
-// 0..n_in-1 of G_30, n_in 30 or 8, 3 outputs, no accumulate), tiles_per_wg 1.
-template <int GL = 6, int MINB = 4>
-__global__ __launch_bounds__(256, MINB) void gf_encode_bitslice_kernel(const KernArgs args) {
-  const uint32_t wg = xcd_group_remap<(1u << GL)>(blockIdx.x, gridDim.x);
-  const PassDesc &P = find_pass(args, wg);
-  const uint32_t tile = wg - P.wg_begin;
-  if (tile >= P.n_tiles) return;
-  const uint32_t wave_id = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (P.n_in == 30)
-    bs_tile<30>(args, P, tile, wave_id);
-  else
-    bs_tile<8>(args, P, tile, wave_id);
-}
-
 // Tail chunk (shard_bytes % 64 = tb != 0): tb/2 symbols, low bytes at
 // [base, base+tb/2), high bytes at [base+tb/2, base+tb) — the crate's tail rule.
 // One workgroup per pass, one lane per symbol; rare and tiny.
@@ -1001,28 +860,10 @@ int kernel_variant() {
 uint32_t tile_bytes() { return kTileHalfChunks * 32; }
 
 hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in, bool subfield,
-                           bool g30, hipStream_t stream) {
+                           hipStream_t stream) {
   if (n_wgs == 0) return hipSuccess;
   const size_t lds = size_t(max_in) * 64 * sizeof(uint2);
   switch (kernel_variant()) {
-    case 97:  // 76 without the per-group read rotation (the A/B partner of 96)
-      if (subfield && args.tiles_per_wg == 1) {
-        hipLaunchKernelGGL((gf_apply_unrolled_kernel<true, 6, 0>), dim3(n_wgs), dim3(256), lds, stream, args);
-        break;
-      }
-      [[fallthrough]];
-    case 96:  // bit-sliced encode for the G_30 launches (no read rotation), else 76
-      if (g30 && args.tiles_per_wg == 1) {
-        hipLaunchKernelGGL(gf_encode_bitslice_kernel<>, dim3(n_wgs), dim3(256), 0, stream, args);
-        break;
-      }
-      if (subfield && args.tiles_per_wg == 1)
-        hipLaunchKernelGGL(gf_apply_unrolled_kernel<true>, dim3(n_wgs), dim3(256), lds, stream, args);
-      else if (subfield)
-        hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16, 1, 1, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
-      else
-        hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16, 1, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
-      break;
     case 5:
       hipLaunchKernelGGL((gf_apply_ring_kernel<0>), dim3(n_wgs), dim3(256), lds, stream, args);
       break;

@@ -80,13 +80,6 @@ static int upload_plan(Plan *p) {
             pp.subfield = false;
             break;
           }
-      {
-        static const CoefMatrix g30 = plan_encode(30, 3);
-        const size_t n = c1 - c0;
-        pp.g30 = r0 == 0 && r1 == 3 && c0 == 0 && c.rows == 3 && (n == 30 || n == 8);
-        for (size_t r = 0; r < 3 && pp.g30; ++r)
-          for (size_t cc = 0; cc < n && pp.g30; ++cc) pp.g30 = c.at(r, cc) == g30.at(r, cc);
-      }
       pp.r0 = uint32_t(r0);
       pp.r1 = uint32_t(r1);
       pp.c0 = uint32_t(c0);
@@ -393,7 +386,7 @@ int Context::run_window(const std::vector<BlockIO> &blocks, size_t shard_bytes,
       ka.n_passes = uint32_t(last - first);
       ka.tiles_per_wg = tpw;
       uint32_t pi = 0, wg = 0, max_in = 0;
-      bool subfield = true, g30 = true;
+      bool subfield = true;
       for (size_t it = first; it < last; ++it) {
         const BlockIO &b = *items[it].b;
         const PlanPass &p = *items[it].p;
@@ -407,7 +400,6 @@ int Context::run_window(const std::vector<BlockIO> &blocks, size_t shard_bytes,
         for (uint32_t r = p.r0; r < p.r1; ++r) ka.ptrs[pi++] = reinterpret_cast<uint64_t>(b.out[r]);
         d.table = reinterpret_cast<uint64_t>(p.d_table);
         subfield = subfield && p.subfield;
-        g30 = g30 && p.g30 && phase == 0;
         d.n_in = n_pad;
         d.n_out = p.r1 - p.r0;
         d.wg_begin = wg;
@@ -420,7 +412,7 @@ int Context::run_window(const std::vector<BlockIO> &blocks, size_t shard_bytes,
         wg += wgs_per_pass;
         max_in = std::max(max_in, n_pad);
       }
-      if (n_tiles) HIP_TRY(launch_gf_apply(ka, wg, max_in, subfield, g30, s));
+      if (n_tiles) HIP_TRY(launch_gf_apply(ka, wg, max_in, subfield, s));
       if (tail) HIP_TRY(launch_gf_tail(ka, s));
       first = last;
     }

@@ -65,9 +65,6 @@ struct PlanPass {
   // the products of a symbol's low byte then have a zero high byte, so the
   // kernel reads those table entries as 4 bytes and skips their high XORs
   bool subfield = false;
-  // the pass is G_30[:, 0:n] for n in {30, 8}: a whole RS(30,3) / RS(8,3)
-  // encode (the bit-sliced variant 96 has these matrices compiled in)
-  bool g30 = false;
 };
 
 // A coefficient plan for one (k, m, erasure pattern), tables on device.
