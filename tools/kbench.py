@@ -28,7 +28,8 @@ def main():
     ap.add_argument("--stagger", default="0",
                     help="comma list: extra bytes between consecutive shards (row pitch S + x); "
                          "suffix b = block-interleaved rows (each block's k data, 3 parity and "
-                         "3 restored rows consecutive in one buffer, as the archive arenas)")
+                         "3 restored rows consecutive in one buffer, as the archive arenas); "
+                         "suffix c = physically contiguous allocations (hipDeviceMallocContiguous)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -38,15 +39,38 @@ def main():
     S = synth.SEGMENT_SIZE
     shapes = synth.block_shapes(a.segments)
     nb = len(shapes)
-    def rows(n, pitch):
+    keep = []  # contiguous allocations stay alive for the whole run
+
+    def contiguous_buffer(nbytes):
+        """hipExtMallocWithFlags(hipDeviceMallocContiguous) wrapped as a torch
+        tensor: physically contiguous, so the row stagger maps onto HBM
+        channels the same way on every box (layout A/B, suffix c)."""
+        import ctypes
+        hip = ctypes.CDLL("libamdhip64.so")
+        ptr = ctypes.c_void_p()
+        rc = hip.hipExtMallocWithFlags(ctypes.byref(ptr), ctypes.c_size_t(nbytes), ctypes.c_uint(0x4))
+        if rc != 0:
+            raise RuntimeError(f"hipExtMallocWithFlags(contiguous, {nbytes}) = {rc}")
+
+        class CAI:
+            __cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1",
+                                        "data": (ptr.value, False), "version": 2}
+        t = torch.as_tensor(CAI(), device="cuda")
+        keep.append((hip, ptr))
+        return t
+
+    def rows(n, pitch, contiguous=False):
         """n shard views of S bytes, row i at byte i * pitch of one buffer."""
-        buf = torch.empty(n * pitch, dtype=torch.uint8, device="cuda")
+        buf = (contiguous_buffer(n * pitch) if contiguous
+               else torch.empty(n * pitch, dtype=torch.uint8, device="cuda"))
         return [buf[i * pitch:i * pitch + S] for i in range(n)]
 
     def build(x):
+        contig = x.endswith("c")
+        x = x.rstrip("c")
         stagger = int(x.rstrip("b"))
         if x.endswith("b"):
-            allr = rows(sum(k + 6 for k in shapes), S + stagger)
+            allr = rows(sum(k + 6 for k in shapes), S + stagger, contig)
             data, par, rest, r = [], [], [], 0
             for k in shapes:
                 data += allr[r:r + k]
@@ -54,9 +78,9 @@ def main():
                 rest += allr[r + k + 3:r + k + 6]
                 r += k + 6
         else:
-            data = rows(a.segments, S + stagger)
-            par = rows(3 * nb, S + stagger)
-            rest = rows(3 * nb, S + stagger)
+            data = rows(a.segments, S + stagger, contig)
+            par = rows(3 * nb, S + stagger, contig)
+            rest = rows(3 * nb, S + stagger, contig)
         for s_ in range(a.segments):
             synth.fill_segment_torch(data[s_], 0xB10C, s_)
         dec_in, dec_out, seg, erased = [], [], 0, []
