@@ -521,3 +521,35 @@ def test_constant_byte_shards(ctx, oracle, byte):
     rest = ctx.decode(o, want)
     for i in (0, 15, 29):
         assert np.array_equal(rest[i], d[i])
+
+
+def test_random_shapes_host_api_vs_oracle(ctx, oracle):
+    """Random (k, m), shard sizes with and without a tail chunk, random erasure
+    patterns (some with a corrupted recovery shard): the HIP path through
+    bfrs_encode / bfrs_decode gives the oracle's bytes.  Covers the looped
+    kernels (k not in {30, 20, 8}), both rates and multi-pass codes."""
+    rng = np.random.default_rng(0x5EED)
+    shapes = [(int(rng.integers(1, 48)), int(rng.integers(1, 9))) for _ in range(16)]
+    shapes += [(70, 3), (3, 6), (5, 9), (30, 3), (20, 3), (8, 3)]
+    for k, m in shapes:
+        if not oracle.lib().oracle_supported(k, m):
+            continue
+        n = int(rng.choice([64, 192, 4096 + 64, 8192 + 38, 130]))
+        data = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(k)]
+        want = oracle.encode(data, m)
+        rec = ctx.encode(data, m)
+        assert all(np.array_equal(a, b) for a, b in zip(rec, want)), (k, m, n)
+        e = int(rng.integers(1, min(k, m) + 1))
+        lost = sorted(rng.choice(k + m, size=e, replace=False).tolist())
+        if all(i >= k for i in lost):
+            lost[0] = 0
+        r = [None if (k + j) in lost else want[j].copy() for j in range(m)]
+        if any(x is not None for x in r) and rng.random() < 0.5:
+            j = next(j for j in range(m) if r[j] is not None)
+            r[j][::5] ^= 0x3C
+        o = [None if i in lost else data[i] for i in range(k)]
+        got = ctx.decode(o, r)
+        ref = oracle.decode(o, r)
+        assert sorted(got) == sorted(ref), (k, m, lost)
+        for i in ref:
+            assert np.array_equal(got[i], ref[i]), (k, m, n, lost, i)
