@@ -23,7 +23,9 @@
  * rows, its own HIP stream), the plan cache and the slot pool are locked, the
  * host-batch pipeline and the BLAKE3 work area are serialised.  A single
  * encoder or decoder object is used by one thread at a time (as the crate's
- * &mut self API implies).  The archive calls (commit, repair, health check)
+ * &mut self API implies).  A context keeps at most BFRS_CODEC_SLOTS idle codec
+ * slots (environment, read by bfrs_open; default 2): set it to the number of
+ * worker threads to keep their pinned + device rows across blocks.  The archive calls (commit, repair, health check)
  * and an open archive handle are serialised inside the library; a handle may
  * be read from several threads.  Distinct contexts are independent.
  */
