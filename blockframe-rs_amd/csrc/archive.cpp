@@ -903,6 +903,8 @@ int bfrs_repair(bfrs_ctx *ctx, const char *archive_dir, bfrs_repair_report *repo
 // but whose parity is not is Degraded (the reference tier-3 check only tests
 // existence, :363-411).  Report: JSON with HealthReport's fields
 // (src/filestore/models.rs:67-82) plus per-tier counts.
+}  // extern "C"
+
 namespace {
 int health_report(bfrs_ctx *ctx, const char *archive_dir, Json *out) {
   Geometry g;
@@ -1058,6 +1060,8 @@ Json file_json(const StoreFile &f) {
   return j;
 }
 }  // namespace
+
+extern "C" {
 
 int bfrs_health_check(bfrs_ctx *ctx, const char *archive_dir, char *json_out, size_t cap,
                       size_t *needed) {

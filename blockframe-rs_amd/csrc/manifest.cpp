@@ -255,9 +255,9 @@ bool read_str_array(const Json *j, std::vector<std::string> *out) {
 }  // namespace
 
 std::string Json::dump() const {
-  std::string s;
-  dump_to(*this, &s);
-  return s;
+  std::string out;
+  dump_to(*this, &out);
+  return out;
 }
 
 bool Json::parse(const std::string &text, Json *out, std::string *err) {
