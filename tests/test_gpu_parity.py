@@ -553,3 +553,30 @@ def test_random_shapes_host_api_vs_oracle(ctx, oracle):
         assert sorted(got) == sorted(ref), (k, m, lost)
         for i in ref:
             assert np.array_equal(got[i], ref[i]), (k, m, n, lost, i)
+
+
+def test_shards_larger_than_one_launch_window(ctx, oracle):
+    """Shards past the 2 GiB launch window (runtime.cpp kMaxWindowBytes: the
+    lane offsets are 32-bit) are processed in column windows: the
+    parity across the window edge and in the tail chunk equals the oracle's
+    on the same slices (the code acts per 64-byte chunk, so a chunk-aligned
+    slice is a shard of its own), and an erased shard decodes back whole."""
+    n = (2 << 30) + 4096 + 38  # two windows, the last one with a 38-byte tail chunk
+    k = 2
+    gen = torch.Generator(device="cuda").manual_seed(0x2B16)
+    data = [torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda", generator=gen)
+            for _ in range(k)]
+    par = [torch.empty(n, dtype=torch.uint8, device="cuda") for _ in range(3)]
+    ctx.encode_batch_dev([k], 3, n, data, par)
+    torch.cuda.synchronize()
+    edge = 2 << 30
+    for lo, hi in ((0, 8192), (edge - 4096, edge + 4096), (n - 38 - 128, n)):
+        want = oracle.encode([d[lo:hi].cpu().numpy() for d in data], 3)
+        for j in range(3):
+            assert np.array_equal(par[j][lo:hi].cpu().numpy(), want[j]), (lo, j)
+    out = torch.empty(n, dtype=torch.uint8, device="cuda")
+    ctx.decode_batch_dev([k], 3, n, [None, data[1]], par, [out, None])
+    torch.cuda.synchronize()
+    assert torch.equal(out, data[0])
+    del data, par, out
+    torch.cuda.empty_cache()
