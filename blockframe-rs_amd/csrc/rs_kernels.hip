@@ -7,9 +7,11 @@
 //
 // Data layout (crate's): a shard is a run of 64-byte chunks; chunk
 // c holds 32 symbols, low bytes at [64c, 64c+32), high bytes at [64c+32, 64c+64).
-// Work unit: one lane owns a 32-byte *half-chunk* = 16 symbols: 16 low bytes at
-// 64c + 16h and the matching 16 high bytes at 64c + 32 + 16h (h = half).  A
-// 256-lane workgroup tile covers 8 KiB of columns of every shard of a block.
+// Work unit: a lane owns 16 symbols (16 low + 16 high bytes).  A 256-lane
+// workgroup tile covers 8 KiB of columns of every shard of a block.  The
+// default kernel (v76, gf_apply_unrolled_kernel) loads whole 1 KiB lines per
+// instruction and regroups halves with v_permlane32_swap (ring_acc_ct); the
+// round-1 kernels load a lane's two 16-B halves directly (ring_acc_halfchunk).
 //
 // Arithmetic: multiplication of a 16-bit symbol by a constant is GF(2)-linear,
 // so coef*x = T0[x&15] ^ T1[(x>>4)&15] ^ T2[(x>>8)&15] ^ T3[x>>12] with 16-entry
@@ -17,7 +19,8 @@
 // outputs: low dword = the outputs' low bytes, high dword = their high bytes.
 // A 16-entry x 8-byte table spans 32 LDS banks, so a ds_read_b64 with any
 // nibble per lane is bank-conflict free.  Per symbol and input: 4 LDS lookups
-// and ~9.6 VALU, independent of the number of outputs (<= 4).
+// and, in v76 (GF(2^8)-subfield coefficients), 4 SDWA address ops + 3 XORs,
+// independent of the number of outputs (<= 4).  DESIGN.md §4.
 //
 // LDS table layout per input i (512 B, tab_idx in kernels.hpp): high-nibble
 // entries at i*512 + 16*v + 8*byte_hi, low-nibble entries at i*512 + 256 +
