@@ -155,6 +155,10 @@ class Runtime:
         if self.dist:
             self.dist.barrier()
 
+    def gather_over_ranks(self, x: float) -> list:
+        from bfrs import parallel
+        return parallel.gather_over_ranks(x, self.dist, device=self.coll_device)
+
     def max_over_ranks(self, x: float) -> float:
         from bfrs import parallel
         return parallel.max_over_ranks(x, self.dist, device=self.coll_device)
@@ -821,6 +825,7 @@ def main():
     elapsed = time.perf_counter() - t0  # this rank's K steps; the job time is the max over ranks
     rt.barrier()
     launch_ms = ev0.elapsed_time(ev1) / (2 * args.steps) if not rt.stub else None
+    rank_ms = [round(x / args.steps * 1e3, 4) for x in rt.gather_over_ranks(elapsed)]
     elapsed = rt.max_over_ranks(elapsed)
 
     enc_ms = dec_ms = copy_ms = None
@@ -882,6 +887,7 @@ def main():
         "settle": {"ms": args.settle_ms, "steps": settle_steps,
                    "note": "untimed clock-settle steps before the warmup"},
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "rank_ms_per_step": rank_ms,
         "higher_is_better": True,
         "scaling": scaling,
         "vs_baseline": None,

@@ -45,6 +45,17 @@ def max_over_ranks(value: float, dist=None, device=None) -> float:
     return float(t.item())
 
 
+def gather_over_ranks(value: float, dist=None, device=None) -> list:
+    """Every rank's float, in rank order (a one-element list without a process group)."""
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return [value]
+    import torch
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [float(x.item()) for x in out]
+
+
 def throughput(bytes_per_rank_per_step: float, world: int, steps: int, elapsed_max: float,
                scaling: str) -> float:
     """Whole-job GiB/s: weak = every rank processed its own bytes; strong = the
