@@ -580,3 +580,59 @@ def test_shards_larger_than_one_launch_window(ctx, oracle):
     assert torch.equal(out, data[0])
     del data, par, out
     torch.cuda.empty_cache()
+
+
+def test_mixed_entry_points_share_one_context_across_threads(ctx, bfrs, oracle):
+    """bfrs.h threading rule under a mixed load: host-API encodes/decodes (the
+    context's slab pipeline), crate-shaped codec objects (pooled slots) and
+    device-batch encodes on per-thread HIP streams, all at once on one
+    context, each result checked against the oracle."""
+    import threading
+    rng = np.random.default_rng(0x7C)
+    n = 64 * 1024 + 64
+    blocks = [[rng.integers(0, 256, n, dtype=np.uint8) for _ in range(k)] for k in (30, 8, 20, 5)]
+    want = [oracle.encode(b, 3) for b in blocks]
+    errors = []
+
+    def host_api(w):
+        for rep in range(3):
+            b = (w + rep) % len(blocks)
+            rec = ctx.encode(blocks[b], 3)
+            assert all(np.array_equal(x, y) for x, y in zip(rec, want[b])), ("host", b)
+            o = [None if i in (0, 2) else blocks[b][i] for i in range(len(blocks[b]))]
+            out = ctx.decode(o, rec)
+            assert np.array_equal(out[0], blocks[b][0]) and np.array_equal(out[2], blocks[b][2])
+
+    def codec_objects(w):
+        for rep in range(3):
+            b = (w + rep) % len(blocks)
+            enc = bfrs.ReedSolomonEncoder(ctx, len(blocks[b]), 3, n)
+            for d in blocks[b]:
+                enc.add_original_shard(d)
+            assert list(enc.encode().recovery_iter()) == [r.tobytes() for r in want[b]], ("obj", b)
+
+    def device_batch(w):
+        stream = torch.cuda.Stream()
+        with torch.cuda.stream(stream):
+            for rep in range(3):
+                b = (w + rep) % len(blocks)
+                d_in = [torch.from_numpy(x).to("cuda", non_blocking=False) for x in blocks[b]]
+                d_out = [torch.empty(n, dtype=torch.uint8, device="cuda") for _ in range(3)]
+                ctx.encode_batch_dev([len(blocks[b])], 3, n, d_in, d_out, stream=stream)
+                stream.synchronize()
+                for j in range(3):
+                    assert np.array_equal(d_out[j].cpu().numpy(), want[b][j]), ("dev", b, j)
+
+    def run(f, w):
+        try:
+            f(w)
+        except Exception as e:  # noqa: BLE001 - reported below
+            errors.append(f"{f.__name__}[{w}]: {e!r}")
+
+    ts = [threading.Thread(target=run, args=(f, w))
+          for w in range(2) for f in (host_api, codec_objects, device_batch)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=180)
+    assert not errors, errors
