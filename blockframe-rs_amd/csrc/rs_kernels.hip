@@ -779,19 +779,9 @@ __device__ __forceinline__ void stage_tables_rotated(const PassDesc &P, uint32_t
 // Host contract: every pass subfield, tiles_per_wg == 1.
 // GL: log2 of the read group (consecutive tiles sharing one starting input,
 // placed on one XCD); STEP: how far consecutive groups' starting inputs move.
-// IL (A/B): read groups of consecutive workgroups cycle over the launch's
-// passes (blocks) instead of covering pass 0 first, when every pass has the
-// same tile count, a multiple of the group (the same shard size: always).
-template <bool B64, int GL = 6, int STEP = 4, bool IL = false>
+template <bool B64, int GL = 6, int STEP = 4>
 __global__ __launch_bounds__(256, 5) void gf_apply_unrolled_kernel(const KernArgs args) {
-  uint32_t wg = xcd_group_remap<(1u << GL)>(blockIdx.x, gridDim.x);
-  if constexpr (IL) {
-    const uint32_t np = args.n_passes, nt = args.passes[0].n_tiles;
-    if (np > 1 && nt % (1u << GL) == 0 && wg < np * nt) {
-      const uint32_t gi = wg >> GL;
-      wg = (gi % np) * nt + (gi / np << GL) + (wg & ((1u << GL) - 1));
-    }
-  }
+  const uint32_t wg = xcd_group_remap<(1u << GL)>(blockIdx.x, gridDim.x);
   const PassDesc &P = find_pass(args, wg);
   const uint32_t tile = wg - P.wg_begin;
   const uint32_t n_in = P.n_in;
@@ -916,12 +906,6 @@ hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in
       else
         hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16, 1, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
       break;
-    case 84:  // 76 with read groups cycling over the blocks of the launch
-      if (subfield && args.tiles_per_wg == 1) {
-        hipLaunchKernelGGL((gf_apply_unrolled_kernel<true, 6, 4, true>), dim3(n_wgs), dim3(256), lds, stream, args);
-        break;
-      }
-      [[fallthrough]];
     case 78:  // 76 with read groups of 16 tiles (the round-1 grouping)
     case 79:  // 76 with read groups of 32 tiles
     case 80:  // 76 with read groups of 128 tiles
