@@ -799,35 +799,6 @@ __global__ __launch_bounds__(256, 5) void gf_apply_unrolled_kernel(const KernArg
     ring_tile_ct<1, 1, 6, false, 1, 1, true>(args, P, tile, wave_id, rot);
 }
 
-// ---- persistent lockstep (v85, round 2 A/B) -----------------------------------
-// A resident grid walks the tiles in order (tile w, w + grid, ...), every
-// tile reading its inputs in the same order (no rotation): the resident
-// workgroups start together and stream input x of ~1,280 consecutive tiles
-// (~10 MiB of one shard) at about the same time, the most sequential read
-// order this pass allows.  Tables are re-staged per tile (a barrier first:
-// the previous tile's lookups must be done).
-template <bool B64>
-__global__ __launch_bounds__(256, 5) void gf_apply_persistent_kernel(const KernArgs args,
-                                                                     uint32_t total) {
-  const uint32_t wave_id = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  for (uint32_t w = blockIdx.x; w < total; w += gridDim.x) {
-    const PassDesc &P = find_pass(args, w);
-    const uint32_t tile = w - P.wg_begin;
-    __syncthreads();
-    stage_tables_rotated(P, 0);
-    if (tile >= P.n_tiles) continue;  // workgroup-uniform
-    const uint32_t n_in = P.n_in;
-    if (n_in == 30)
-      tile_unrolled<30, 1, B64>(args, P, tile, wave_id, 0);
-    else if (n_in == 8)
-      tile_unrolled<8, 1, B64>(args, P, tile, wave_id, 0);
-    else if (n_in == 20)
-      tile_unrolled<20, 1, B64>(args, P, tile, wave_id, 0);
-    else
-      ring_tile_ct<1, 1, 6, false, 1, 1, true>(args, P, tile, wave_id, 0);
-  }
-}
-
 // Tail chunk (shard_bytes % 64 = tb != 0): tb/2 symbols, low bytes at
 // [base, base+tb/2), high bytes at [base+tb/2, base+tb) — the crate's tail rule.
 // One workgroup per pass, one lane per symbol; rare and tiny.
@@ -935,22 +906,6 @@ hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in
       else
         hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16, 1, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
       break;
-    case 85:  // persistent lockstep grid (no rotation)
-      if (subfield && args.tiles_per_wg == 1) {
-        static int grid = 0;
-        if (!grid) {
-          int per_cu = 0, cus = 0, dev = 0;
-          (void)hipGetDevice(&dev);
-          (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-          (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gf_apply_persistent_kernel<true>,
-                                                             256, lds);
-          grid = std::max(1, per_cu) * std::max(1, cus);
-        }
-        hipLaunchKernelGGL(gf_apply_persistent_kernel<true>, dim3(std::min<uint32_t>(n_wgs, uint32_t(grid))),
-                           dim3(256), lds, stream, args, n_wgs);
-        break;
-      }
-      [[fallthrough]];
     case 78:  // 76 with read groups of 16 tiles (the round-1 grouping)
     case 79:  // 76 with read groups of 32 tiles
     case 80:  // 76 with read groups of 128 tiles
