@@ -779,16 +779,13 @@ __device__ __forceinline__ void stage_tables_rotated(const PassDesc &P, uint32_t
 // Host contract: every pass subfield, tiles_per_wg == 1.
 // GL: log2 of the read group (consecutive tiles sharing one starting input,
 // placed on one XCD); STEP: how far consecutive groups' starting inputs move.
-// NG (A/B): starting inputs cycle over NG values only (group g starts at
-// input (g mod NG) * STEP): fewer distinct shards in flight at once.
-template <bool B64, int GL = 6, int STEP = 4, int NG = 0>
+template <bool B64, int GL = 6, int STEP = 4>
 __global__ __launch_bounds__(256, 5) void gf_apply_unrolled_kernel(const KernArgs args) {
   const uint32_t wg = xcd_group_remap<(1u << GL)>(blockIdx.x, gridDim.x);
   const PassDesc &P = find_pass(args, wg);
   const uint32_t tile = wg - P.wg_begin;
   const uint32_t n_in = P.n_in;
-  const uint32_t g = NG > 0 ? (tile >> GL) % uint32_t(NG) : (tile >> GL);
-  const uint32_t rot = P.rotate ? (g * STEP) % n_in : 0;  // read order of v41/v58
+  const uint32_t rot = P.rotate ? ((tile >> GL) * STEP) % n_in : 0;  // read order of v41/v58
   stage_tables_rotated(P, rot);
   if (tile >= P.n_tiles) return;
   const uint32_t wave_id = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -909,20 +906,6 @@ hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in
       else
         hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16, 1, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
       break;
-    case 86:  // 76 with starting inputs cycling over 8 values (one per XCD of a run)
-    case 87:  // ... 4 values, 8 inputs apart
-    case 88:  // ... 16 values, 2 inputs apart
-      if (subfield && args.tiles_per_wg == 1) {
-        const int v = kernel_variant();
-        if (v == 86)
-          hipLaunchKernelGGL((gf_apply_unrolled_kernel<true, 6, 4, 8>), dim3(n_wgs), dim3(256), lds, stream, args);
-        else if (v == 87)
-          hipLaunchKernelGGL((gf_apply_unrolled_kernel<true, 6, 8, 4>), dim3(n_wgs), dim3(256), lds, stream, args);
-        else
-          hipLaunchKernelGGL((gf_apply_unrolled_kernel<true, 6, 2, 16>), dim3(n_wgs), dim3(256), lds, stream, args);
-        break;
-      }
-      [[fallthrough]];
     case 78:  // 76 with read groups of 16 tiles (the round-1 grouping)
     case 79:  // 76 with read groups of 32 tiles
     case 80:  // 76 with read groups of 128 tiles
