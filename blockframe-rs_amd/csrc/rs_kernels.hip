@@ -799,57 +799,6 @@ __global__ __launch_bounds__(256, 5) void gf_apply_unrolled_kernel(const KernArg
     ring_tile_ct<1, 1, 6, false, 1, 1, true>(args, P, tile, wave_id, rot);
 }
 
-// ---- 512-lane workgroups over two tiles (v89, round 2 A/B) ---------------------
-// membench8 (r02z): a 16 KiB workgroup run (8 waves x 2 KiB) streams 1.3%
-// faster than 8 KiB.  Host grid tiles_per_wg = 2; waves 0-3 take tile 2w,
-// waves 4-7 tile 2w + 1, one table staging for both.
-template <int NT>
-__device__ __forceinline__ void stage_tables_rotated_nt(const PassDesc &P, uint32_t rot) {
-  extern __shared__ __attribute__((aligned(16))) uint2 lds_table[];
-  const uint32_t n_in = P.n_in;
-  const AS_GLOBAL u32x4 *tab = (const AS_GLOBAL u32x4 *)(uintptr_t)P.table;
-  u32x4 *dst = reinterpret_cast<u32x4 *>(lds_table);
-  const uint32_t n16 = n_in * 32;
-  constexpr int R = int(kMaxPassInputs * 32 / NT);
-  u32x4 v[R];
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const uint32_t e = threadIdx.x + uint32_t(NT) * r;
-    v[r] = e < n16 ? tab[e] : u32x4{0, 0, 0, 0};
-  }
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const uint32_t e = threadIdx.x + uint32_t(NT) * r;
-    if (e < n16) {
-      const uint32_t i = e >> 5;
-      const uint32_t x = i >= rot ? i - rot : i + n_in - rot;
-      dst[x * 32 + (e & 31)] = v[r];
-    }
-  }
-  __syncthreads();
-}
-
-__global__ __launch_bounds__(512, 2) void gf_apply_unrolled_wide_kernel(const KernArgs args) {
-  constexpr int GL = 5, STEP = 4;  // 32 workgroups x 16 KiB = the 512 KiB read group of v76
-  const uint32_t wg = xcd_group_remap<(1u << GL)>(blockIdx.x, gridDim.x);
-  const PassDesc &P = find_pass(args, wg);
-  const uint32_t tile2 = wg - P.wg_begin;
-  const uint32_t n_in = P.n_in;
-  const uint32_t rot = P.rotate ? ((tile2 >> GL) * STEP) % n_in : 0;
-  stage_tables_rotated_nt<512>(P, rot);
-  const uint32_t w8 = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t tile = 2 * tile2 + (w8 >> 2), wave_id = w8 & 3;
-  if (tile >= P.n_tiles) return;
-  if (n_in == 30)
-    tile_unrolled<30, 1, true>(args, P, tile, wave_id, rot);
-  else if (n_in == 8)
-    tile_unrolled<8, 1, true>(args, P, tile, wave_id, rot);
-  else if (n_in == 20)
-    tile_unrolled<20, 1, true>(args, P, tile, wave_id, rot);
-  else
-    ring_tile_ct<1, 1, 6, false, 1, 1, true>(args, P, tile, wave_id, rot);
-}
-
 // Tail chunk (shard_bytes % 64 = tb != 0): tb/2 symbols, low bytes at
 // [base, base+tb/2), high bytes at [base+tb/2, base+tb) — the crate's tail rule.
 // One workgroup per pass, one lane per symbol; rare and tiny.
@@ -913,8 +862,6 @@ int kernel_variant() {
 
 uint32_t tile_bytes() { return kTileHalfChunks * 32; }
 
-uint32_t preferred_tiles_per_wg() { return kernel_variant() == 89 ? 2 : 1; }
-
 hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in, bool subfield,
                            hipStream_t stream) {
   if (n_wgs == 0) return hipSuccess;
@@ -959,12 +906,6 @@ hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in
       else
         hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16, 1, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
       break;
-    case 89:  // 512-lane workgroups over two tiles (host tiles_per_wg = 2)
-      if (subfield && args.tiles_per_wg == 2) {
-        hipLaunchKernelGGL(gf_apply_unrolled_wide_kernel, dim3(n_wgs), dim3(512), lds, stream, args);
-        break;
-      }
-      [[fallthrough]];
     case 78:  // 76 with read groups of 16 tiles (the round-1 grouping)
     case 79:  // 76 with read groups of 32 tiles
     case 80:  // 76 with read groups of 128 tiles
