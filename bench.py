@@ -474,30 +474,41 @@ def crate_api(ctx, sets, reps=3):
     Chunker::generate_parity on one RS(30,3) block of 32 MiB segments
     (src/chunker/generate.rs:59-104) and recover_segment_rs30_3 of one erased
     segment (src/filestore/recovery.rs:118-173), pageable host buffers in and
-    out as the Rust Vecs are."""
+    out as the Rust Vecs are.  Timed at the C-ABI (what the Rust binding
+    calls): fresh, untouched output buffers per call, like the Vecs the
+    reference allocates (generate.rs:95-96), so their page faults count.  The
+    Python wrappers' extra bytes() copies are reported apart (`python_wrapper_ms`)."""
     import numpy as np
     import bfrs
     S, k = sets.S, sets.shapes[0]
     segs = [sets.data[i].cpu().numpy() for i in range(k)]
     ch = bfrs.Chunker(ctx)
-    t_gen = []
-    for _ in range(reps):
-        t0 = time.perf_counter()
-        par = ch.generate_parity(segs, k, 3)
-        t_gen.append(time.perf_counter() - t0)
-    par = [np.frombuffer(p, np.uint8) for p in par]
+
+    def timed(f, n=reps):
+        ts = []
+        for _ in range(n):
+            t0 = time.perf_counter()
+            f()
+            ts.append(time.perf_counter() - t0)
+        return min(ts)
+
+    tg = timed(lambda: ch.generate_parity_into(segs, k, 3,
+                                               [np.empty(S, np.uint8) for _ in range(3)]))
+    tg_py = timed(lambda: ch.generate_parity(segs, k, 3))
+    par = [np.empty(S, np.uint8) for _ in range(3)]
+    ch.generate_parity_into(segs, k, 3, par)
     target = sets.erased[0][0]
     slots = [None if i == target else segs[i] for i in range(k)] + [None] * (30 - k)
-    t_rec = []
-    for _ in range(reps):
-        t0 = time.perf_counter()
-        got = bfrs.recover_segment_rs30_3(ctx, slots, par, target)
-        t_rec.append(time.perf_counter() - t0)
-    assert np.array_equal(np.frombuffer(got, np.uint8), segs[target]), "crate_api recover mismatch"
+    got = np.empty(S, np.uint8)
+    tr = timed(lambda: bfrs.recover_segment_rs30_3_into(ctx, slots, par, target,
+                                                        np.empty(S, np.uint8)))
+    tr_py = timed(lambda: bfrs.recover_segment_rs30_3(ctx, slots, par, target))
+    assert bfrs.recover_segment_rs30_3_into(ctx, slots, par, target, got) == S
+    assert np.array_equal(got, segs[target]), "crate_api recover mismatch"
     gib = k * S / 2**30
-    tg, tr = min(t_gen), min(t_rec)
     # rayon's shape (commit.rs:391-466): one generate_parity per block, all of
-    # C2's blocks at once from worker threads sharing the one context
+    # C2's blocks at once from worker threads sharing the one context (ctypes
+    # drops the GIL for the call)
     import threading
     blocks, off = [], 0
     for kb in sets.shapes:
@@ -507,7 +518,8 @@ def crate_api(ctx, sets, reps=3):
 
     def worker(b):
         try:
-            bfrs.Chunker(ctx).generate_parity(blocks[b], len(blocks[b]), 3)
+            bfrs.Chunker(ctx).generate_parity_into(
+                blocks[b], len(blocks[b]), 3, [np.empty(S, np.uint8) for _ in range(3)])
         except Exception as e:  # noqa: BLE001 - reported below
             errors.append(repr(e))
 
@@ -524,15 +536,18 @@ def crate_api(ctx, sets, reps=3):
     par_gib = sum(sets.shapes) * S / 2**30
     return {
         "generate_parity": {"ms": round(tg * 1e3, 2), "GiBps": round(gib / tg, 2),
+                            "python_wrapper_ms": round(tg_py * 1e3, 2),
                             "what": f"RS({k},3) block of {S >> 20} MiB segments, pageable host in/out"},
         "recover_segment_rs30_3": {"ms": round(tr * 1e3, 2), "GiBps_of_block": round(gib / tr, 2),
+                                   "python_wrapper_ms": round(tr_py * 1e3, 2),
                                    "what": "one erased segment of that block, pageable host in/out"},
         "generate_parity_all_blocks_threads": {
             "ms": round(min(t_par) * 1e3, 2), "GiBps": round(par_gib / min(t_par), 2),
             "what": f"{len(blocks)} blocks ({'+'.join(map(str, sets.shapes))} x {S >> 20} MiB) "
                     "on as many threads, one shared context (rayon over blocks), best of 2",
             "codec_slots": int(os.environ.get("BFRS_CODEC_SLOTS", "2"))},
-        "reps": reps, "timing": "best of reps, wall clock",
+        "reps": reps, "timing": "C-ABI call (bfrs_generate_parity / bfrs_recover_segment_rs30_3) "
+                                "through ctypes, fresh output buffers, best of reps, wall clock",
     }
 
 

@@ -225,6 +225,16 @@ def _host_ptr(buf) -> int:
     raise TypeError(f"unsupported host buffer type {type(buf)}")
 
 
+def _out_nbytes(buf) -> int:
+    """Size of a writable output buffer (numpy array or bytearray)."""
+    import numpy as np
+    if isinstance(buf, np.ndarray):
+        return buf.nbytes
+    if isinstance(buf, bytearray):
+        return len(buf)
+    raise TypeError(f"output buffer must be a numpy array or bytearray, not {type(buf)}")
+
+
 def _as_np(buf):
     import numpy as np
     if isinstance(buf, np.ndarray):
@@ -519,13 +529,23 @@ class Chunker:
         segs = [_as_np(s) for s in segments]
         maxlen = max((s.size for s in segs), default=0)
         outs = [np.empty(maxlen, dtype=np.uint8) for _ in range(parity_shards)]
+        self.generate_parity_into(segs, data_shards, parity_shards, outs)
+        return [o.tobytes() for o in outs]
+
+    def generate_parity_into(self, segments, data_shards: int, parity_shards: int, outs) -> int:
+        """generate_parity writing into caller buffers (each >= the longest
+        segment), as a Rust caller of the C-ABI would; returns the parity length."""
+        segs = [_as_np(s) for s in segments]
+        if len(outs) < parity_shards or any(
+                _out_nbytes(o) < max((s.size for s in segs), default=0) for o in outs):
+            raise ValueError("generate_parity_into: output buffers too small")
         ps, ks = _ptr_array([s.ctypes.data if s.size else None for s in segs])
         lens = (_sz * max(1, len(segs)))(*[s.size for s in segs])
-        po, ko = _ptr_array([o.ctypes.data for o in outs])
+        po, ko = _ptr_array([_host_ptr(o) for o in outs])
         plen = _sz()
         _check(lib().bfrs_generate_parity(self.ctx.handle, ps, lens, len(segs), data_shards,
                                           parity_shards, po, ctypes.byref(plen)))
-        return [o.tobytes() for o in outs]
+        return plen.value
 
     def generate_parity_segmented(self, segment_data):
         import numpy as np
@@ -561,17 +581,29 @@ def recover_segment_rs30_3(ctx: Context, valid_segments, block_parity, target_in
     segs = [None if s is None else _as_np(s) for s in valid_segments]
     par = [_as_np(p) for p in block_parity]
     sizes = [s.size for s in segs if s is not None] + [p.size for p in par]
-    n = max(sizes, default=0)
-    out = np.empty(max(1, n), dtype=np.uint8)
+    out = np.empty(max(1, max(sizes, default=0)), dtype=np.uint8)
+    n = recover_segment_rs30_3_into(ctx, segs, par, target_index, out)
+    return out[:n].tobytes()
+
+
+def recover_segment_rs30_3_into(ctx: Context, valid_segments, block_parity, target_index: int,
+                                out) -> int:
+    """recover_segment_rs30_3 writing into a caller buffer (>= the largest
+    shard), as a Rust caller of the C-ABI would; returns the restored length."""
+    segs = [None if s is None else _as_np(s) for s in valid_segments]
+    par = [_as_np(p) for p in block_parity]
+    n = max([s.size for s in segs if s is not None] + [p.size for p in par], default=0)
+    if _out_nbytes(out) < n:
+        raise ValueError("recover_segment_rs30_3_into: output buffer too small")
     ps, ks = _ptr_array([None if s is None else s.ctypes.data for s in segs])
     slens = (_sz * max(1, len(segs)))(*[0 if s is None else s.size for s in segs])
     pp, kp = _ptr_array([p.ctypes.data for p in par])
     plens = (_sz * max(1, len(par)))(*[p.size for p in par])
     olen = _sz()
     _check(lib().bfrs_recover_segment_rs30_3(ctx.handle, ps, slens, len(segs), pp, plens,
-                                             len(par), target_index, out.ctypes.data,
+                                             len(par), target_index, _host_ptr(out),
                                              ctypes.byref(olen)))
-    return out[:olen.value].tobytes()
+    return olen.value
 
 
 # ---- integrity helpers + archive pipeline (src/utils.rs, src/merkle_tree,

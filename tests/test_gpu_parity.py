@@ -411,6 +411,28 @@ def test_recover_segment_rs30_3_roundtrip(ctx, bfrs, oracle):
     assert "Failed to restore target segment" in str(e.value)
 
 
+def test_into_forms_match_wrappers(ctx, bfrs, oracle):
+    """The caller-buffer forms bench.py's crate_api times: the same bytes as the
+    wrappers (and the oracle), numpy or bytearray outputs, short buffers refused
+    before the call."""
+    rng = np.random.default_rng(10)
+    n = 3 << 16
+    data = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(30)]
+    want = [r.tobytes() for r in oracle.encode(data, 3)]
+    outs = [np.empty(n, np.uint8), bytearray(n), np.empty(n + 64, np.uint8)]
+    assert bfrs.Chunker(ctx).generate_parity_into(data, 30, 3, outs) == n
+    assert [bytes(o[:n]) for o in outs] == want
+    with pytest.raises(ValueError):
+        bfrs.Chunker(ctx).generate_parity_into(data, 30, 3, [np.empty(n - 2, np.uint8)] * 3)
+    slots = [None if i == 11 else data[i] for i in range(30)]
+    par = [np.frombuffer(p, np.uint8) for p in want]
+    got = bytearray(n)
+    assert bfrs.recover_segment_rs30_3_into(ctx, slots, par, 11, got) == n
+    assert bytes(got) == data[11].tobytes()
+    with pytest.raises(ValueError):
+        bfrs.recover_segment_rs30_3_into(ctx, slots, par, 11, np.empty(n - 64, np.uint8))
+
+
 # ---------------------------------------------------------------- BASELINE config sizes
 def _c2_workload(seed, nseg):
     from bfrs import synth
