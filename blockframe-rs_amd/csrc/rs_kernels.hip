@@ -694,9 +694,20 @@ __device__ __forceinline__ void unrolled_ring(const uint64_t *in, uint32_t rot, 
   (unrolled_step<N, LPOL, B64, Cs>(in, rot, ln, mask, A, B, acc_lo, acc_hi), ...);
 }
 
-// Epilogue of an unrolled tile: outputs back to the contiguous layout, nt stores.
-__device__ __forceinline__ void tile_store(const KernArgs &args, const PassDesc &P, const CtLane &ln,
-                                           uint32_t (&acc_lo)[16], uint32_t (&acc_hi)[16]) {
+template <int N, int LPOL, bool B64>
+__device__ __forceinline__ void tile_unrolled(const KernArgs &args, const PassDesc &P,
+                                              uint32_t tile, uint32_t wave_id, uint32_t rot) {
+  const uint64_t wchunk0 = (uint64_t(tile) * 4 + wave_id) * 32;
+  if (wchunk0 >= P.full_chunks) return;  // wave-uniform
+  const CtLane ln = ct_lane(wchunk0, P.full_chunks);
+  const uint64_t *in = args.ptrs + P.in;
+  const uint32_t mask = __builtin_amdgcn_readfirstlane(0xF0u);
+  uint32_t acc_lo[16], acc_hi[16];
+#pragma unroll
+  for (int s = 0; s < 16; ++s) acc_lo[s] = acc_hi[s] = 0;
+  u32x4 A[N], B[N];
+  unrolled_ring<N, LPOL, B64>(in, rot, ln, mask, A, B, acc_lo, acc_hi,
+                         std::make_integer_sequence<uint32_t, N + 3>{});
   const uint32_t n_out = P.n_out;
   const uint64_t *outp = args.ptrs + P.out;
   const bool accumulate = P.accumulate != 0;
@@ -722,89 +733,6 @@ __device__ __forceinline__ void tile_store(const KernArgs &args, const PassDesc 
     if (ln.okA) store16_nt(dst + ln.offA, ol);
     if (ln.okB) store16_nt(dst + ln.offB, oh);
   }
-}
-
-template <int N, int LPOL, bool B64>
-__device__ __forceinline__ void tile_unrolled(const KernArgs &args, const PassDesc &P,
-                                              uint32_t tile, uint32_t wave_id, uint32_t rot) {
-  const uint64_t wchunk0 = (uint64_t(tile) * 4 + wave_id) * 32;
-  if (wchunk0 >= P.full_chunks) return;  // wave-uniform
-  const CtLane ln = ct_lane(wchunk0, P.full_chunks);
-  const uint64_t *in = args.ptrs + P.in;
-  const uint32_t mask = __builtin_amdgcn_readfirstlane(0xF0u);
-  uint32_t acc_lo[16], acc_hi[16];
-#pragma unroll
-  for (int s = 0; s < 16; ++s) acc_lo[s] = acc_hi[s] = 0;
-  u32x4 A[N], B[N];
-  unrolled_ring<N, LPOL, B64>(in, rot, ln, mask, A, B, acc_lo, acc_hi,
-                         std::make_integer_sequence<uint32_t, N + 3>{});
-  tile_store(args, P, ln, acc_lo, acc_hi);
-}
-
-// v98: the ring's first 3 inputs (HBM) are issued together with the
-// workgroup's table loads (L2), so a new workgroup's first data requests no
-// longer wait for the table staging and its barrier.  The table loads are asm
-// too and go first: vmcnt(6) then waits for them alone.  Every wave issues
-// the data loads (a wave past the shard's last chunk reads chunk 0 through
-// ct_lane's fallback offsets), so the counts are the same on every path.
-template <int N, int LPOL, bool B64, uint32_t Off, uint32_t... Cs>
-__device__ __forceinline__ void unrolled_ring_off(const uint64_t *in, uint32_t rot, const CtLane &ln,
-                                                  uint32_t mask, u32x4 (&A)[N], u32x4 (&B)[N],
-                                                  uint32_t (&acc_lo)[16], uint32_t (&acc_hi)[16],
-                                                  std::integer_sequence<uint32_t, Cs...>) {
-  (unrolled_step<N, LPOL, B64, Cs + Off>(in, rot, ln, mask, A, B, acc_lo, acc_hi), ...);
-}
-
-template <int N, int LPOL, bool B64>
-__device__ __forceinline__ void tile_unrolled_ovl(const KernArgs &args, const PassDesc &P,
-                                                  uint32_t tile, uint32_t wave_id, uint32_t rot) {
-  extern __shared__ __attribute__((aligned(16))) uint2 lds_table[];
-  constexpr int R = (N * 32 + 255) / 256;  // 16-B table loads per lane
-  static_assert(R >= 1 && R <= 4, "table loads per lane");
-  const uint32_t n16 = uint32_t(N) * 32;
-  const uint64_t tab = P.table;
-  u32x4 v[4];
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const uint32_t e = threadIdx.x + 256u * r;
-    const uint32_t off = (e < n16 ? e : 0u) * 16u;
-    asm volatile("global_load_dwordx4 %0, %1, %2" : "=&v"(v[r]) : "v"(off), "s"(tab) : "memory");
-  }
-  const uint64_t wchunk0 = (uint64_t(tile) * 4 + wave_id) * 32;
-  const CtLane ln = ct_lane(wchunk0, P.full_chunks);
-  const uint64_t *in = args.ptrs + P.in;
-  const uint32_t mask = __builtin_amdgcn_readfirstlane(0xF0u);
-  uint32_t acc_lo[16], acc_hi[16];
-  u32x4 A[N], B[N];
-  unrolled_ring_off<N, LPOL, B64, 0>(in, rot, ln, mask, A, B, acc_lo, acc_hi,
-                                     std::make_integer_sequence<uint32_t, 3>{});
-  if constexpr (R == 1)
-    asm volatile("s_waitcnt vmcnt(6)" : "+v"(v[0])::"memory");
-  else if constexpr (R == 2)
-    asm volatile("s_waitcnt vmcnt(6)" : "+v"(v[0]), "+v"(v[1])::"memory");
-  else if constexpr (R == 3)
-    asm volatile("s_waitcnt vmcnt(6)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2])::"memory");
-  else
-    asm volatile("s_waitcnt vmcnt(6)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3])::"memory");
-  u32x4 *dst = reinterpret_cast<u32x4 *>(lds_table);
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const uint32_t e = threadIdx.x + 256u * r;
-    if (e < n16) {
-      const uint32_t i = e >> 5;  // source input
-      const uint32_t x = i >= rot ? i - rot : i + N - rot;  // its slot
-      dst[x * 32 + (e & 31)] = v[r];
-    }
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  // no early exit for a wave past the last chunk (a branch here makes the
-  // register allocator copy the in-flight ring registers): it runs the ring
-  // on chunk 0's bytes and tile_store skips all its stores (okA = okB = 0)
-#pragma unroll
-  for (int s = 0; s < 16; ++s) acc_lo[s] = acc_hi[s] = 0;
-  unrolled_ring_off<N, LPOL, B64, 3>(in, rot, ln, mask, A, B, acc_lo, acc_hi,
-                                     std::make_integer_sequence<uint32_t, N>{});
-  tile_store(args, P, ln, acc_lo, acc_hi);
 }
 
 // Pass lookup (binary search over wg_begin) without staging.
@@ -851,21 +779,16 @@ __device__ __forceinline__ void stage_tables_rotated(const PassDesc &P, uint32_t
 // Host contract: every pass subfield, tiles_per_wg == 1.
 // GL: log2 of the read group (consecutive tiles sharing one starting input,
 // placed on one XCD); STEP: how far consecutive groups' starting inputs move.
-template <bool B64, int GL = 6, int STEP = 4, bool OVL = false>
+template <bool B64, int GL = 6, int STEP = 4>
 __global__ __launch_bounds__(256, 5) void gf_apply_unrolled_kernel(const KernArgs args) {
   const uint32_t wg = xcd_group_remap<(1u << GL)>(blockIdx.x, gridDim.x);
   const PassDesc &P = find_pass(args, wg);
   const uint32_t tile = wg - P.wg_begin;
   const uint32_t n_in = P.n_in;
   const uint32_t rot = P.rotate ? ((tile >> GL) * STEP) % n_in : 0;  // read order of v41/v58
-  const uint32_t wave_id = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if constexpr (OVL) {  // v98: table staging overlapped with the first data loads
-    if (n_in == 30) return tile_unrolled_ovl<30, 1, B64>(args, P, tile, wave_id, rot);
-    if (n_in == 8) return tile_unrolled_ovl<8, 1, B64>(args, P, tile, wave_id, rot);
-    if (n_in == 20) return tile_unrolled_ovl<20, 1, B64>(args, P, tile, wave_id, rot);
-  }
   stage_tables_rotated(P, rot);
   if (tile >= P.n_tiles) return;
+  const uint32_t wave_id = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (n_in == 30)
     tile_unrolled<30, 1, B64>(args, P, tile, wave_id, rot);
   else if (n_in == 8)
@@ -978,16 +901,6 @@ hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in
       hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16, 1, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
       break;
     case 75:  // 73 with the GF(2^8)-subfield arithmetic when every pass allows it
-      if (subfield)
-        hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16, 1, 1, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
-      else
-        hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16, 1, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
-      break;
-    case 98:  // 76 with the table staging overlapped with the first data loads
-      if (subfield && args.tiles_per_wg == 1) {
-        hipLaunchKernelGGL((gf_apply_unrolled_kernel<true, 6, 4, true>), dim3(n_wgs), dim3(256), lds, stream, args);
-        break;
-      }
       if (subfield)
         hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16, 1, 1, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
       else
