@@ -935,7 +935,6 @@ hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in
         break;
       }
       [[fallthrough]];
-    case 99:  // 76 kernel; decode passes read originals first (runtime.cpp)
     case 76:  // unrolled SDWA-addressed kernel where the launch allows it, else 75
       if (subfield && args.tiles_per_wg == 1)
         hipLaunchKernelGGL(gf_apply_unrolled_kernel<true>, dim3(n_wgs), dim3(256), lds, stream, args);

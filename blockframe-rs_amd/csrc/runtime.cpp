@@ -313,29 +313,12 @@ int Context::get_encode_plan(size_t k, size_t m, PlanRef *out) {
 
 int Context::get_decode_plan(size_t k, size_t m, const std::vector<uint8_t> &orig_present,
                              const std::vector<uint8_t> &rec_present, PlanRef *out) {
-  const bool orig_first = decode_orig_first();
-  std::string key = (orig_first ? "O" : "D") + std::to_string(k) + "," + std::to_string(m) + ":";
+  std::string key = "D" + std::to_string(k) + "," + std::to_string(m) + ":";
   for (uint8_t b : orig_present) key.push_back(b ? '1' : '0');
   key.push_back('/');
   for (uint8_t b : rec_present) key.push_back(b ? '1' : '0');
-  return cached_plan(*this, key, [&] {
-    CoefMatrix c = plan_decode(k, m, orig_present, rec_present);
-    if (!orig_first) return c;
-    // columns: present originals first, then present recovery shards
-    size_t nr = 0;
-    for (uint8_t b : rec_present) nr += b != 0;
-    CoefMatrix o = c;
-    const size_t no = c.cols - nr;
-    for (size_t r = 0; r < c.rows; ++r)
-      for (size_t j = 0; j < c.cols; ++j)
-        o.c[r * c.cols + j] = c.c[r * c.cols + (j < no ? nr + j : j - no)];
-    return o;
-  }, out);
+  return cached_plan(*this, key, [&] { return plan_decode(k, m, orig_present, rec_present); }, out);
 }
-
-// Experiment (variant 99): decode passes read the surviving originals first
-// and the recovery shards last (the planner's column order is the reverse).
-bool decode_orig_first() { return kernel_variant() == 99; }
 
 int Context::run_blocks(const std::vector<BlockIO> &blocks, size_t shard_bytes, hipStream_t s) {
   if (shard_bytes <= kMaxWindowBytes) return run_window(blocks, shard_bytes, s);
@@ -644,16 +627,11 @@ int decode_batch_on(bfrs_ctx *ctx, size_t nblocks, const uint32_t *ks, size_t m,
     }
     BlockIO io;
     if ((rc = c.get_decode_plan(k, m, op, rp, &io.plan))) return rc;
-    const bool orig_first = decode_orig_first();
-    auto add_rec = [&]() -> int {
-      for (size_t j = 0; j < m; ++j)
-        if (rp[j]) {
-          if (int e = check_dev_ptr(d_rec[b * m + j], "recovery shard pointer")) return e;
-          io.in.push_back(d_rec[b * m + j]);
-        }
-      return BFRS_OK;
-    };
-    if (!orig_first && (rc = add_rec())) return rc;
+    for (size_t j = 0; j < m; ++j)
+      if (rp[j]) {
+        if ((rc = check_dev_ptr(d_rec[b * m + j], "recovery shard pointer"))) return rc;
+        io.in.push_back(d_rec[b * m + j]);
+      }
     for (size_t i = 0; i < k; ++i)
       if (op[i]) {
         if ((rc = check_dev_ptr(d_orig[oi + i], "original shard pointer"))) return rc;
@@ -662,7 +640,6 @@ int decode_batch_on(bfrs_ctx *ctx, size_t nblocks, const uint32_t *ks, size_t m,
         if ((rc = check_dev_ptr(d_restored[oi + i], "restored shard pointer"))) return rc;
         io.out.push_back(d_restored[oi + i]);
       }
-    if (orig_first && (rc = add_rec())) return rc;
     oi += k;
     blocks.push_back(std::move(io));
   }

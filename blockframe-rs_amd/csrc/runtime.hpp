@@ -170,7 +170,6 @@ struct Context {
 
 // Argument validation shared by every entry point (crate's Error variants).
 int check_shape(size_t k, size_t m, size_t shard_bytes);
-bool decode_orig_first();
 
 // Batch entry points with an explicit stream (the C-ABI wrappers pass the
 // caller's stream, NULL meaning HIP's default stream; the host-memory API and
