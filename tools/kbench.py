@@ -1,6 +1,9 @@
 """A/B timing of gf_apply variants in ONE process (interleaved rounds).
 
 usage: python tools/kbench.py [--rounds R] [--iters N] [--variants 41,5,44] [--tpw 1,2,5]
+A variant "V:io" runs kernel V in io mode enc / dec / encdr (an encode over the
+decode's regions: survivors + parity rows in, restored rows out) / encr (data in,
+restored rows out): memory-region diagnosis, outputs not checked.
 Variant 44 is a traffic-only probe (no GF arithmetic, wrong output): it gives the
 ceiling of this exact access pattern.  Also times a torch device copy.
 """
@@ -92,18 +95,30 @@ def main():
                 if i in er:
                     erased.append((3 * b + er.index(i), seg + i))
             seg += k
-        return dict(data=data, par=par, rest=rest, dec_in=dec_in, dec_out=dec_out, erased=erased)
+        dr_in, seg = [], 0  # per block: surviving data rows, then its 3 parity rows
+        for b, k in enumerate(shapes):
+            dr_in += [x for x in dec_in[seg:seg + k] if x is not None] + par[3 * b:3 * b + 3]
+            seg += k
+        return dict(data=data, par=par, rest=rest, dec_in=dec_in, dec_out=dec_out, erased=erased,
+                    dr_in=dr_in)
 
     layouts = {x: build(x) for x in a.stagger.split(",")}
     ctx = bfrs.Context(0)
     stream = torch.cuda.current_stream()
     alg = sum(k + 3 for k in shapes) * S
 
-    def run(L):
-        if a.decode:
+    def run(L, io=None):
+        io = io or ("dec" if a.decode else "enc")
+        if io == "dec":
             ctx.decode_batch_dev(shapes, 3, S, L["dec_in"], L["par"], L["dec_out"], stream=stream)
-        else:
+        elif io == "enc":
             ctx.encode_batch_dev(shapes, 3, S, L["data"], L["par"], stream=stream)
+        elif io == "encdr":  # an encode over the decode's regions: survivors + parity in, restored out
+            ctx.encode_batch_dev(shapes, 3, S, L["dr_in"], L["rest"], stream=stream)
+        elif io == "encr":  # an encode writing the restored rows instead of the parity rows
+            ctx.encode_batch_dev(shapes, 3, S, L["data"], L["rest"], stream=stream)
+        else:
+            raise SystemExit(f"unknown io mode {io}")
 
     os.environ["BFRS_KERNEL_VARIANT"] = "1"
     os.environ.pop("BFRS_TILES_PER_WG", None)
@@ -127,7 +142,7 @@ def main():
     rng = random.Random(0x5EED)
 
     def select(v, t):
-        os.environ["BFRS_KERNEL_VARIANT"] = v
+        os.environ["BFRS_KERNEL_VARIANT"] = v.split(":")[0]
         if t == "0":
             os.environ.pop("BFRS_TILES_PER_WG", None)
         else:
@@ -143,12 +158,13 @@ def main():
             # launches (an idle gap or host check puts the next ~30 launches
             # on ramping clocks)
             t1 = time.perf_counter()
+            io = v.split(":")[1] if ":" in v else None
             while time.perf_counter() - t1 < a.settle_ms / 1e3:
-                run(L)
+                run(L, io)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
             for _ in range(a.iters):
-                run(L)
+                run(L, io)
             e1.record(stream)
             torch.cuda.synchronize()
             res[(v, t, x)].append(e0.elapsed_time(e1) / a.iters)
@@ -164,7 +180,7 @@ def main():
         copy_ms.append(e0.elapsed_time(e1) / a.iters)
     # correctness of every codec variant, after the timing
     for (v, t, x) in configs:
-        if v in PROBES:
+        if v in PROBES or ":" in v:  # probes and io-mode runs have no codec output to check
             continue
         L = layouts[x]
         select(v, t)
