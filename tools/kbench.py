@@ -32,7 +32,8 @@ def main():
                     help="comma list: extra bytes between consecutive shards (row pitch S + x); "
                          "suffix b = block-interleaved rows (each block's k data, 3 parity and "
                          "3 restored rows consecutive in one buffer, as the archive arenas); "
-                         "suffix c = physically contiguous allocations (hipDeviceMallocContiguous)")
+                         "suffix c = physically contiguous allocations (hipDeviceMallocContiguous); "
+                         "suffix s = data, parity and restored rows in one allocation")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -71,8 +72,14 @@ def main():
     def build(x):
         contig = x.endswith("c")
         x = x.rstrip("c")
+        single = x.endswith("s")
+        x = x.rstrip("s")
         stagger = int(x.rstrip("b"))
-        if x.endswith("b"):
+        if single:  # data, parity and restored rows in ONE allocation (bench --layout single)
+            allr = rows(a.segments + 6 * nb, S + stagger, contig)
+            data, par, rest = allr[:a.segments], allr[a.segments:a.segments + 3 * nb], \
+                allr[a.segments + 3 * nb:]
+        elif x.endswith("b"):
             allr = rows(sum(k + 6 for k in shapes), S + stagger, contig)
             data, par, rest, r = [], [], [], 0
             for k in shapes:
@@ -200,6 +207,10 @@ def main():
         out[f"v{v}_tpw{t}" + (f"_stagger{x}" if x != "0" else "")] = {"ms": round(m, 4), "GBps": round(alg / m / 1e6, 1), "all_ms": [round(x, 4) for x in ms]}
     cm = float(np.median(copy_ms))
     out["torch_copy_same_bytes"] = {"ms": round(cm, 4), "GBps": round(alg / cm / 1e6, 1)}
+    # device addresses of each layout's first data / parity / restored row
+    # (placement study: does speed follow the virtual address?)
+    out["addresses"] = {x: {"data": hex(L["data"][0].data_ptr()), "par": hex(L["par"][0].data_ptr()),
+                            "rest": hex(L["rest"][0].data_ptr())} for x, L in layouts.items()}
     print(json.dumps({"decode": a.decode, "alg_bytes": alg, **out}, indent=1))
 
 

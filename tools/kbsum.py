@@ -7,5 +7,5 @@ for f in sys.argv[1:]:
     d = json.loads(t[t.find("{"):])
     print("==", f)
     for k, v in d.items():
-        if isinstance(v, dict):
+        if isinstance(v, dict) and "ms" in v:
             print(f"  {k:32s} {v['ms']:.4f} ms {v['GBps']:8.1f} GB/s {v.get('all_ms', '')}")
