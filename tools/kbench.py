@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--tpw", default="0")
     ap.add_argument("--segments", type=int, default=128)
     ap.add_argument("--decode", action="store_true")
+    ap.add_argument("--copy-probe", action="store_true",
+                    help="also time a torch copy inside each layout's first buffer (placement study)")
     ap.add_argument("--settle-ms", type=float, default=200.0,
                     help="untimed launches of the same config right before each timed run")
     ap.add_argument("--stagger", default="0",
@@ -67,9 +69,13 @@ def main():
         """n shard views of S bytes, row i at byte i * pitch of one buffer."""
         buf = (contiguous_buffer(n * pitch) if contiguous
                else torch.empty(n * pitch, dtype=torch.uint8, device="cuda"))
+        bufs.append(buf)
         return [buf[i * pitch:i * pitch + S] for i in range(n)]
 
+    bufs = []  # the flat buffer behind each rows() call (copy probe)
+
     def build(x):
+        del bufs[:]
         contig = x.endswith("c")
         x = x.rstrip("c")
         single = x.endswith("s")
@@ -107,7 +113,7 @@ def main():
             dr_in += [x for x in dec_in[seg:seg + k] if x is not None] + par[3 * b:3 * b + 3]
             seg += k
         return dict(data=data, par=par, rest=rest, dec_in=dec_in, dec_out=dec_out, erased=erased,
-                    dr_in=dr_in)
+                    dr_in=dr_in, flat=bufs[0])
 
     layouts = {x: build(x) for x in a.stagger.split(",")}
     ctx = bfrs.Context(0)
@@ -207,6 +213,23 @@ def main():
         out[f"v{v}_tpw{t}" + (f"_stagger{x}" if x != "0" else "")] = {"ms": round(m, 4), "GBps": round(alg / m / 1e6, 1), "all_ms": [round(x, 4) for x in ms]}
     cm = float(np.median(copy_ms))
     out["torch_copy_same_bytes"] = {"ms": round(cm, 4), "GBps": round(alg / cm / 1e6, 1)}
+    # placement probe: a plain torch copy inside each layout's first buffer
+    # (first half -> second half), timed like the kernels
+    if a.copy_probe:
+        for x, L in layouts.items():
+            fl = L["flat"]
+            h = fl.numel() // 2
+            src_, dst_ = fl[:h], fl[h:2 * h]
+            for _ in range(5):
+                dst_.copy_(src_)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(a.iters):
+                dst_.copy_(src_)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / a.iters
+            out[f"copy_in_layout_{x}"] = {"ms": round(ms, 4), "GBps": round(2 * h / ms / 1e6, 1)}
     # device addresses of each layout's first data / parity / restored row
     # (placement study: does speed follow the virtual address?)
     out["addresses"] = {x: {"data": hex(L["data"][0].data_ptr()), "par": hex(L["par"][0].data_ptr()),
