@@ -35,7 +35,7 @@ def main():
                          "suffix b = block-interleaved rows (each block's k data, 3 parity and "
                          "3 restored rows consecutive in one buffer, as the archive arenas); "
                          "suffix c = physically contiguous allocations (hipDeviceMallocContiguous); "
-                         "suffix s = data, parity and restored rows in one allocation")
+                         "suffix s = data, parity and restored rows in one allocation; suffix r = every row its own allocation")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -80,8 +80,19 @@ def main():
         x = x.rstrip("c")
         single = x.endswith("s")
         x = x.rstrip("s")
+        per_row = x.endswith("r")
+        x = x.rstrip("r")
         stagger = int(x.rstrip("b"))
-        if single:  # data, parity and restored rows in ONE allocation (bench --layout single)
+        if per_row:  # every shard row its own allocation
+            def one(n):
+                out = []
+                for _ in range(n):
+                    b_ = torch.empty(S + stagger, dtype=torch.uint8, device="cuda")
+                    bufs.append(b_)
+                    out.append(b_[:S])
+                return out
+            data, par, rest = one(a.segments), one(3 * nb), one(3 * nb)
+        elif single:  # data, parity and restored rows in ONE allocation (bench --layout single)
             allr = rows(a.segments + 6 * nb, S + stagger, contig)
             data, par, rest = allr[:a.segments], allr[a.segments:a.segments + 3 * nb], \
                 allr[a.segments + 3 * nb:]
