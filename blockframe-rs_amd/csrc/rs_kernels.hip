@@ -694,7 +694,7 @@ __device__ __forceinline__ void unrolled_ring(const uint64_t *in, uint32_t rot, 
   (unrolled_step<N, LPOL, B64, Cs>(in, rot, ln, mask, A, B, acc_lo, acc_hi), ...);
 }
 
-template <int N, int LPOL, bool B64, int SPOL = 1>
+template <int N, int LPOL, bool B64>
 __device__ __forceinline__ void tile_unrolled(const KernArgs &args, const PassDesc &P,
                                               uint32_t tile, uint32_t wave_id, uint32_t rot) {
   const uint64_t wchunk0 = (uint64_t(tile) * 4 + wave_id) * 32;
@@ -730,8 +730,8 @@ __device__ __forceinline__ void tile_unrolled(const KernArgs &args, const PassDe
         oh ^= u32x4{p.x, p.y, p.z, p.w};
       }
     }
-    if (ln.okA) store16_pol<SPOL>(dst + ln.offA, ol);
-    if (ln.okB) store16_pol<SPOL>(dst + ln.offB, oh);
+    if (ln.okA) store16_nt(dst + ln.offA, ol);
+    if (ln.okB) store16_nt(dst + ln.offB, oh);
   }
 }
 
@@ -779,7 +779,7 @@ __device__ __forceinline__ void stage_tables_rotated(const PassDesc &P, uint32_t
 // Host contract: every pass subfield, tiles_per_wg == 1.
 // GL: log2 of the read group (consecutive tiles sharing one starting input,
 // placed on one XCD); STEP: how far consecutive groups' starting inputs move.
-template <bool B64, int GL = 6, int STEP = 4, int LP = 1, int SP = 1>
+template <bool B64, int GL = 6, int STEP = 4>
 __global__ __launch_bounds__(256, 5) void gf_apply_unrolled_kernel(const KernArgs args) {
   const uint32_t wg = xcd_group_remap<(1u << GL)>(blockIdx.x, gridDim.x);
   const PassDesc &P = find_pass(args, wg);
@@ -790,11 +790,11 @@ __global__ __launch_bounds__(256, 5) void gf_apply_unrolled_kernel(const KernArg
   if (tile >= P.n_tiles) return;
   const uint32_t wave_id = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (n_in == 30)
-    tile_unrolled<30, LP, B64, SP>(args, P, tile, wave_id, rot);
+    tile_unrolled<30, 1, B64>(args, P, tile, wave_id, rot);
   else if (n_in == 8)
-    tile_unrolled<8, LP, B64, SP>(args, P, tile, wave_id, rot);
+    tile_unrolled<8, 1, B64>(args, P, tile, wave_id, rot);
   else if (n_in == 20)  // config 4's last block, RS(20,3)
-    tile_unrolled<20, LP, B64, SP>(args, P, tile, wave_id, rot);
+    tile_unrolled<20, 1, B64>(args, P, tile, wave_id, rot);
   else
     ring_tile_ct<1, 1, 6, false, 1, 1, true>(args, P, tile, wave_id, rot);
 }
@@ -905,21 +905,6 @@ hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in
         hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16, 1, 1, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
       else
         hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16, 1, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
-      break;
-    case 100:  // 76 with plain (default-policy) loads
-    case 101:  // 76 with plain (write-back) stores
-    case 102:  // 76 with plain loads and plain stores
-      if (subfield && args.tiles_per_wg == 1) {
-        const int v = kernel_variant();
-        if (v == 100)
-          hipLaunchKernelGGL((gf_apply_unrolled_kernel<true, 6, 4, 0, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
-        else if (v == 101)
-          hipLaunchKernelGGL((gf_apply_unrolled_kernel<true, 6, 4, 1, 0>), dim3(n_wgs), dim3(256), lds, stream, args);
-        else
-          hipLaunchKernelGGL((gf_apply_unrolled_kernel<true, 6, 4, 0, 0>), dim3(n_wgs), dim3(256), lds, stream, args);
-        break;
-      }
-      hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16, 1, 1, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
       break;
     case 78:  // 76 with read groups of 16 tiles (the round-1 grouping)
     case 79:  // 76 with read groups of 32 tiles
