@@ -779,18 +779,13 @@ __device__ __forceinline__ void stage_tables_rotated(const PassDesc &P, uint32_t
 // Host contract: every pass subfield, tiles_per_wg == 1.
 // GL: log2 of the read group (consecutive tiles sharing one starting input,
 // placed on one XCD); STEP: how far consecutive groups' starting inputs move.
-template <bool B64, int GL = 6, int STEP = 4, uint32_t SCAT = 0>
+template <bool B64, int GL = 6, int STEP = 4>
 __global__ __launch_bounds__(256, 5) void gf_apply_unrolled_kernel(const KernArgs args) {
   const uint32_t wg = xcd_group_remap<(1u << GL)>(blockIdx.x, gridDim.x);
   const PassDesc &P = find_pass(args, wg);
-  uint32_t tile = wg - P.wg_begin;
+  const uint32_t tile = wg - P.wg_begin;
   const uint32_t n_in = P.n_in;
   const uint32_t rot = P.rotate ? ((tile >> GL) * STEP) % n_in : 0;  // read order of v41/v58
-  if constexpr (SCAT > 0) {  // v103: consecutive read groups at scattered column blocks
-    const uint32_t g = tile >> GL, ng = P.n_tiles >> GL;
-    if (g < ng && ng % SCAT != 0)
-      tile = (((g * SCAT) % ng) << GL) | (tile & ((1u << GL) - 1));
-  }
   stage_tables_rotated(P, rot);
   if (tile >= P.n_tiles) return;
   const uint32_t wave_id = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -910,17 +905,6 @@ hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in
         hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16, 1, 1, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
       else
         hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16, 1, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
-      break;
-    case 103:  // 76 with consecutive read groups on scattered column blocks (group g -> 37 g mod groups)
-    case 104:  // 76 without read rotation (every group starts at input 0)
-      if (subfield && args.tiles_per_wg == 1) {
-        if (kernel_variant() == 103)
-          hipLaunchKernelGGL((gf_apply_unrolled_kernel<true, 6, 4, 37>), dim3(n_wgs), dim3(256), lds, stream, args);
-        else
-          hipLaunchKernelGGL((gf_apply_unrolled_kernel<true, 6, 0>), dim3(n_wgs), dim3(256), lds, stream, args);
-        break;
-      }
-      hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16, 1, 1, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
       break;
     case 78:  // 76 with read groups of 16 tiles (the round-1 grouping)
     case 79:  // 76 with read groups of 32 tiles
