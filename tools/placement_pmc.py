@@ -62,9 +62,19 @@ def run(a):
         if a.probe:  # plain streams over the same data allocation, settled the same way
             flat = flats[2 * c]
             h = flat.numel() // 2
+            import ctypes
+            sp = ctypes.CDLL(os.path.join(ROOT, "tools", "libstreamprobe.so"))
+            scratch = torch.empty(1 << 20, dtype=torch.int64, device="cuda")
+            sh = ctypes.c_void_p(stream.cuda_stream)
+            nt_read = lambda: sp.bfrs_probe_read(ctypes.c_void_p(flat.data_ptr()),  # noqa: E731
+                                                 ctypes.c_size_t(flat.numel()),
+                                                 ctypes.c_void_p(scratch.data_ptr()), sh)
+            nt_write = lambda: sp.bfrs_probe_write(ctypes.c_void_p(flat.data_ptr()),  # noqa: E731
+                                                   ctypes.c_size_t(flat.numel()), sh)
             for name, fn in (("copy", lambda: flat[h:2 * h].copy_(flat[:h])),
                              ("read", lambda: flat.view(torch.int64).sum()),
-                             ("fill", lambda: flat.fill_(7))):
+                             ("fill", lambda: flat.fill_(7)),
+                             ("ntread", nt_read), ("ntwrite", nt_write)):
                 for _ in range(10):
                     fn()
                 e[0].record(stream)
@@ -73,7 +83,7 @@ def run(a):
                 e[1].record(stream)
                 torch.cuda.synchronize()
                 ms = e[0].elapsed_time(e[1]) / a.launches
-                nbytes = {"copy": 2 * h, "read": flat.numel(), "fill": flat.numel()}[name]
+                nbytes = 2 * h if name == "copy" else flat.numel()
                 row[f"{name}_GBps"] = round(nbytes / ms / 1e6, 1)
         timing.append(row)
     print(json.dumps({"copies": a.copies, "launches": a.launches, "timing": timing,
