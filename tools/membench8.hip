@@ -435,6 +435,34 @@ int main(int argc, char **argv) {
       run<30, 3, 1, 0, 1, 1, 2, 1, 0, 8>("rs", 5);   // 1 KiB/wave, 8 KiB/WG
       run<30, 3, 2, 0, 1, 1, 2, 1, 0, 16>("rs", 5);  // 2 KiB/wave, 32 KiB/WG
     }
+    if (!strcmp(only, "place") && rep == 0) {
+      // placement study: the same patterns on several separately
+      // allocated data sets; a pattern whose time does not depend on the copy
+      // is robust to where the driver puts the shards
+      const int copies = 6;
+      std::vector<uint8_t *> keep;
+      for (int c = 0; c < copies; ++c) {
+        uint8_t *d = nullptr;
+        CHECK(hipMalloc(&d, g.pitch * kShards));
+        CHECK(hipMemset(d, 0x5a, g.pitch * kShards));
+        keep.push_back(d);
+      }
+      for (int c = 0; c < copies; ++c) {
+        g.data = keep[c];
+        char t[32];
+        snprintf(t, sizeof t, "c%d_rs", c);
+        run<30, 3, 2, 0, 1, 1, 2, 1, 0, 4>(t, 5);  // product: 2 KiB/wave, 8 KiB/WG
+        run<30, 3, 4, 0, 1, 1, 2, 1, 0, 4>(t, 4);  // 4 KiB/wave
+        run<30, 3, 8, 0, 1, 1, 1, 1, 0, 4>(t, 4);  // 8 KiB/wave, 2 in flight
+        snprintf(t, sizeof t, "c%d_rsro", c);
+        run<30, 0, 2, 0, 1, 1, 2, 1>(t, 5);        // 30 read streams, no writes
+        snprintf(t, sizeof t, "c%d_k10", c);
+        run<10, 1, 4, 0, 1, 1, 2, 1>(t);
+        snprintf(t, sizeof t, "c%d_read", c);
+        run<1, 0, 4, 0, 1, 0, 2, 0>(t);
+      }
+      return 0;
+    }
     if (all || !strcmp(only, "mix")) {
       run<10, 1, 4, 0, 0, 1, 2, 1>("mix");
       run<3, 3, 4, 0, 0, 1, 2, 1>("mix");
