@@ -799,124 +799,6 @@ __global__ __launch_bounds__(256, 5) void gf_apply_unrolled_kernel(const KernArg
     ring_tile_ct<1, 1, 6, false, 1, 1, true>(args, P, tile, wave_id, rot);
 }
 
-// ---- 4 KiB per wave and input (v92-v94, round 2 A/B) --------------------------
-// tools/membench8 (r02z): the traffic-only pattern runs 4.8% faster when each
-// wave streams 4 KiB of every input instead of 2 KiB (the workgroup's 16 KiB
-// alone buys 1.3%).  Here a workgroup covers two consecutive 8 KiB tiles (the
-// host's tiles_per_wg = 2 grid) and each wave two consecutive 2 KiB groups of
-// 16 symbols per lane: 4 loads per input, 64 accumulator VGPRs, D inputs in
-// flight.
-template <int N>
-__device__ __forceinline__ void vm_wait4(u32x4 &A0, u32x4 &B0, u32x4 &A1, u32x4 &B1) {
-  asm volatile("s_waitcnt vmcnt(%4)" : "+v"(A0), "+v"(B0), "+v"(A1), "+v"(B1) : "n"(N) : "memory");
-}
-
-template <int N, int D, uint32_t C>
-__device__ __forceinline__ void unrolled_step2(const uint64_t *in, uint32_t rot, const CtLane (&ln)[2],
-                                               uint32_t mask, u32x4 (&A)[N][2], u32x4 (&B)[N][2],
-                                               uint32_t (&acc_lo)[2][16], uint32_t (&acc_hi)[2][16]) {
-  if constexpr (C < uint32_t(N)) {  // issue input C: both groups' runs
-    uint32_t src = rot + C;
-    src = src >= uint32_t(N) ? src - N : src;
-    const uint64_t base = in[src];
-    gload_ct<1>(A[C][0], B[C][0], base, ln[0].offA, ln[0].offB);
-    gload_ct<1>(A[C][1], B[C][1], base, ln[1].offA, ln[1].offB);
-  }
-  if constexpr (C >= uint32_t(D) && C - D < uint32_t(N)) {  // consume input C - D
-    constexpr uint32_t c = C - D;
-    constexpr int after = (N - 1 - int(c)) < D ? (N - 1 - int(c)) : D;
-    vm_wait4<4 * after>(A[c][0], B[c][0], A[c][1], B[c][1]);
-#pragma unroll
-    for (int g = 0; g < 2; ++g) {
-      u32x4 L = A[c][g], H = B[c][g];
-      halves_swap(L, H);
-      mac_slot<c, true>(L, H, mask, acc_lo[g], acc_hi[g]);
-    }
-  }
-}
-
-template <int N, int D, uint32_t... Cs>
-__device__ __forceinline__ void unrolled_ring2(const uint64_t *in, uint32_t rot, const CtLane (&ln)[2],
-                                               uint32_t mask, u32x4 (&A)[N][2], u32x4 (&B)[N][2],
-                                               uint32_t (&acc_lo)[2][16], uint32_t (&acc_hi)[2][16],
-                                               std::integer_sequence<uint32_t, Cs...>) {
-  (unrolled_step2<N, D, Cs>(in, rot, ln, mask, A, B, acc_lo, acc_hi), ...);
-}
-
-// tile2 = index of the workgroup's 16 KiB (two 8 KiB tiles) within the pass
-template <int N, int D>
-__device__ __forceinline__ void tile_unrolled2(const KernArgs &args, const PassDesc &P,
-                                               uint32_t tile2, uint32_t wave_id, uint32_t rot) {
-  const uint64_t wchunk0 = (uint64_t(tile2) * 4 + wave_id) * 64;
-  if (wchunk0 >= P.full_chunks) return;  // wave-uniform
-  const CtLane ln[2] = {ct_lane(wchunk0, P.full_chunks), ct_lane(wchunk0 + 32, P.full_chunks)};
-  const uint64_t *in = args.ptrs + P.in;
-  const uint32_t mask = __builtin_amdgcn_readfirstlane(0xF0u);
-  uint32_t acc_lo[2][16], acc_hi[2][16];
-#pragma unroll
-  for (int g = 0; g < 2; ++g)
-#pragma unroll
-    for (int s = 0; s < 16; ++s) acc_lo[g][s] = acc_hi[g][s] = 0;
-  u32x4 A[N][2], B[N][2];
-  unrolled_ring2<N, D>(in, rot, ln, mask, A, B, acc_lo, acc_hi,
-                       std::make_integer_sequence<uint32_t, N + D>{});
-  const uint32_t n_out = P.n_out;
-  const uint64_t *outp = args.ptrs + P.out;
-  const bool accumulate = P.accumulate != 0;
-#pragma unroll
-  for (int g = 0; g < 2; ++g) {
-    transpose_outputs(acc_lo[g]);
-    transpose_outputs(acc_hi[g]);
-  }
-#pragma unroll
-  for (uint32_t t = 0; t < kMaxPassOutputs; ++t) {
-    if (t >= n_out) break;
-    const uint64_t dst = outp[t];
-#pragma unroll
-    for (int g = 0; g < 2; ++g) {
-      u32x4 ol = {acc_lo[g][t], acc_lo[g][4 + t], acc_lo[g][8 + t], acc_lo[g][12 + t]};
-      u32x4 oh = {acc_hi[g][t], acc_hi[g][4 + t], acc_hi[g][8 + t], acc_hi[g][12 + t]};
-      halves_swap(ol, oh);
-      if (accumulate) {
-        if (ln[g].okA) {
-          const uint4 p = load16(dst + ln[g].offA);
-          ol ^= u32x4{p.x, p.y, p.z, p.w};
-        }
-        if (ln[g].okB) {
-          const uint4 p = load16(dst + ln[g].offB);
-          oh ^= u32x4{p.x, p.y, p.z, p.w};
-        }
-      }
-      if (ln[g].okA) store16_nt(dst + ln[g].offA, ol);
-      if (ln[g].okB) store16_nt(dst + ln[g].offB, oh);
-    }
-  }
-}
-
-// Host contract: every pass subfield, tiles_per_wg == 2 (one workgroup per
-// two consecutive 8 KiB tiles); passes of other sizes run the looped subfield
-// ring over the two tiles in turn.
-template <int D, int GL, int MINB>
-__global__ __launch_bounds__(256, MINB) void gf_apply_unrolled2_kernel(const KernArgs args) {
-  constexpr int STEP = 4;
-  const uint32_t wg = xcd_group_remap<(1u << GL)>(blockIdx.x, gridDim.x);
-  const PassDesc &P = find_pass(args, wg);
-  const uint32_t tile2 = wg - P.wg_begin;
-  const uint32_t n_in = P.n_in;
-  const uint32_t rot = P.rotate ? ((tile2 >> GL) * STEP) % n_in : 0;
-  stage_tables_rotated(P, rot);
-  if (2 * tile2 >= P.n_tiles) return;
-  const uint32_t wave_id = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (n_in == 30) {
-    tile_unrolled2<30, D>(args, P, tile2, wave_id, rot);
-  } else if (n_in == 8) {
-    tile_unrolled2<8, D>(args, P, tile2, wave_id, rot);
-  } else {
-    ring_tile_ct<1, 1, 6, false, 1, 1, true>(args, P, 2 * tile2, wave_id, rot);
-    ring_tile_ct<1, 1, 6, false, 1, 1, true>(args, P, 2 * tile2 + 1, wave_id, rot);
-  }
-}
-
 // Tail chunk (shard_bytes % 64 = tb != 0): tb/2 symbols, low bytes at
 // [base, base+tb/2), high bytes at [base+tb/2, base+tb) — the crate's tail rule.
 // One workgroup per pass, one lane per symbol; rare and tiny.
@@ -980,37 +862,11 @@ int kernel_variant() {
 
 uint32_t tile_bytes() { return kTileHalfChunks * 32; }
 
-uint32_t preferred_tiles_per_wg() {
-  const int v = kernel_variant();
-  return v >= 92 && v <= 95 ? 2 : 1;
-}
-
 hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in, bool subfield,
                            hipStream_t stream) {
   if (n_wgs == 0) return hipSuccess;
   const size_t lds = size_t(max_in) * 64 * sizeof(uint2);
   switch (kernel_variant()) {
-    case 92:  // two 8 KiB tiles per workgroup, 4 KiB per wave and input, 2 in flight, groups of 32
-    case 93:  // ... 1 input in flight, 4 waves/SIMD
-    case 94:  // ... 2 in flight, groups of 64 workgroups
-    case 95:  // ... 1 in flight, 4 waves/SIMD, groups of 64 workgroups
-      if (subfield && args.tiles_per_wg == 2) {
-        const int v = kernel_variant();
-        if (v == 92)
-          hipLaunchKernelGGL((gf_apply_unrolled2_kernel<2, 5, 3>), dim3(n_wgs), dim3(256), lds, stream, args);
-        else if (v == 93)
-          hipLaunchKernelGGL((gf_apply_unrolled2_kernel<1, 5, 4>), dim3(n_wgs), dim3(256), lds, stream, args);
-        else if (v == 95)
-          hipLaunchKernelGGL((gf_apply_unrolled2_kernel<1, 6, 4>), dim3(n_wgs), dim3(256), lds, stream, args);
-        else
-          hipLaunchKernelGGL((gf_apply_unrolled2_kernel<2, 6, 3>), dim3(n_wgs), dim3(256), lds, stream, args);
-        break;
-      }
-      if (subfield)
-        hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16, 1, 1, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
-      else
-        hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16, 1, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
-      break;
     case 5:
       hipLaunchKernelGGL((gf_apply_ring_kernel<0>), dim3(n_wgs), dim3(256), lds, stream, args);
       break;
