@@ -65,8 +65,6 @@ static_assert(sizeof(KernArgs) <= 4096, "kernel arguments must fit 4 KiB");
 
 // Column bytes one workgroup tile covers in the selected kernel variant.
 uint32_t tile_bytes();
-// Tiles per workgroup the selected variant is built for (1; 2 for v105).
-uint32_t preferred_tiles_per_wg();
 int kernel_variant();
 
 // subfield: every pass of the launch has GF(2^8)-subfield coefficients

@@ -799,210 +799,6 @@ __global__ __launch_bounds__(256, 5) void gf_apply_unrolled_kernel(const KernArg
     ring_tile_ct<1, 1, 6, false, 1, 1, true>(args, P, tile, wave_id, rot);
 }
 
-// ---- packed accumulators (v105/v106, round 2 A/B) ---------------------------
-// With three outputs, v76's accumulators waste a byte lane: acc_lo[s] and
-// acc_hi[s] each hold 4 output bytes of symbol s, byte 3 unused.  Here
-// acc_a[s] = {lo0, lo1, lo2, hi0} and acc_b[s/2] holds {hi1, hi2} of symbol s
-// in bytes 0-1 (s even) or 2-3 (s odd): 24 VGPRs per 16 symbols instead of
-// 32, which buys 4 KiB per wave and input (v105) at 4 waves/SIMD.  The tables
-// are re-laid in LDS at staging (768 B per input): the high-byte entries
-// become {lo0..lo2, hi0 | hi1, hi2, 0, 0}, and a third 256-B region holds
-// their odd-symbol copies {.. | 0, 0, hi1, hi2}.  Per symbol and input the
-// work is v76's: 4 SDWA + 4 ds_read_b64 + 3 v_bitop3.  Passes with more than
-// three outputs or other input counts keep v76 (host check).
-constexpr uint32_t kSlotP3 = 768;
-
-__device__ __forceinline__ void stage_tables_p3(const PassDesc &P, uint32_t rot) {
-  extern __shared__ __attribute__((aligned(16))) uint2 lds_table[];
-  const uint32_t n_in = P.n_in;
-  const AS_GLOBAL u32x4 *tab = (const AS_GLOBAL u32x4 *)(uintptr_t)P.table;
-  const uint32_t n16 = n_in * 32;  // 32 chunks of 16 B per input: {entry byte_hi 0, entry byte_hi 1}
-  u32x4 v[kMaxPassInputs * 32 / 256];
-#pragma unroll
-  for (int r = 0; r < int(kMaxPassInputs * 32 / 256); ++r) {
-    const uint32_t e = threadIdx.x + 256u * r;
-    v[r] = e < n16 ? tab[e] : u32x4{0, 0, 0, 0};
-  }
-  char *base = reinterpret_cast<char *>(lds_table);
-#pragma unroll
-  for (int r = 0; r < int(kMaxPassInputs * 32 / 256); ++r) {
-    const uint32_t e = threadIdx.x + 256u * r;
-    if (e < n16) {
-      const uint32_t i = e >> 5, c = e & 31, half = c >> 4, nib = c & 15;
-      const uint32_t x = i >= rot ? i - rot : i + n_in - rot;  // its slot
-      const u32x4 q = v[r];  // x,y = byte_hi 0 entry (lo, hi); z,w = byte_hi 1 entry
-      const uint32_t lo1 = q.z | (q.w << 24);
-      const uint32_t hi12 = (q.w >> 8) & 0xFFFFu;
-      char *slot = base + x * kSlotP3;
-      *reinterpret_cast<u32x4 *>(slot + half * 256 + nib * 16) = u32x4{q.x, 0u, lo1, hi12};
-      *reinterpret_cast<uint2 *>(slot + 512 + nib * 16 + half * 8) = make_uint2(lo1, hi12 << 16);
-    }
-  }
-  __syncthreads();
-}
-
-template <uint32_t SLOT>
-__device__ __forceinline__ void mac_slot_p3(const u32x4 &L, const u32x4 &H, uint32_t mask,
-                                            uint32_t (&acc_a)[16], uint32_t (&acc_b)[8]) {
-  const AS_LDS uint8_t *t = (const AS_LDS uint8_t *)(uintptr_t)(SLOT * kSlotP3);
-  const uint32_t l[4] = {L.x, L.y, L.z, L.w};
-  const uint32_t h[4] = {H.x, H.y, H.z, H.w};
-#pragma unroll
-  for (int d = 0; d < 4; ++d) {
-    uint64_t a[4], b[4];
-    uint2 e2[4], e3[4];
-#define BFRS_LOOKUPS_P3(K)                                                                          \
-  a[K] = *(const AS_LDS uint64_t *)(t + 256 + sdwa_lo_nib16<K>(l[d]));                              \
-  b[K] = *(const AS_LDS uint64_t *)(t + sdwa_hi_nib16<K>(l[d], mask));                              \
-  {                                                                                                 \
-    const uint64_t v2 = *(const AS_LDS uint64_t *)(t + ((K) & 1 ? 512 + 8 : 256 + 8) +              \
-                                                   sdwa_lo_nib16<K>(h[d]));                         \
-    const uint64_t v3 = *(const AS_LDS uint64_t *)(t + ((K) & 1 ? 512 : 8) +                        \
-                                                   sdwa_hi_nib16<K>(h[d], mask));                   \
-    e2[K] = make_uint2(uint32_t(v2), uint32_t(v2 >> 32));                                           \
-    e3[K] = make_uint2(uint32_t(v3), uint32_t(v3 >> 32));                                           \
-  }
-#pragma unroll
-    for (int g = 0; g < 2; ++g) {
-      if (g == 0) {
-        BFRS_LOOKUPS_P3(0)
-        BFRS_LOOKUPS_P3(1)
-      } else {
-        BFRS_LOOKUPS_P3(2)
-        BFRS_LOOKUPS_P3(3)
-      }
-#pragma unroll
-      for (int k = 2 * g; k < 2 * g + 2; ++k) {
-        const int s = d * 4 + k;
-        const uint32_t a2 = xor3_lo64(acc_a[s], a[k], b[k]);
-        acc_a[s] = xor3_ordered(a2, e2[k].x, e3[k].x);
-        acc_b[s >> 1] = xor3_ordered(acc_b[s >> 1], e2[k].y, e3[k].y);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-#undef BFRS_LOOKUPS_P3
-  }
-}
-
-template <int N>
-__device__ __forceinline__ void vm_wait_g(u32x4 (&A)[2], u32x4 (&B)[2]) {
-  asm volatile("s_waitcnt vmcnt(%4)" : "+v"(A[0]), "+v"(B[0]), "+v"(A[1]), "+v"(B[1]) : "n"(N) : "memory");
-}
-
-// G = 2-KiB groups per wave (2: 4 KiB per wave and input), D = inputs in flight
-template <int N, int G, int D, uint32_t C>
-__device__ __forceinline__ void step_p3(const uint64_t *in, uint32_t rot, const CtLane (&ln)[G],
-                                        uint32_t mask, u32x4 (&A)[N][G], u32x4 (&B)[N][G],
-                                        uint32_t (&acc_a)[G][16], uint32_t (&acc_b)[G][8]) {
-  if constexpr (C < uint32_t(N)) {  // issue input C
-    uint32_t src = rot + C;
-    src = src >= uint32_t(N) ? src - N : src;
-    const uint64_t base = in[src];
-#pragma unroll
-    for (int g = 0; g < G; ++g) gload_ct<1>(A[C][g], B[C][g], base, ln[g].offA, ln[g].offB);
-  }
-  if constexpr (C >= uint32_t(D) && C - D < uint32_t(N)) {  // consume input C - D
-    constexpr uint32_t c = C - D;
-    constexpr int after = (N - 1 - int(c)) < D ? (N - 1 - int(c)) : D;
-    if constexpr (G == 2)
-      vm_wait_g<4 * after>(A[c], B[c]);
-    else
-      vm_wait_n<2 * after>(A[c][0], B[c][0]);
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      u32x4 L = A[c][g], H = B[c][g];
-      halves_swap(L, H);
-      mac_slot_p3<c>(L, H, mask, acc_a[g], acc_b[g]);
-    }
-  }
-}
-
-template <int N, int G, int D, uint32_t... Cs>
-__device__ __forceinline__ void ring_p3(const uint64_t *in, uint32_t rot, const CtLane (&ln)[G],
-                                        uint32_t mask, u32x4 (&A)[N][G], u32x4 (&B)[N][G],
-                                        uint32_t (&acc_a)[G][16], uint32_t (&acc_b)[G][8],
-                                        std::integer_sequence<uint32_t, Cs...>) {
-  (step_p3<N, G, D, Cs>(in, rot, ln, mask, A, B, acc_a, acc_b), ...);
-}
-
-// tw = index of the workgroup's G consecutive 8 KiB tiles within the pass
-template <int N, int G, int D>
-__device__ __forceinline__ void tile_p3(const KernArgs &args, const PassDesc &P, uint32_t tw,
-                                        uint32_t wave_id, uint32_t rot) {
-  const uint64_t wchunk0 = (uint64_t(tw) * 4 + wave_id) * 32 * G;
-  if (wchunk0 >= P.full_chunks) return;  // wave-uniform
-  CtLane ln[G];
-#pragma unroll
-  for (int g = 0; g < G; ++g) ln[g] = ct_lane(wchunk0 + 32 * g, P.full_chunks);
-  const uint64_t *in = args.ptrs + P.in;
-  const uint32_t mask = __builtin_amdgcn_readfirstlane(0xF0u);
-  uint32_t acc_a[G][16], acc_b[G][8];
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-#pragma unroll
-    for (int s = 0; s < 16; ++s) acc_a[g][s] = 0;
-#pragma unroll
-    for (int s = 0; s < 8; ++s) acc_b[g][s] = 0;
-  }
-  u32x4 A[N][G], B[N][G];
-  ring_p3<N, G, D>(in, rot, ln, mask, A, B, acc_a, acc_b, std::make_integer_sequence<uint32_t, N + D>{});
-  const uint32_t n_out = P.n_out;
-  const uint64_t *outp = args.ptrs + P.out;
-  const bool accumulate = P.accumulate != 0;
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-    uint32_t acc_lo[16], acc_hi[16];
-#pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      acc_lo[s] = acc_a[g][s];  // byte 3 (hi0) only reaches output 3, never stored
-      acc_hi[s] = __builtin_amdgcn_perm(acc_b[g][s >> 1], acc_a[g][s], (s & 1) ? 0x0C070603u : 0x0C050403u);
-    }
-    transpose_outputs(acc_lo);
-    transpose_outputs(acc_hi);
-#pragma unroll
-    for (uint32_t t = 0; t < 3; ++t) {
-      if (t >= n_out) break;
-      u32x4 ol = {acc_lo[t], acc_lo[4 + t], acc_lo[8 + t], acc_lo[12 + t]};
-      u32x4 oh = {acc_hi[t], acc_hi[4 + t], acc_hi[8 + t], acc_hi[12 + t]};
-      halves_swap(ol, oh);
-      const uint64_t dst = outp[t];
-      if (accumulate) {
-        if (ln[g].okA) {
-          const uint4 p = load16(dst + ln[g].offA);
-          ol ^= u32x4{p.x, p.y, p.z, p.w};
-        }
-        if (ln[g].okB) {
-          const uint4 p = load16(dst + ln[g].offB);
-          oh ^= u32x4{p.x, p.y, p.z, p.w};
-        }
-      }
-      if (ln[g].okA) store16_nt(dst + ln[g].offA, ol);
-      if (ln[g].okB) store16_nt(dst + ln[g].offB, oh);
-    }
-  }
-}
-
-// Host contract: every pass subfield with n_in in {30, 20, 8} and n_out <= 3,
-// tiles_per_wg == G; LDS = max_in * kSlotP3.
-template <int G, int D, int GL, int MINB>
-__global__ __launch_bounds__(256, MINB) void gf_apply_p3_kernel(const KernArgs args) {
-  constexpr int STEP = 4;
-  const uint32_t wg = xcd_group_remap<(1u << GL)>(blockIdx.x, gridDim.x);
-  const PassDesc &P = find_pass(args, wg);
-  const uint32_t tw = wg - P.wg_begin;
-  const uint32_t n_in = P.n_in;
-  const uint32_t rot = P.rotate ? ((tw >> GL) * STEP) % n_in : 0;
-  stage_tables_p3(P, rot);
-  if (G * tw >= P.n_tiles) return;
-  const uint32_t wave_id = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (n_in == 30)
-    tile_p3<30, G, D>(args, P, tw, wave_id, rot);
-  else if (n_in == 8)
-    tile_p3<8, G, D>(args, P, tw, wave_id, rot);
-  else
-    tile_p3<20, G, D>(args, P, tw, wave_id, rot);
-}
-
 // Tail chunk (shard_bytes % 64 = tb != 0): tb/2 symbols, low bytes at
 // [base, base+tb/2), high bytes at [base+tb/2, base+tb) — the crate's tail rule.
 // One workgroup per pass, one lane per symbol; rare and tiny.
@@ -1066,21 +862,6 @@ int kernel_variant() {
 
 uint32_t tile_bytes() { return kTileHalfChunks * 32; }
 
-uint32_t preferred_tiles_per_wg() { return kernel_variant() == 105 ? 2 : 1; }
-
-namespace {
-// v105/v106 need every pass subfield, n_in in {30, 20, 8}, n_out <= 3, and
-// tiles_per_wg equal to their group count
-bool p3_ok(const KernArgs &args, bool subfield, uint32_t groups) {
-  if (!subfield || args.tiles_per_wg != groups) return false;
-  for (uint32_t i = 0; i < args.n_passes; ++i) {
-    const PassDesc &d = args.passes[i];
-    if (d.n_out > 3 || (d.n_in != 30 && d.n_in != 20 && d.n_in != 8)) return false;
-  }
-  return true;
-}
-}  // namespace
-
 hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in, bool subfield,
                            hipStream_t stream) {
   if (n_wgs == 0) return hipSuccess;
@@ -1124,22 +905,6 @@ hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in
         hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16, 1, 1, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
       else
         hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16, 1, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
-      break;
-    case 105:  // packed accumulators, 4 KiB per wave and input, 2 in flight, 4 waves/SIMD
-      if (p3_ok(args, subfield, 2)) {
-        hipLaunchKernelGGL((gf_apply_p3_kernel<2, 2, 5, 4>), dim3(n_wgs), dim3(256),
-                           size_t(max_in) * kSlotP3, stream, args);
-        break;
-      }
-      hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16, 1, 1, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
-      break;
-    case 106:  // packed accumulators, 2 KiB per wave (v76's shape), 3 in flight
-      if (p3_ok(args, subfield, 1)) {
-        hipLaunchKernelGGL((gf_apply_p3_kernel<1, 3, 6, 5>), dim3(n_wgs), dim3(256),
-                           size_t(max_in) * kSlotP3, stream, args);
-        break;
-      }
-      hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16, 1, 1, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
       break;
     case 78:  // 76 with read groups of 16 tiles (the round-1 grouping)
     case 79:  // 76 with read groups of 32 tiles

@@ -378,7 +378,7 @@ int Context::run_window(const std::vector<BlockIO> &blocks, size_t shard_bytes,
 
       // Workgroup sizing: one 8 KiB tile per workgroup unless the grid is huge.
       const uint64_t total_tiles = uint64_t(n_tiles) * (last - first);
-      uint32_t tpw = uint32_t(std::max<uint64_t>(preferred_tiles_per_wg(), total_tiles / 65536));
+      uint32_t tpw = uint32_t(std::max<uint64_t>(1, total_tiles / 65536));
       if (const char *e = std::getenv("BFRS_TILES_PER_WG")) tpw = std::max(1, atoi(e));
       const uint32_t wgs_per_pass = (n_tiles + tpw - 1) / tpw;
 
