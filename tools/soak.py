@@ -1,0 +1,146 @@
+"""GPU soak test (measurement/test tool; the oracle is the checker only).
+
+For a fixed wall time, T threads share ONE context whose plan cache is capped
+small (BFRS_PLAN_CACHE, default 16) so plans are evicted while other threads'
+batches hold theirs.  Every case draws a random shape (k <= 64, m <= 8,
+shard bytes even incl. tails, 0..m erasures, sometimes a corrupted recovery
+shard) and one entry point (one-shot host API, host batch of 1-4 blocks,
+device batch of 1-4 blocks), runs it on the GPU and compares every output
+byte with oracle/rs_oracle.c.  Prints one JSON line; exit 1 on any mismatch.
+
+usage: BFRS_PLAN_CACHE=16 python3 tools/soak.py [--seconds 60] [--threads 4]
+"""
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "blockframe-rs_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seconds", type=float, default=60.0)
+    ap.add_argument("--threads", type=int, default=4)
+    ap.add_argument("--seed", type=int, default=0x50A4)
+    a = ap.parse_args()
+    os.environ.setdefault("BFRS_PLAN_CACHE", "16")
+    import numpy as np
+    import torch
+    import bfrs
+    import oracle
+
+    ctx = bfrs.Context(0)
+    stats = {"cases": 0, "bytes": 0, "by_api": {}, "failures": []}
+    lock = threading.Lock()
+    stop = time.perf_counter() + a.seconds
+
+    def one_block(rng):
+        k = int(rng.choice([1, 2, 3, 4, 5, 8, 20, 30, int(rng.integers(1, 65))]))
+        m = int(rng.choice([1, 2, 3, 3, 3, 4, int(rng.integers(1, 9))]))
+        return k, m
+
+    def worker(tid):
+        rng = np.random.default_rng(a.seed + tid)
+        stream = torch.cuda.Stream()
+        while time.perf_counter() < stop:
+            api = str(rng.choice(["host", "host_batch", "dev_batch"]))
+            k, m = one_block(rng)
+            nblocks = 1 if api == "host" else int(rng.integers(1, 5))
+            n = int(rng.choice([64, 128, 4096, 65536, int(rng.integers(1, 3000)) * 2]))
+            blocks = []
+            for _ in range(nblocks):
+                data = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(k)]
+                rec = oracle.encode(data, m)
+                ne = int(rng.integers(0, m + 1))
+                er = sorted(rng.choice(k, min(ne, k), replace=False).tolist()) if ne else []
+                # keep k shards: drop recovery shards beyond what the erasures need
+                rec_in = list(rec)
+                spare = m - len(er)
+                for j in sorted(rng.choice(m, int(rng.integers(0, spare + 1)), replace=False).tolist()):
+                    rec_in[j] = None
+                if rng.random() < 0.15 and any(r is not None for r in rec_in):
+                    j = next(i for i, r in enumerate(rec_in) if r is not None)
+                    rec_in[j] = rec_in[j].copy()
+                    rec_in[j][int(rng.integers(0, n))] ^= 0x5A  # corrupted, non-codeword input
+                orig_in = [None if i in er else data[i] for i in range(k)]
+                blocks.append((data, rec, orig_in, rec_in, er))
+            try:
+                # encode check for every block, decode check (vs the oracle's decode of the
+                # same, possibly corrupted, inputs) for blocks with erasures
+                if api == "host":
+                    data, rec, orig_in, rec_in, er = blocks[0]
+                    got = ctx.encode(data, m)
+                    ok = all(np.array_equal(g, r) for g, r in zip(got, rec))
+                    if er:
+                        want = oracle.decode(orig_in, rec_in)
+                        out = ctx.decode(orig_in, rec_in)
+                        ok = ok and all(np.array_equal(out[i], want[i]) for i in want)
+                elif api == "host_batch":
+                    # one shape per batch (the batch API shares k across blocks only via ks)
+                    ks = [k] * nblocks
+                    origs = [x for b in blocks for x in b[0]]
+                    outs = [np.empty(n, np.uint8) for _ in range(m * nblocks)]
+                    ctx.encode_host_batch(ks, m, n, origs, outs)
+                    ok = all(np.array_equal(outs[b * m + j], blocks[b][1][j])
+                             for b in range(nblocks) for j in range(m))
+                    oi = [x for b in blocks for x in b[2]]
+                    ri = [x for b in blocks for x in b[3]]
+                    ro = [np.empty(n, np.uint8) if x is None else None for x in oi]
+                    ctx.decode_host_batch(ks, m, n, oi, ri, ro)
+                    for b, blk in enumerate(blocks):
+                        if blk[4]:
+                            want = oracle.decode(blk[2], blk[3])
+                            ok = ok and all(np.array_equal(ro[b * k + i], want[i]) for i in want)
+                else:
+                    ks = [k] * nblocks
+                    with torch.cuda.stream(stream):
+                        d_orig = [torch.from_numpy(x).cuda() for b in blocks for x in b[0]]
+                        d_rec = [torch.empty(n, dtype=torch.uint8, device="cuda") for _ in range(m * nblocks)]
+                        ctx.encode_batch_dev(ks, m, n, d_orig, d_rec, stream=stream)
+                        d_oi = [None if x is None else torch.from_numpy(x).cuda() for b in blocks for x in b[2]]
+                        d_ri = [None if x is None else torch.from_numpy(x).cuda() for b in blocks for x in b[3]]
+                        d_ro = [torch.empty(n, dtype=torch.uint8, device="cuda") if x is None else None
+                                for x in d_oi]
+                        ctx.decode_batch_dev(ks, m, n, d_oi, d_ri, d_ro, stream=stream)
+                        stream.synchronize()
+                    ok = all(np.array_equal(d_rec[b * m + j].cpu().numpy(), blocks[b][1][j])
+                             for b in range(nblocks) for j in range(m))
+                    for b, blk in enumerate(blocks):
+                        if blk[4]:
+                            want = oracle.decode(blk[2], blk[3])
+                            ok = ok and all(np.array_equal(d_ro[b * k + i].cpu().numpy(), want[i])
+                                            for i in want)
+            except bfrs.BfrsError as e:  # every drawn shape is valid and keeps >= k shards
+                ok, err = False, f"{e.code}: {e}"
+            except Exception as e:  # noqa: BLE001 -- record, keep the thread alive
+                ok, err = False, f"{type(e).__name__}: {e}"
+            else:
+                err = None
+            with lock:
+                stats["cases"] += 1
+                stats["bytes"] += nblocks * (k + m) * n
+                stats["by_api"][api] = stats["by_api"].get(api, 0) + 1
+                if not ok and len(stats["failures"]) < 20:
+                    stats["failures"].append({"api": api, "k": k, "m": m, "n": n, "nblocks": nblocks,
+                                              "erasures": [b[4] for b in blocks], "error": err})
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(a.threads)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    ctx.close()
+    stats["plan_cache"] = int(os.environ["BFRS_PLAN_CACHE"])
+    stats["threads"] = a.threads
+    stats["seconds"] = a.seconds
+    print(json.dumps(stats))
+    return 1 if stats["failures"] else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
