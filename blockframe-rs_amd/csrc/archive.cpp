@@ -872,7 +872,10 @@ int bfrs_repair(bfrs_ctx *ctx, const char *archive_dir, bfrs_repair_report *repo
     }
     return BFRS_OK;
   }
-  // tiers 1/2 (repair_tiny :497, repair_segment :542): per-segment RS(1,3)
+  // tiers 1/2 (repair_tiny :497, repair_segment :542): per-segment RS(1,3).
+  // The reference restores only the data; with the intended semantics, as
+  // for tier 3, a damaged parity copy is re-encoded from the verified data
+  // (RS(1,3) through the codec) and checked against the manifest too.
   bfrs_archive a;
   a.ctx = ctx;
   a.g = g;
@@ -884,14 +887,42 @@ int bfrs_repair(bfrs_ctx *ctx, const char *archive_dir, bfrs_repair_report *repo
     SegPtr v;
     bool ok = false;
     if ((rc = a.load_clean(i, &v, &ok))) return rc;
-    if (ok) continue;
-    rc = a.recover(i, &v);
-    if (rc == BFRS_E_NOT_ENOUGH_SHARDS) {
-      ++report->unrecoverable_blocks;
-      continue;
+    if (!ok) {
+      rc = a.recover(i, &v);
+      if (rc == BFRS_E_NOT_ENOUGH_SHARDS) {
+        ++report->unrecoverable_blocks;
+        continue;
+      }
+      if (rc) return rc;
+      ++report->segments_repaired;
     }
-    if (rc) return rc;
-    ++report->segments_repaired;
+    std::vector<std::string> ppath, phash;
+    for (size_t p = 0; p < kParity; ++p) {
+      ppath.push_back(g.mf.tier == 2 ? t2_par(g.dir, i, p)
+                                     : g.dir + "/parity_" + std::to_string(p) + ".dat");
+      phash.push_back(g.mf.tier == 2 ? g.mf.segments.at(int64_t(i)).parity[p]
+                                     : g.mf.leaves.at(int64_t(p + 1)));
+    }
+    std::vector<size_t> bad;
+    std::vector<uint8_t> tmp;
+    for (size_t p = 0; p < kParity; ++p)
+      if (!load_verified(ppath[p], phash[p], &tmp)) bad.push_back(p);
+    if (bad.empty()) continue;
+    const size_t shard = (v->n + 63) / 64 * 64;  // generate.rs:34: padded to 64
+    std::vector<uint8_t> padded(shard, 0);
+    std::memcpy(padded.data(), v->p, v->n);
+    std::vector<std::vector<uint8_t>> par(kParity, std::vector<uint8_t>(shard));
+    const uint8_t *orig[1] = {padded.data()};
+    uint8_t *outp[kParity];
+    for (size_t p = 0; p < kParity; ++p) outp[p] = par[p].data();
+    const uint32_t k1 = 1;
+    if ((rc = bfrs_encode_host_batch(ctx, 1, &k1, kParity, shard, orig, outp))) return rc;
+    for (size_t p : bad) {
+      if (blake3_hex(par[p].data(), shard) != phash[p])
+        return set_error(BFRS_E_WRAPPER, "re-encoded parity fails the manifest hash");
+      if (!write_file(ppath[p], par[p].data(), shard)) return io_error("write parity");
+      ++report->parity_repaired;
+    }
   }
   return BFRS_OK;
   BFRS_API_END

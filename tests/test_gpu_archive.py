@@ -238,18 +238,27 @@ def test_repair_tier2_and_tier1(ctx, bfrs, tmp_path):
     os.remove(os.path.join(a2, "segments", "segment_1.dat"))
     _flip(os.path.join(a2, "segments", "segment_3.dat"))  # the 10-byte tail
     _flip(os.path.join(a2, "parity", "segment_3_parity_0.dat"))
+    os.remove(os.path.join(a2, "parity", "segment_0_parity_2.dat"))  # data intact, one copy lost
     rep = bfrs.repair(ctx, a2)
+    # the reference restores only data; the intended semantics (as tier 3)
+    # also re-encode every damaged parity copy from the verified data
     assert rep["segments_repaired"] == 2 and rep["unrecoverable_blocks"] == 0
+    assert rep["parity_repaired"] == 2
     assert np.array_equal(_read(os.path.join(a2, "segments", "segment_1.dat")), d[SEG:2 * SEG])
     assert np.array_equal(_read(os.path.join(a2, "segments", "segment_3.dat")), d[3 * SEG:])
+    assert np.array_equal(_read(os.path.join(a2, "parity", "segment_3_parity_0.dat")), _pad(d[3 * SEG:], 64))
+    assert np.array_equal(_read(os.path.join(a2, "parity", "segment_0_parity_2.dat")), d[:SEG])
+    assert bfrs.health_check(ctx, a2)["status"] == "Healthy"
 
     path, d = _file(tmp_path, 777, seed=9, name="t1.bin")
     a1 = bfrs.commit(ctx, path, str(tmp_path / "archive"))
     os.remove(os.path.join(a1, "data.dat"))
     os.remove(os.path.join(a1, "parity_0.dat"))
     rep = bfrs.repair(ctx, a1)
-    assert rep["segments_repaired"] == 1
+    assert rep["segments_repaired"] == 1 and rep["parity_repaired"] == 1
     assert np.array_equal(_read(os.path.join(a1, "data.dat")), d)
+    assert np.array_equal(_read(os.path.join(a1, "parity_0.dat")), _pad(d, 832))
+    assert bfrs.health_check(ctx, a1)["status"] == "Healthy"
 
 
 # ---------------------------------------------------------------- read path (FUSE core)
