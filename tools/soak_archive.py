@@ -16,7 +16,7 @@ delete, truncate), and checks against a model of what must happen:
     (generate.rs:84, commit.rs:440-441).
 Prints one JSON line; exit 1 on any violation.
 
-usage: python3 tools/soak_archive.py [--seconds 90] [--workdir /tmp]
+usage: python3 tools/soak_archive.py [--seconds 90] [--readers 4] [--workdir /tmp]
 """
 import argparse
 import json
@@ -24,6 +24,7 @@ import os
 import shutil
 import sys
 import tempfile
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -35,6 +36,7 @@ def main():
     ap.add_argument("--seconds", type=float, default=90.0)
     ap.add_argument("--seed", type=int, default=0xA4C1)
     ap.add_argument("--workdir", default=None)
+    ap.add_argument("--readers", type=int, default=4, help="threads sharing one read handle")
     a = ap.parse_args()
     import numpy as np
     import bfrs
@@ -155,6 +157,29 @@ def main():
                 continue
             if recoverable:
                 stats["recoverable"] += 1
+                if a.readers > 1 and rng.random() < 0.5:
+                    # several threads reading random ranges through ONE handle
+                    # (prefetch and reconstruction shared between them)
+                    errs = []
+                    with bfrs.Archive(ctx, adir, cache_segments=4) as ar:
+                        def reader(seed):
+                            r = np.random.default_rng(seed)
+                            for _ in range(16):
+                                off = int(r.integers(0, n))
+                                ln = int(r.integers(1, min(n - off, 3 * S) + 1))
+                                got = ar.read(off, ln)
+                                if got != data[off:off + ln].tobytes():
+                                    errs.append((off, ln))
+                        th = [threading.Thread(target=reader, args=(int(rng.integers(1 << 30)),))
+                              for _ in range(a.readers)]
+                        for t in th:
+                            t.start()
+                        for t in th:
+                            t.join()
+                    stats["concurrent_reads"] = stats.get("concurrent_reads", 0) + 1
+                    if errs:
+                        fail(case, f"concurrent reads differ at {errs[:3]}")
+                        continue
                 if not np.array_equal(read_all(adir, n), data):
                     fail(case, "read of the damaged archive differs")
                     continue
