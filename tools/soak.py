@@ -5,7 +5,7 @@ small (BFRS_PLAN_CACHE, default 16) so plans are evicted while other threads'
 batches hold theirs.  Every case draws a random shape (k <= 64, m <= 8,
 shard bytes even incl. tails, 0..m erasures, sometimes a corrupted recovery
 shard) and one entry point (one-shot host API, host batch of 1-4 blocks,
-device batch of 1-4 blocks), runs it on the GPU and compares every output
+device batch of 1-4 blocks, the encoder/decoder objects), runs it on the GPU and compares every output
 byte with oracle/rs_oracle.c.  Prints one JSON line; exit 1 on any mismatch.
 
 usage: BFRS_PLAN_CACHE=16 python3 tools/soak.py [--seconds 60] [--threads 4]
@@ -48,9 +48,9 @@ def main():
         rng = np.random.default_rng(a.seed + tid)
         stream = torch.cuda.Stream()
         while time.perf_counter() < stop:
-            api = str(rng.choice(["host", "host_batch", "dev_batch"]))
+            api = str(rng.choice(["host", "host_batch", "dev_batch", "objects"]))
             k, m = one_block(rng)
-            nblocks = 1 if api == "host" else int(rng.integers(1, 5))
+            nblocks = 1 if api in ("host", "objects") else int(rng.integers(1, 5))
             n = int(rng.choice([64, 128, 4096, 65536, int(rng.integers(1, 3000)) * 2]))
             blocks = []
             for _ in range(nblocks):
@@ -80,6 +80,33 @@ def main():
                         want = oracle.decode(orig_in, rec_in)
                         out = ctx.decode(orig_in, rec_in)
                         ok = ok and all(np.array_equal(out[i], want[i]) for i in want)
+                elif api == "objects":
+                    # the crate-shaped objects; the encoder is reused for a second
+                    # round (the crate resets it once its result is released), the
+                    # decoder gets its shards in random order
+                    data, rec, orig_in, rec_in, er = blocks[0]
+                    enc = bfrs.ReedSolomonEncoder(ctx, k, m, n)
+                    ok = True
+                    for rnd in range(2):
+                        src = data if rnd == 0 else [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(k)]
+                        want = rec if rnd == 0 else oracle.encode(src, m)
+                        for x in src:
+                            enc.add_original_shard(x)
+                        got = list(enc.encode().recovery_iter())
+                        ok = ok and all(g == w.tobytes() for g, w in zip(got, want))
+                    del enc
+                    if er:
+                        dec = bfrs.ReedSolomonDecoder(ctx, k, m, n)
+                        items = [("o", i, x) for i, x in enumerate(orig_in) if x is not None] + \
+                                [("r", j, x) for j, x in enumerate(rec_in) if x is not None]
+                        for t_, i, x in [items[q] for q in rng.permutation(len(items))]:
+                            (dec.add_original_shard if t_ == "o" else dec.add_recovery_shard)(i, x)
+                        dec.decode()
+                        want = oracle.decode(orig_in, rec_in)
+                        ok = ok and all(dec.restored_original(i) == want[i].tobytes() for i in want)
+                        ok = ok and all(dec.restored_original(i) is None
+                                        for i in range(k) if orig_in[i] is not None)
+                        del dec
                 elif api == "host_batch":
                     # one shape per batch (the batch API shares k across blocks only via ks)
                     ks = [k] * nblocks
