@@ -208,6 +208,25 @@ def test_large_code_multiphase(ctx, oracle):
             assert np.array_equal(rest[i], d[i])
 
 
+def test_device_path_limit_k1024(ctx, bfrs, oracle):
+    """The device path's largest code (k = 1024, DESIGN §8: 16 accumulate
+    phases of 64 inputs) against the oracle, and the documented refusal above it."""
+    rng = np.random.default_rng(0x400)
+    k, m, n = 1024, 3, 640
+    d = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(k)]
+    want = oracle.encode(d, m, oracle.ENGINE_AVX2)
+    got = ctx.encode(d, m)
+    assert all(np.array_equal(a, b) for a, b in zip(got, want))
+    er = [0, 511, 1023]
+    o = [None if i in er else d[i] for i in range(k)]
+    rest = ctx.decode(o, want)
+    for i in er:
+        assert np.array_equal(rest[i], d[i]), i
+    with pytest.raises(bfrs.BfrsError) as e:
+        ctx.encode(d + [d[0]], m)
+    assert e.value.code == bfrs.E_UNSUPPORTED_SHARD_COUNT
+
+
 def test_misaligned_device_pointer_rejected(ctx, bfrs):
     buf = torch.zeros(4096 + 16, dtype=torch.uint8, device="cuda")
     bad = buf.data_ptr() + 8
