@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--seconds", type=float, default=60.0)
     ap.add_argument("--threads", type=int, default=4)
     ap.add_argument("--seed", type=int, default=0x50A4)
+    ap.add_argument("--large", action="store_true", help="10% of cases with 1-3 MiB shards")
     a = ap.parse_args()
     os.environ.setdefault("BFRS_PLAN_CACHE", "16")
     import numpy as np
@@ -52,10 +53,12 @@ def main():
             k, m = one_block(rng)
             nblocks = 1 if api in ("host", "objects") else int(rng.integers(1, 5))
             n = int(rng.choice([64, 128, 4096, 65536, int(rng.integers(1, 3000)) * 2]))
+            if a.large and rng.random() < 0.1:  # multi-tile grids: 1-3 MiB with a ragged tail
+                n = int(rng.integers(1, 4)) * (1 << 20) + int(rng.integers(0, 64)) * 2
             blocks = []
             for _ in range(nblocks):
                 data = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(k)]
-                rec = oracle.encode(data, m)
+                rec = oracle.encode(data, m, oracle.ENGINE_AVX2)
                 ne = int(rng.integers(0, m + 1))
                 er = sorted(rng.choice(k, min(ne, k), replace=False).tolist()) if ne else []
                 # keep k shards: drop recovery shards beyond what the erasures need
@@ -77,7 +80,7 @@ def main():
                     got = ctx.encode(data, m)
                     ok = all(np.array_equal(g, r) for g, r in zip(got, rec))
                     if er:
-                        want = oracle.decode(orig_in, rec_in)
+                        want = oracle.decode(orig_in, rec_in, oracle.ENGINE_AVX2)
                         out = ctx.decode(orig_in, rec_in)
                         ok = ok and all(np.array_equal(out[i], want[i]) for i in want)
                 elif api == "objects":
@@ -89,7 +92,7 @@ def main():
                     ok = True
                     for rnd in range(2):
                         src = data if rnd == 0 else [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(k)]
-                        want = rec if rnd == 0 else oracle.encode(src, m)
+                        want = rec if rnd == 0 else oracle.encode(src, m, oracle.ENGINE_AVX2)
                         for x in src:
                             enc.add_original_shard(x)
                         got = list(enc.encode().recovery_iter())
@@ -102,7 +105,7 @@ def main():
                         for t_, i, x in [items[q] for q in rng.permutation(len(items))]:
                             (dec.add_original_shard if t_ == "o" else dec.add_recovery_shard)(i, x)
                         dec.decode()
-                        want = oracle.decode(orig_in, rec_in)
+                        want = oracle.decode(orig_in, rec_in, oracle.ENGINE_AVX2)
                         ok = ok and all(dec.restored_original(i) == want[i].tobytes() for i in want)
                         ok = ok and all(dec.restored_original(i) is None
                                         for i in range(k) if orig_in[i] is not None)
@@ -121,7 +124,7 @@ def main():
                     ctx.decode_host_batch(ks, m, n, oi, ri, ro)
                     for b, blk in enumerate(blocks):
                         if blk[4]:
-                            want = oracle.decode(blk[2], blk[3])
+                            want = oracle.decode(blk[2], blk[3], oracle.ENGINE_AVX2)
                             ok = ok and all(np.array_equal(ro[b * k + i], want[i]) for i in want)
                 else:
                     ks = [k] * nblocks
@@ -139,7 +142,7 @@ def main():
                              for b in range(nblocks) for j in range(m))
                     for b, blk in enumerate(blocks):
                         if blk[4]:
-                            want = oracle.decode(blk[2], blk[3])
+                            want = oracle.decode(blk[2], blk[3], oracle.ENGINE_AVX2)
                             ok = ok and all(np.array_equal(d_ro[b * k + i].cpu().numpy(), want[i])
                                             for i in want)
             except bfrs.BfrsError as e:  # every drawn shape is valid and keeps >= k shards
@@ -159,6 +162,11 @@ def main():
     th = [threading.Thread(target=worker, args=(t,)) for t in range(a.threads)]
     for t in th:
         t.start()
+    while any(t.is_alive() for t in th):  # progress on stderr (long runs must keep writing)
+        th[0].join(timeout=30)
+        with lock:
+            print(f"progress: {stats['cases']} cases, {len(stats['failures'])} failures",
+                  file=sys.stderr, flush=True)
     for t in th:
         t.join()
     ctx.close()

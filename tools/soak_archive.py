@@ -201,6 +201,9 @@ def main():
         except Exception as e:  # noqa: BLE001 -- any other error is a violation
             fail(case, f"{type(e).__name__}: {e}")
         finally:
+            if stats["cases"] % 200 == 0:  # progress on stderr (long runs must keep writing)
+                print(f"progress: {stats['cases']} cases, {len(stats['failures'])} failures",
+                      file=sys.stderr, flush=True)
             stats["cases"] += 1
             stats["by_tier"][str(tier)] = stats["by_tier"].get(str(tier), 0) + 1
             shutil.rmtree(work, ignore_errors=True)
