@@ -1,9 +1,10 @@
-"""Short GPU soaks (tools/soak.py, tools/soak_archive.py) inside the -m gpu
+"""Short GPU soaks (tools/soak.py, tools/soak_blake3.py, tools/soak_archive.py) inside the -m gpu
 suite: random shapes, erasure patterns and corrupted recovery shards through
 every codec entry point on several threads with an evicting plan cache, and
 random commit / damage / read / repair cases of the archive pipeline, each
 checked byte for byte against oracle/ (the checker) or the original file.
-The long runs are recorded in profiles/r02 (soak_r02bx/cb, soak_archive_r02by/ca)."""
+The long runs are recorded in profiles/r02 (soak_r02bx/cb/cf, soak_blake3_r02ci,
+soak_archive_r02by/ca/cg)."""
 import json
 import os
 import subprocess
@@ -31,6 +32,11 @@ def test_codec_soak_short():
     res = _run(["tools/soak.py", "--seconds", "8", "--threads", "4", "--seed", "7"],
                {"BFRS_PLAN_CACHE": "16"})
     assert res["cases"] > 100 and set(res["by_api"]) == {"host", "host_batch", "dev_batch", "objects"}
+
+
+def test_blake3_soak_short():
+    res = _run(["tools/soak_blake3.py", "--seconds", "5", "--seed", "13"])
+    assert res["messages"] > 100 and res["combines"] > 5
 
 
 def test_archive_soak_short(tmp_path):
