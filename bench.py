@@ -306,7 +306,12 @@ def run_c4_strong(rt, ctx, args, stream_handle):
     settle(rt, lambda: dec(stream_handle), min(args.settle_ms, 300.0))
     _, t_dec = timed(rt, lambda: dec(stream_handle), steps)
     rt.sync()
-    sets.check_restored()
+    check = {"decode": check_restored(sets)}
+    if rt.world == 1 and not rt.stub:
+        check["encode"] = check_parity_golden(sets.parity, shapes, sets.S, 0xB10C, "c4_320x32MiB")
+    else:
+        check["encode"] = {"match": None, "note": "golden digests cover whole shards; at N > 1 "
+                                                  "the stripes are checked in tests (gloo world 2)"}
     pcie = None
     if args.pcie == "auto" and not rt.stub:
         # device-resident AND incl. pinned H2D/D2H; every
@@ -333,9 +338,50 @@ def run_c4_strong(rt, ctx, args, stream_handle):
         "unit": "GiB/s",
         "ms_per_encode": round(t_enc / steps * 1e3, 4), "ms_per_decode": round(t_dec / steps * 1e3, 4),
         "pcie_inclusive": pcie,
+        "parity_check": check,
     }
     del sets
     return out
+
+
+# ---------------------------------------------------------------- parity check
+GOLDEN = os.path.join(ROOT, "tests", "golden", "rs_large.json")
+
+
+def golden_parity(name):
+    try:
+        return json.load(open(GOLDEN))[name]
+    except (OSError, ValueError, KeyError):
+        return None
+
+
+def check_parity_golden(parity_rows, shapes, S, seed, name):
+    """SHA-256 of every parity shard the timed launches wrote against the
+    committed oracle digests (tests/golden/rs_large.json[name]); None when no
+    golden entry covers this batch (other sizes / seeds)."""
+    import hashlib
+    g = golden_parity(name)
+    if not g or g["blocks"] != list(shapes) or g["segment_size"] != S or g["seed"] != seed:
+        return None
+    bad = []
+    for b in range(len(shapes)):
+        for j in range(3):
+            h = hashlib.sha256(parity_rows[3 * b + j].cpu().numpy().tobytes()).hexdigest()
+            if h != g["parity_sha256"][b][j]:
+                bad.append([b, j])
+    return {"golden": f"tests/golden/rs_large.json[{name}]", "shards": 3 * len(shapes),
+            "mismatched": bad, "match": not bad}
+
+
+def check_restored(sets):
+    """The restored shards of the timed decodes equal the erased originals."""
+    seg, bad = 0, []
+    for b, k in enumerate(sets.shapes):
+        for t, i in enumerate(sets.erased[b]):
+            if not sets.torch_equal(sets.restored[3 * b + t], sets.data[seg + i]):
+                bad.append([b, i])
+        seg += k
+    return {"restored_shards": sum(len(e) for e in sets.erased), "mismatched": bad, "match": not bad}
 
 
 # ---------------------------------------------------------------- host side
@@ -469,7 +515,42 @@ def cpu_baseline(args, sets, info):
     }
 
 
-def crate_api(ctx, sets, reps=3):
+def pcie_link(S, k):
+    """Host link rates on this box (torch copies of k x S bytes, best of 3) and
+    the PCIe floor they put under one crate-shaped RS(k,3) block: encode moves
+    k shards in and 3 out, a one-target decode k shards in and 1 out."""
+    import numpy as np
+    import torch
+    n = k * S
+    dev = torch.empty(n, dtype=torch.uint8, device="cuda")
+    pageable = torch.from_numpy(np.ones(n, np.uint8))
+    pinned = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+    pinned.fill_(1)
+
+    def best(f, reps=3):
+        ts = []
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            f()
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        return min(ts)
+
+    r = {"bytes": n,
+         "h2d_pageable_GBps": n / best(lambda: dev.copy_(pageable)) / 1e9,
+         "h2d_pinned_GBps": n / best(lambda: dev.copy_(pinned, non_blocking=True)) / 1e9,
+         "d2h_pinned_GBps": n / best(lambda: pinned.copy_(dev, non_blocking=True)) / 1e9,
+         "d2h_pageable_GBps": n / best(lambda: pageable.copy_(dev)) / 1e9}
+    h2d = max(r["h2d_pageable_GBps"], r["h2d_pinned_GBps"]) * 1e9
+    d2h = max(r["d2h_pageable_GBps"], r["d2h_pinned_GBps"]) * 1e9
+    r["floor_generate_parity_ms"] = (k * S / h2d + 3 * S / d2h) * 1e3
+    r["floor_recover_one_target_ms"] = (k * S / h2d + S / d2h) * 1e3
+    del dev, pageable, pinned
+    return {key: (round(v, 2) if isinstance(v, float) else v) for key, v in r.items()}
+
+
+def crate_api(ctx, sets, reps=3, staging_ab=True):
     """The per-block host-memory path BlockFrame calls:
     Chunker::generate_parity on one RS(30,3) block of 32 MiB segments
     (src/chunker/generate.rs:59-104) and recover_segment_rs30_3 of one erased
@@ -477,7 +558,11 @@ def crate_api(ctx, sets, reps=3):
     out as the Rust Vecs are.  Timed at the C-ABI (what the Rust binding
     calls): fresh, untouched output buffers per call, like the Vecs the
     reference allocates (generate.rs:95-96), so their page faults count.  The
-    Python wrappers' extra bytes() copies are reported apart (`python_wrapper_ms`)."""
+    Python wrappers' extra bytes() copies are reported apart (`python_wrapper_ms`).
+    `breakdown` times the same block through the encoder / decoder objects
+    call by call (add / encode or decode / fetch of the outputs), `link` the
+    box's PCIe rates and the floor they set, `pinned_staging` the round-2
+    staging (BFRS_CODEC_STAGING=pinned) on a second context, same block."""
     import numpy as np
     import bfrs
     S, k = sets.S, sets.shapes[0]
@@ -492,20 +577,72 @@ def crate_api(ctx, sets, reps=3):
             ts.append(time.perf_counter() - t0)
         return min(ts)
 
-    tg = timed(lambda: ch.generate_parity_into(segs, k, 3,
-                                               [np.empty(S, np.uint8) for _ in range(3)]))
+    def wrappers(c):
+        chk = bfrs.Chunker(c)
+        tg = timed(lambda: chk.generate_parity_into(segs, k, 3,
+                                                    [np.empty(S, np.uint8) for _ in range(3)]))
+        par = [np.empty(S, np.uint8) for _ in range(3)]
+        chk.generate_parity_into(segs, k, 3, par)
+        target = sets.erased[0][0]
+        slots = [None if i == target else segs[i] for i in range(k)] + [None] * (30 - k)
+        tr = timed(lambda: bfrs.recover_segment_rs30_3_into(c, slots, par, target,
+                                                            np.empty(S, np.uint8)))
+        got = np.empty(S, np.uint8)
+        assert bfrs.recover_segment_rs30_3_into(c, slots, par, target, got) == S
+        assert np.array_equal(got, segs[target]), "crate_api recover mismatch"
+        return tg, tr, par, slots, target
+
+    tg, tr, par, slots, target = wrappers(ctx)
     tg_py = timed(lambda: ch.generate_parity(segs, k, 3))
-    par = [np.empty(S, np.uint8) for _ in range(3)]
-    ch.generate_parity_into(segs, k, 3, par)
-    target = sets.erased[0][0]
-    slots = [None if i == target else segs[i] for i in range(k)] + [None] * (30 - k)
-    got = np.empty(S, np.uint8)
-    tr = timed(lambda: bfrs.recover_segment_rs30_3_into(ctx, slots, par, target,
-                                                        np.empty(S, np.uint8)))
     tr_py = timed(lambda: bfrs.recover_segment_rs30_3(ctx, slots, par, target))
-    assert bfrs.recover_segment_rs30_3_into(ctx, slots, par, target, got) == S
-    assert np.array_equal(got, segs[target]), "crate_api recover mismatch"
     gib = k * S / 2**30
+
+    def breakdown():
+        """Encoder / decoder objects call by call, best of reps each."""
+        best = {}
+
+        def upd(key, v):
+            best[key] = min(best.get(key, 1e9), v)
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            enc = bfrs.ReedSolomonEncoder(ctx, k, 3, S)
+            t1 = time.perf_counter()
+            for sgm in segs:
+                enc.add_original_shard(sgm)
+            t2 = time.perf_counter()
+            enc.encode()
+            t3 = time.perf_counter()
+            outs = [np.empty(S, np.uint8) for _ in range(3)]
+            for j in range(3):
+                outs[j][:] = enc.recovery_view(j)  # the to_vec() of generate.rs:95-96
+            t4 = time.perf_counter()
+            del enc
+            upd("encoder_new_ms", t1 - t0)
+            upd("encoder_add_ms", t2 - t1)
+            upd("encoder_encode_ms", t3 - t2)
+            upd("encoder_fetch_ms", t4 - t3)
+            t0 = time.perf_counter()
+            dec = bfrs.ReedSolomonDecoder(ctx, 30, 3, S)
+            t1 = time.perf_counter()
+            for i, sgm in enumerate(slots):
+                if sgm is not None:
+                    dec.add_original_shard(i, sgm)
+            for j in range(3):
+                dec.add_recovery_shard(j, par[j])
+            t2 = time.perf_counter()
+            dec.decode()
+            t3 = time.perf_counter()
+            out = np.empty(S, np.uint8)
+            out[:] = dec.restored_view(target)  # recovery.rs:167-169's to_vec()
+            t4 = time.perf_counter()
+            del dec
+            upd("decoder_new_ms", t1 - t0)
+            upd("decoder_add_ms", t2 - t1)
+            upd("decoder_decode_ms", t3 - t2)
+            upd("decoder_fetch_ms", t4 - t3)
+        return {key: round(v * 1e3, 2) for key, v in best.items()}
+
+    bd = breakdown()
     # rayon's shape (commit.rs:391-466): one generate_parity per block, all of
     # C2's blocks at once from worker threads sharing the one context (ctypes
     # drops the GIL for the call)
@@ -534,13 +671,15 @@ def crate_api(ctx, sets, reps=3):
         t_par.append(time.perf_counter() - t0)
     assert not errors, errors
     par_gib = sum(sets.shapes) * S / 2**30
-    return {
+    res = {
+        "staging": os.environ.get("BFRS_CODEC_STAGING", "direct"),
         "generate_parity": {"ms": round(tg * 1e3, 2), "GiBps": round(gib / tg, 2),
                             "python_wrapper_ms": round(tg_py * 1e3, 2),
                             "what": f"RS({k},3) block of {S >> 20} MiB segments, pageable host in/out"},
         "recover_segment_rs30_3": {"ms": round(tr * 1e3, 2), "GiBps_of_block": round(gib / tr, 2),
                                    "python_wrapper_ms": round(tr_py * 1e3, 2),
                                    "what": "one erased segment of that block, pageable host in/out"},
+        "breakdown": bd,
         "generate_parity_all_blocks_threads": {
             "ms": round(min(t_par) * 1e3, 2), "GiBps": round(par_gib / min(t_par), 2),
             "what": f"{len(blocks)} blocks ({'+'.join(map(str, sets.shapes))} x {S >> 20} MiB) "
@@ -549,6 +688,26 @@ def crate_api(ctx, sets, reps=3):
         "reps": reps, "timing": "C-ABI call (bfrs_generate_parity / bfrs_recover_segment_rs30_3) "
                                 "through ctypes, fresh output buffers, best of reps, wall clock",
     }
+    res["link"] = pcie_link(S, k)
+    if staging_ab:
+        old = os.environ.get("BFRS_CODEC_STAGING")
+        os.environ["BFRS_CODEC_STAGING"] = "pinned"
+        try:
+            c2 = bfrs.Context(ctx.device)
+        finally:
+            if old is None:
+                del os.environ["BFRS_CODEC_STAGING"]
+            else:
+                os.environ["BFRS_CODEC_STAGING"] = old
+        try:
+            pg, pr, *_ = wrappers(c2)
+        finally:
+            c2.close()
+        res["pinned_staging"] = {"generate_parity_ms": round(pg * 1e3, 2),
+                                 "recover_segment_rs30_3_ms": round(pr * 1e3, 2),
+                                 "what": "BFRS_CODEC_STAGING=pinned (round 2: memcpy into pinned "
+                                         "rows, then H2D), second context, same block"}
+    return res
 
 
 def pcie_inclusive(ctx, sets, steps=2, rt=None, job_bytes=None):
@@ -793,7 +952,10 @@ def main():
         lo_b, hi_b = parallel.stripe_ranges(S_full, rt.world)[rt.rank]
         S, seed = hi_b - lo_b, 0xB10C
     else:
-        lo_b, S, seed = 0, S_full, 0xB10C + rt.rank
+        # every rank encodes the golden batch (seed 0xB10C, tests/golden/
+        # rs_large.json): each GPU computes its own copy, so each can be
+        # checked bit-exact against the committed digests after the timed region
+        lo_b, S, seed = 0, S_full, 0xB10C
     sets = ShardSets(rt, shapes, S, args.layout, args.pitch)
     fill(rt, sets, seed, lo_b, S_full)
 
@@ -863,7 +1025,13 @@ def main():
         copy_ms = per_launch(lambda _h: cp_dst.copy_(cp_src))
         del cp_src, cp_dst
     rt.sync()
-    sets.check_restored()  # correctness guard on the measured buffers (on device)
+    # correctness of the measured buffers: every rank's parity against the
+    # golden digests, every rank's restored shards against its originals
+    my_check = {"encode": (check_parity_golden(sets.parity, shapes, S, seed, "c2_128x32MiB")
+                           if not rt.stub else None),
+                "decode": check_restored(sets)}
+    ok_here = my_check["decode"]["match"] and (my_check["encode"] or {}).get("match") is not False
+    ranks_ok = rt.gather_over_ranks(1.0 if ok_here else 0.0)
     data_bytes = sum(shapes) * S                     # original data per direction (this rank)
     alg_bytes = sum(k + 3 for k in shapes) * S        # HBM bytes per launch (both directions)
     scaling = "strong" if args.strong else "weak"
@@ -876,7 +1044,7 @@ def main():
 
     if rt.rank != 0:
         rt.close()
-        return 0
+        return 0 if ok_here else 3
 
     n1 = rt.world == 1
     info = host_info()
@@ -918,7 +1086,7 @@ def main():
         "vs_baseline": None,
         "dtype": "u8",
         "data": ("STUB (CPU rehearsal of the launcher, not a measurement)" if rt.stub else
-                 "synthetic splitmix64 bytes (seed 0xB10C+rank), resident in HBM"),
+                 "synthetic splitmix64 bytes (seed 0xB10C on every rank), resident in HBM"),
         "config": {
             "workload": ("BASELINE configs[3]: 10 GiB archive, 320 x 32 MiB segments = "
                          "10xRS(30,3)+1xRS(20,3), column-striped over the GPUs"
@@ -960,11 +1128,22 @@ def main():
         line["pcie_inclusive"] = pcie
         line["c5"] = c5
     line["c4_strong"] = c4
+    line["parity_check"] = {
+        "c2_encode": my_check["encode"], "c3_decode": my_check["decode"],
+        "ranks_ok": [bool(x) for x in ranks_ok],
+        "c4_encode": (c4 or {}).get("parity_check", {}).get("encode"),
+        "c4_decode": (c4 or {}).get("parity_check", {}).get("decode"),
+        "c5_blake3": None if c5 is None else c5.get("blake3_match"),
+        "when": "after the timed region, on the buffers the timed launches wrote",
+    }
+    flags = [all(ranks_ok), (my_check["encode"] or {}).get("match"),
+             (c4 or {}).get("parity_check", {}).get("encode", {}).get("match"),
+             (c4 or {}).get("parity_check", {}).get("decode", {}).get("match"),
+             None if c5 is None else c5.get("blake3_match")]
+    line["parity_check"]["all_ok"] = not any(f is False for f in flags)
     print(json.dumps(line), flush=True)
     rt.close()
-    if c5 is not None and c5.get("blake3_match") is False:
-        return 1
-    return 0
+    return 0 if line["parity_check"]["all_ok"] else 1
 
 
 def sets_pitch(S, args, rt):

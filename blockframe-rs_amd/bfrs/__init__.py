@@ -453,6 +453,25 @@ def _stream_handle(stream, tensors=()) -> Optional[int]:
     return stream.cuda_stream  # torch.cuda.Stream
 
 
+def _live_codec(obj):
+    """The object's handle; its context must still be open (include/bfrs.h:
+    a codec object may only be freed after bfrs_close)."""
+    if not getattr(obj, "handle", None):
+        raise BfrsError(E_INVALID_ARGUMENT, "codec object already freed")
+    if not obj.ctx.handle:
+        raise BfrsError(E_INVALID_ARGUMENT, "the codec object's context is closed")
+    return obj.handle
+
+
+def _view(fn, handle, index):
+    import numpy as np
+    p, n = ctypes.c_void_p(), _sz()
+    _check(fn(handle, index, ctypes.byref(p), ctypes.byref(n)))
+    a = np.ctypeslib.as_array((ctypes.c_uint8 * n.value).from_address(p.value))
+    a.flags.writeable = False
+    return a
+
+
 class ReedSolomonEncoder:
     """reed_solomon_simd::ReedSolomonEncoder over the HIP path."""
 
@@ -467,18 +486,26 @@ class ReedSolomonEncoder:
             lib().bfrs_encoder_free(self.handle)
             self.handle = None
 
+    def _h(self):
+        return _live_codec(self)
+
     def add_original_shard(self, shard) -> None:
         a = _as_np(shard)
-        _check(lib().bfrs_encoder_add_original_shard(self.handle, a.ctypes.data, a.size))
+        _check(lib().bfrs_encoder_add_original_shard(self._h(), a.ctypes.data, a.size))
 
     def encode(self) -> "ReedSolomonEncoder":
-        _check(lib().bfrs_encoder_encode(self.handle))
+        _check(lib().bfrs_encoder_encode(self._h()))
         return self
+
+    def recovery_view(self, index: int):
+        """Recovery shard `index` as a read-only numpy view of the encoder's
+        pinned row (valid until the next call on this encoder), no copy."""
+        return _view(lib().bfrs_encoder_recovery, self._h(), index)
 
     def recovery_iter(self):
         for j in range(self.recovery_count):
             p, n = ctypes.c_void_p(), _sz()
-            _check(lib().bfrs_encoder_recovery(self.handle, j, ctypes.byref(p), ctypes.byref(n)))
+            _check(lib().bfrs_encoder_recovery(self._h(), j, ctypes.byref(p), ctypes.byref(n)))
             yield ctypes.string_at(p, n.value)
 
 
@@ -496,21 +523,34 @@ class ReedSolomonDecoder:
             lib().bfrs_decoder_free(self.handle)
             self.handle = None
 
+    def _h(self):
+        return _live_codec(self)
+
     def add_original_shard(self, index: int, shard) -> None:
         a = _as_np(shard)
-        _check(lib().bfrs_decoder_add_original_shard(self.handle, index, a.ctypes.data, a.size))
+        _check(lib().bfrs_decoder_add_original_shard(self._h(), index, a.ctypes.data, a.size))
 
     def add_recovery_shard(self, index: int, shard) -> None:
         a = _as_np(shard)
-        _check(lib().bfrs_decoder_add_recovery_shard(self.handle, index, a.ctypes.data, a.size))
+        _check(lib().bfrs_decoder_add_recovery_shard(self._h(), index, a.ctypes.data, a.size))
 
     def decode(self) -> "ReedSolomonDecoder":
-        _check(lib().bfrs_decoder_decode(self.handle))
+        _check(lib().bfrs_decoder_decode(self._h()))
         return self
+
+    def restored_view(self, index: int):
+        """Restored original `index` as a read-only numpy view (valid until the
+        next add/decode call), or None if it was not restored."""
+        try:
+            return _view(lib().bfrs_decoder_restored_original, self._h(), index)
+        except BfrsError as e:
+            if e.code == E_NOT_RESTORED:
+                return None
+            raise
 
     def restored_original(self, index: int) -> Optional[bytes]:
         p, n = ctypes.c_void_p(), _sz()
-        rc = lib().bfrs_decoder_restored_original(self.handle, index, ctypes.byref(p),
+        rc = lib().bfrs_decoder_restored_original(self._h(), index, ctypes.byref(p),
                                                   ctypes.byref(n))
         if rc == E_NOT_RESTORED:
             return None

@@ -603,8 +603,48 @@ struct bfrs_archive {
   std::string seg_path(size_t gi) const;
   int load_clean(size_t gi, SegPtr *out, bool *ok);  // no locks held
   int recover(size_t gi, SegPtr *out);              // no locks held
+  // Verify segment gi (and reconstruct it if damaged) with mu released,
+  // holding gi in `inflight` so that other readers wait for it.  Every exit,
+  // an exception included, re-locks, drops gi from inflight and wakes the
+  // waiters; an exception becomes an error code here (a prefetch thread has
+  // nobody to catch it).  *verified: the file was clean; *restored: rebuilt.
+  int load_inflight(std::unique_lock<std::mutex> &l, size_t gi, SegPtr *seg, bool *verified,
+                    bool *restored);
   void prefetch_loop();
 };
+
+int bfrs_archive::load_inflight(std::unique_lock<std::mutex> &l, size_t gi, SegPtr *seg,
+                                bool *verified, bool *restored) {
+  inflight.insert(gi);
+  struct Done {
+    bfrs_archive *a;
+    std::unique_lock<std::mutex> &l;
+    size_t gi;
+    ~Done() {
+      if (!l.owns_lock()) l.lock();
+      a->inflight.erase(gi);
+      a->cv.notify_all();
+    }
+  } done{this, l, gi};
+  *verified = *restored = false;
+  l.unlock();
+  int rc;
+  try {
+    rc = load_clean(gi, seg, verified);
+    if (rc == BFRS_OK && !*verified) {
+      rc = recover(gi, seg);
+      *restored = rc == BFRS_OK;
+    }
+  } catch (const std::bad_alloc &) {
+    rc = set_error(BFRS_E_NOMEM, "host memory allocation failed");
+  } catch (const std::exception &ex) {
+    rc = set_error(BFRS_E_WRAPPER, std::string("internal error: ") + ex.what());
+  } catch (...) {
+    rc = set_error(BFRS_E_WRAPPER, "internal error");
+  }
+  l.lock();
+  return rc;
+}
 
 std::string bfrs_archive::expected_hash(size_t gi) const {
   const Manifest &mf = g.mf;
@@ -725,24 +765,16 @@ void bfrs_archive::prefetch_loop() {
     const size_t gi = wantq.front();
     wantq.pop_front();
     if (cache.count(gi) || inflight.count(gi)) continue;
-    inflight.insert(gi);
-    l.unlock();
+    // damaged: reconstructed (with its block's siblings) ahead of the reader;
+    // a failure is left to the reader, which loads the segment itself
     SegPtr seg;
-    bool ok = false;
-    int rc = load_clean(gi, &seg, &ok);
-    bool restored = false;
-    if (rc == BFRS_OK && !ok) {  // damaged: reconstruct it (and its block's siblings) ahead of the reader
-      rc = recover(gi, &seg);
-      restored = rc == BFRS_OK;
-    }
-    l.lock();
+    bool ok = false, restored = false;
+    const int rc = load_inflight(l, gi, &seg, &ok, &restored);
     if (rc == BFRS_OK && (ok || restored)) {
       put(gi, seg);
       st.verified += ok;
       ++st.prefetched;
     }
-    inflight.erase(gi);
-    cv.notify_all();
   }
 }
 
@@ -1229,14 +1261,8 @@ int bfrs_archive_read(bfrs_archive *a, uint64_t offset, size_t len, uint8_t *out
       ++a->st.misses;
       // queued but not started: load it here instead
       a->wantq.erase(std::remove(a->wantq.begin(), a->wantq.end(), gi), a->wantq.end());
-      a->inflight.insert(gi);
-      l.unlock();
-      bool ok = false;
-      int rc = a->load_clean(gi, &seg, &ok);
-      if (rc == BFRS_OK && !ok) rc = a->recover(gi, &seg);
-      l.lock();
-      a->inflight.erase(gi);
-      a->cv.notify_all();
+      bool ok = false, restored = false;
+      const int rc = a->load_inflight(l, gi, &seg, &ok, &restored);
       if (rc) return rc;
       if (ok) ++a->st.verified;
       a->put(gi, seg);

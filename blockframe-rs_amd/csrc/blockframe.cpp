@@ -60,15 +60,11 @@ int bfrs_generate_parity(bfrs_ctx *ctx, const uint8_t *const *segments, const si
     }
     if ((rc = bfrs_encoder_add_original_shard(enc.p, src, max_len))) return rc;
   }
-  if ((rc = bfrs_encoder_encode(enc.p))) return rc;  // generate.rs:92
-  for (size_t j = 0; j < parity_shards; ++j) {       // generate.rs:95-96
-    const uint8_t *data;
-    size_t len;
-    if ((rc = bfrs_encoder_recovery(enc.p, j, &data, &len))) return rc;
+  for (size_t j = 0; j < parity_shards; ++j)
     if (!parity_out[j]) return set_error(BFRS_E_INVALID_ARGUMENT, "parity buffer is NULL");
-    host_copy(parity_out[j], data, len);
-  }
-  return BFRS_OK;
+  // generate.rs:92 + 95-96: encode, the recovery shards straight into the
+  // caller's buffers (the reference's to_vec copies)
+  return encoder_encode_to_host(enc.p, parity_out);
   BFRS_API_END
 }
 
@@ -92,15 +88,9 @@ int bfrs_generate_parity_segmented(bfrs_ctx *ctx, const uint8_t *segment, size_t
     rc = bfrs_encoder_add_original_shard(enc.p, segment, padded);
   }
   if (rc) return rc;
-  if ((rc = bfrs_encoder_encode(enc.p))) return rc;
-  for (size_t j = 0; j < 3; ++j) {
-    const uint8_t *data;
-    size_t n;
-    if ((rc = bfrs_encoder_recovery(enc.p, j, &data, &n))) return rc;
+  for (size_t j = 0; j < 3; ++j)
     if (!parity_out[j]) return set_error(BFRS_E_INVALID_ARGUMENT, "parity buffer is NULL");
-    std::memcpy(parity_out[j], data, n);
-  }
-  return BFRS_OK;
+  return encoder_encode_to_host(enc.p, parity_out);
   BFRS_API_END
 }
 
@@ -171,13 +161,11 @@ int bfrs_recover_segment_rs30_3(bfrs_ctx *ctx, const uint8_t *const *segments,
     if ((rc = bfrs_decoder_add_recovery_shard(dec.p, j, block_parity[j], parity_lens[j])))
       return rc;
   if ((rc = bfrs_decoder_decode(dec.p))) return rc;
-  const uint8_t *data;
-  size_t len;
-  if (bfrs_decoder_restored_original(dec.p, target_index, &data, &len))
-    return wrapper_error("Failed to restore target segment");
+  // recovery.rs:166-170: only the target leaves the device, straight into out
   if (!out) return set_error(BFRS_E_INVALID_ARGUMENT, "out is NULL");
-  host_copy(out, data, len);
-  *out_len = len;
+  if (decoder_restored_to_host(dec.p, target_index, out))
+    return wrapper_error("Failed to restore target segment");
+  *out_len = shard_size;
   return BFRS_OK;
   BFRS_API_END
 }

@@ -3,15 +3,21 @@
 // reference uses it (src/chunker/generate.rs:37-49,84-96;
 // src/filestore/recovery.rs:58-69,152-170; src/filestore/health.rs:733-752).
 //
-// Each object holds a CodecSlot from its context's cache (runtime.hpp): k + m
+// Each object holds a CodecSlot from its context's pool (runtime.hpp): k + m
 // shard rows of HBM, the same rows of pinned host memory, and a stream of its
-// own.  add_*_shard copies the caller's bytes into the pinned row (the crate
-// likewise copies each added shard into its work area, so the caller may
-// reuse its buffer at once) and queues the row's H2D copy, so the copy of
-// shard i+1 overlaps the DMA of shard i.  encode()/decode() queue the HIP
-// pass and the D2H of the results into pinned rows; results stay valid until
-// the next call on the object.  Objects are used by one thread at a time;
-// objects of one context may live on different threads.
+// own.  add_*_shard moves the caller's bytes to the shard's device row before
+// it returns (the crate likewise copies each added shard into its work area,
+// so the caller may reuse its buffer at once): by default one DMA straight
+// from the caller's buffer (Staging::kDirect); BFRS_CODEC_STAGING=pinned
+// copies into the pinned row first and queues its H2D (round 2's path,
+// DESIGN.md §7c).  encode() queues the HIP pass and the D2H of the recovery
+// shards into pinned rows; decode() runs the pass and restored_original(i)
+// fetches row i on first use (BlockFrame asks for one target,
+// recovery.rs:166-170).  Results stay valid until the next call on the
+// object.  Objects are used by one thread at a time; objects of one context
+// may live on different threads.  An object holds its context's slot pool
+// (shared), so it may be freed after bfrs_close; every other call needs the
+// context open.
 #include <algorithm>
 #include <cstring>
 #include <sstream>
@@ -31,22 +37,36 @@ int shard_size_error(size_t expected, size_t got) {
 
 struct CodecObject {
   bfrs_ctx *ctx;
+  std::shared_ptr<CodecPool> pool;
   size_t k, m, shard_bytes;
   std::unique_ptr<CodecSlot> slot;
   uint8_t *d_row(size_t i) const { return static_cast<uint8_t *>(slot->d) + i * slot->stride; }
   uint8_t *h_row(size_t i) const { return slot->h + i * slot->stride; }
-  // stage a host shard into row i (pinned copy + async H2D on the slot stream)
+  int acquire(bfrs_ctx *c, size_t k_, size_t m_, size_t bytes) {
+    ctx = c;
+    pool = c->impl.codec_pool;
+    k = k_;
+    m = m_;
+    shard_bytes = bytes;
+    return pool->acquire(k + m, shard_bytes, &slot);
+  }
+  // Stage a host shard into device row i; the caller's buffer is free again
+  // on return.
   int stage(size_t i, const uint8_t *src, size_t len) {
-    HIP_TRY(hipSetDevice(ctx->impl.device));
-    // the row's previous H2D (an earlier round on this object) must be done
-    // before its pinned bytes are overwritten: rows are reused only after
-    // encode()/decode() synchronised the stream, so no wait is needed here
-    host_copy(h_row(i), src, len);
-    HIP_TRY(hipMemcpyAsync(d_row(i), h_row(i), len, hipMemcpyHostToDevice, slot->stream));
+    HIP_TRY(hipSetDevice(pool->device));
+    if (pool->staging == Staging::kPinned) {
+      // the row's previous H2D (an earlier round on this object) is done:
+      // rows are reused only after encode()/decode() synchronised the stream
+      host_copy(h_row(i), src, len);
+      HIP_TRY(hipMemcpyAsync(d_row(i), h_row(i), len, hipMemcpyHostToDevice, slot->stream));
+    } else {
+      HIP_TRY(hipMemcpyAsync(d_row(i), src, len, hipMemcpyHostToDevice, slot->stream));
+      HIP_TRY(hipStreamSynchronize(slot->stream));
+    }
     return BFRS_OK;
   }
   ~CodecObject() {
-    if (slot) ctx->impl.codec_release(std::move(slot));
+    if (slot) pool->release(std::move(slot));
   }
 };
 
@@ -55,11 +75,13 @@ struct CodecObject {
 struct bfrs_encoder : CodecObject {
   size_t received = 0;
   bool encoded = false;
+  bool fetched_to_pinned = false;  // the pinned rows k.. hold the recovery shards
 };
 
 struct bfrs_decoder : CodecObject {
   std::vector<uint8_t> orig_present, rec_present;
-  std::vector<uint8_t> restored;  // 1 = row i holds a restored original (pinned)
+  std::vector<uint8_t> restored;  // 1 = device row i holds a restored original
+  std::vector<uint8_t> fetched;   // 1 = its pinned row holds it too
   bool decoded = false;
 };
 
@@ -73,11 +95,7 @@ int bfrs_encoder_new(bfrs_ctx *ctx, size_t k, size_t m, size_t shard_bytes, bfrs
   if (rc) return rc;
   auto *e = new (std::nothrow) bfrs_encoder;
   if (!e) return set_error(BFRS_E_NOMEM, "encoder allocation failed");
-  e->ctx = ctx;
-  e->k = k;
-  e->m = m;
-  e->shard_bytes = shard_bytes;
-  if ((rc = ctx->impl.codec_acquire(k + m, shard_bytes, &e->slot))) {
+  if ((rc = e->acquire(ctx, k, m, shard_bytes))) {
     delete e;
     return rc;
   }
@@ -106,9 +124,11 @@ int bfrs_encoder_add_original_shard(bfrs_encoder *e, const uint8_t *shard, size_
   BFRS_API_END
 }
 
-int bfrs_encoder_encode(bfrs_encoder *e) {
-  BFRS_API_BEGIN
-  if (!e) return set_error(BFRS_E_INVALID_ARGUMENT, "encode: NULL encoder");
+}  // extern "C"
+
+namespace {
+// Queue the encode pass of a fully staged encoder on its slot stream.
+int encoder_run(bfrs_encoder *e) {
   if (e->received < e->k || e->encoded) {
     std::ostringstream os;
     os << "too few original shards: got " << (e->encoded ? 0 : e->received)
@@ -120,13 +140,46 @@ int bfrs_encoder_encode(bfrs_encoder *e) {
   for (size_t i = 0; i < e->k; ++i) din[i] = e->d_row(i);
   for (size_t j = 0; j < e->m; ++j) dout[j] = e->d_row(e->k + j);
   const uint32_t kk = uint32_t(e->k);
-  hipStream_t st = e->slot->stream;
-  int rc = encode_batch_on(e->ctx, 1, &kk, e->m, e->shard_bytes, din.data(), dout.data(), st);
+  return encode_batch_on(e->ctx, 1, &kk, e->m, e->shard_bytes, din.data(), dout.data(),
+                         e->slot->stream);
+}
+}  // namespace
+
+int bfrs::encoder_encode_to_host(bfrs_encoder *e, uint8_t *const *outs) {
+  int rc = encoder_run(e);
   if (rc) return rc;
+  hipStream_t st = e->slot->stream;
+  for (size_t j = 0; j < e->m; ++j) {
+    if (e->pool->staging == Staging::kPinned)  // round 2: pinned row, then a host copy
+      HIP_TRY(hipMemcpyAsync(e->h_row(e->k + j), e->d_row(e->k + j), e->shard_bytes,
+                             hipMemcpyDeviceToHost, st));
+    else
+      HIP_TRY(hipMemcpyAsync(outs[j], e->d_row(e->k + j), e->shard_bytes, hipMemcpyDeviceToHost, st));
+  }
+  HIP_TRY(hipStreamSynchronize(st));
+  if (e->pool->staging == Staging::kPinned)
+    for (size_t j = 0; j < e->m; ++j) host_copy(outs[j], e->h_row(e->k + j), e->shard_bytes);
+  // the pinned rows do not hold the recovery shards: the object is spent
+  // (the next add_original_shard starts a new round, as after encode())
+  e->encoded = true;
+  e->fetched_to_pinned = e->pool->staging == Staging::kPinned;
+  return BFRS_OK;
+}
+
+extern "C" {
+
+int bfrs_encoder_encode(bfrs_encoder *e) {
+  BFRS_API_BEGIN
+  if (!e) return set_error(BFRS_E_INVALID_ARGUMENT, "encode: NULL encoder");
+  int rc = encoder_run(e);
+  if (rc) return rc;
+  hipStream_t st = e->slot->stream;
   for (size_t j = 0; j < e->m; ++j)
-    HIP_TRY(hipMemcpyAsync(e->h_row(e->k + j), dout[j], e->shard_bytes, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(e->h_row(e->k + j), e->d_row(e->k + j), e->shard_bytes,
+                           hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   e->encoded = true;
+  e->fetched_to_pinned = true;
   return BFRS_OK;
   BFRS_API_END
 }
@@ -134,7 +187,7 @@ int bfrs_encoder_encode(bfrs_encoder *e) {
 int bfrs_encoder_recovery(bfrs_encoder *e, size_t index, const uint8_t **data, size_t *len) {
   BFRS_API_BEGIN
   if (!e || !data || !len) return set_error(BFRS_E_INVALID_ARGUMENT, "recovery: NULL argument");
-  if (!e->encoded || index >= e->m) {
+  if (!e->encoded || !e->fetched_to_pinned || index >= e->m) {
     std::ostringstream os;
     os << "invalid recovery shard index: " << index << " >= recovery_count " << e->m;
     return set_error(BFRS_E_INVALID_RECOVERY_SHARD_INDEX, os.str());
@@ -155,13 +208,9 @@ int bfrs_decoder_new(bfrs_ctx *ctx, size_t k, size_t m, size_t shard_bytes, bfrs
   if (rc) return rc;
   auto *d = new (std::nothrow) bfrs_decoder;
   if (!d) return set_error(BFRS_E_NOMEM, "decoder allocation failed");
-  d->ctx = ctx;
-  d->k = k;
-  d->m = m;
-  d->shard_bytes = shard_bytes;
   d->orig_present.assign(k, 0);
   d->rec_present.assign(m, 0);
-  if ((rc = ctx->impl.codec_acquire(k + m, shard_bytes, &d->slot))) {
+  if ((rc = d->acquire(ctx, k, m, shard_bytes))) {
     delete d;
     return rc;
   }
@@ -174,6 +223,7 @@ static void decoder_reset_if_done(bfrs_decoder *d) {
   if (d->decoded) {
     d->decoded = false;
     d->restored.clear();
+    d->fetched.clear();
     std::fill(d->orig_present.begin(), d->orig_present.end(), 0);
     std::fill(d->rec_present.begin(), d->rec_present.end(), 0);
   }
@@ -238,6 +288,7 @@ int bfrs_decoder_decode(bfrs_decoder *d) {
     return set_error(BFRS_E_NOT_ENOUGH_SHARDS, os.str());
   }
   d->restored.assign(d->k, 0);
+  d->fetched.assign(d->k, 0);
   d->decoded = true;
   hipStream_t st = d->slot->stream;
   if (orig_recv == d->k) {  // nothing to restore; the staged copies still have to land
@@ -259,12 +310,8 @@ int bfrs_decoder_decode(bfrs_decoder *d) {
   int rc = decode_batch_on(d->ctx, 1, &kk, d->m, d->shard_bytes, dorig.data(), drec.data(),
                            drest.data(), st);
   if (rc) return rc;
-  for (size_t i = 0; i < d->k; ++i)
-    if (!d->orig_present[i]) {
-      HIP_TRY(hipMemcpyAsync(d->h_row(i), drest[i], d->shard_bytes, hipMemcpyDeviceToHost, st));
-      d->restored[i] = 1;
-    }
   HIP_TRY(hipStreamSynchronize(st));
+  for (size_t i = 0; i < d->k; ++i) d->restored[i] = !d->orig_present[i];
   return BFRS_OK;
   BFRS_API_END
 }
@@ -278,6 +325,13 @@ int bfrs_decoder_restored_original(bfrs_decoder *d, size_t index, const uint8_t 
   *len = 0;
   if (!d->decoded || index >= d->restored.size() || !d->restored[index])
     return set_error(BFRS_E_NOT_RESTORED, "original shard was not restored");
+  if (!d->fetched[index]) {  // D2H of this row on first use
+    HIP_TRY(hipSetDevice(d->pool->device));
+    HIP_TRY(hipMemcpyAsync(d->h_row(index), d->d_row(index), d->shard_bytes, hipMemcpyDeviceToHost,
+                           d->slot->stream));
+    HIP_TRY(hipStreamSynchronize(d->slot->stream));
+    d->fetched[index] = 1;
+  }
   *data = d->h_row(index);
   *len = d->shard_bytes;
   return BFRS_OK;
@@ -287,3 +341,21 @@ int bfrs_decoder_restored_original(bfrs_decoder *d, size_t index, const uint8_t 
 void bfrs_decoder_free(bfrs_decoder *d) { delete d; }
 
 }  // extern "C"
+
+int bfrs::decoder_restored_to_host(bfrs_decoder *d, size_t index, uint8_t *out) {
+  if (!d->decoded || index >= d->restored.size() || !d->restored[index])
+    return set_error(BFRS_E_NOT_RESTORED, "original shard was not restored");
+  if (d->pool->staging == Staging::kPinned || d->fetched[index]) {  // via the pinned row
+    const uint8_t *data;
+    size_t len;
+    int rc = bfrs_decoder_restored_original(d, index, &data, &len);
+    if (rc) return rc;
+    host_copy(out, data, len);
+    return BFRS_OK;
+  }
+  HIP_TRY(hipSetDevice(d->pool->device));
+  HIP_TRY(hipMemcpyAsync(out, d->d_row(index), d->shard_bytes, hipMemcpyDeviceToHost,
+                         d->slot->stream));
+  HIP_TRY(hipStreamSynchronize(d->slot->stream));
+  return BFRS_OK;
+}

@@ -65,7 +65,11 @@ static_assert(sizeof(KernArgs) <= 4096, "kernel arguments must fit 4 KiB");
 
 // Column bytes one workgroup tile covers in the selected kernel variant.
 uint32_t tile_bytes();
+// The kernel BFRS_KERNEL_VARIANT selects (76 when unset), or -1 when this
+// build does not carry that variant (the product library: 76, 75 and 73 only;
+// the A/B variants live in libbfrs_ab.so, rs_kernels.hip).
 int kernel_variant();
+bool ab_build();
 
 // subfield: every pass of the launch has GF(2^8)-subfield coefficients
 // (PlanPass::subfield), so the subfield kernel form may run.

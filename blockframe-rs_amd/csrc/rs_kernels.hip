@@ -133,6 +133,7 @@ __device__ __forceinline__ void mac_input_sub(const uint4 &L, const uint4 &H, ui
   }
 }
 
+#ifdef BFRS_AB_VARIANTS
 // Traffic-only probe (measurement only, NOT a codec): same memory traffic, no tables.
 // The XORs are asm so the compiler cannot fold "0 ^ load" into a register
 // copy of a load that is still in flight (tools/inflight_check.py).
@@ -153,6 +154,7 @@ __device__ __forceinline__ uint32_t gather_byte(const uint32_t (&acc)[16], int d
   return ((acc[4 * d + 0] >> sh) & 0xFF) | (((acc[4 * d + 1] >> sh) & 0xFF) << 8) |
          (((acc[4 * d + 2] >> sh) & 0xFF) << 16) | (((acc[4 * d + 3] >> sh) & 0xFF) << 24);
 }
+#endif  // BFRS_AB_VARIANTS
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -191,6 +193,7 @@ __device__ __forceinline__ void store16_nt(uint64_t a, const u32x4 &v) {
 // 32-bit lane offset.  The compiler does not know an asm output is written
 // asynchronously, so no code may copy or spill a destination register before
 // its wait (tools/inflight_check.py, tests/test_isa_hazards.py).
+#ifdef BFRS_AB_VARIANTS  // round-1 half-chunk layout (A/B build only)
 // LPOL 1: non-temporal (streaming) cache policy on the loads.
 template <int LPOL = 0>
 __device__ __forceinline__ void gload_half_chunk(u32x4 &L, u32x4 &H, uint64_t base,
@@ -210,6 +213,8 @@ __device__ __forceinline__ void gload_half_chunk(u32x4 &L, u32x4 &H, uint64_t ba
         : "v"(voff), "s"(base)
         : "memory");
 }
+
+#endif  // BFRS_AB_VARIANTS
 
 // Wait until at most N vector-memory ops are outstanding; L/H are in/out
 // operands so no consumer can be scheduled above the wait.
@@ -286,6 +291,7 @@ __device__ __forceinline__ void input_ring(uint32_t n_in, const Load &load, cons
   vm_wait<0>(LA, HA);
 }
 
+#ifdef BFRS_AB_VARIANTS  // round-1 half-chunk layout (A/B build only)
 // Lane layout: lane = one 32-byte half-chunk, 16 B at +0 (low bytes) and
 // 16 B at +32 (high bytes): every 128-B line is touched by two instructions.
 // Accumulates lane `lane` (0..255) of `tile`; false if the lane's half-chunk
@@ -331,6 +337,8 @@ __device__ __forceinline__ bool ring_acc_halfchunk(const KernArgs &args, const P
       });
   return true;
 }
+
+#endif  // BFRS_AB_VARIANTS
 
 // ---- contiguous-line layout (LAY 1, round 2) --------------------------------
 // Every load / store instruction covers 1 KiB of contiguous columns (16 whole
@@ -439,10 +447,15 @@ __device__ __forceinline__ bool ring_acc_ct(const KernArgs &args, const PassDesc
         const uint32_t r = SLOTS ? x : idx(x);
         u32x4 L = Av, H = Bv;
         halves_swap(L, H);
+#ifdef BFRS_AB_VARIANTS
         if constexpr (PROBE)  // traffic-only probe (measurement, NOT a codec)
           mac_input_stream(make_uint4(L.x, L.y, L.z, L.w), make_uint4(H.x, H.y, H.z, H.w), acc_lo,
                            acc_hi);
-        else if constexpr (SUB)
+        else
+#else
+        static_assert(!PROBE, "traffic-only probes exist only in the A/B build");
+#endif
+        if constexpr (SUB)
           mac_input_sub(make_uint4(L.x, L.y, L.z, L.w), make_uint4(H.x, H.y, H.z, H.w), 2 * r,
                         2 * r + 1, acc_lo, acc_hi);
         else
@@ -488,6 +501,7 @@ __device__ __forceinline__ void ring_tile_ct(const KernArgs &args, const PassDes
   }
 }
 
+#ifdef BFRS_AB_VARIANTS  // round-1 half-chunk layout (A/B build only)
 template <int LPOL, int SPOL, int ROT = 0, bool PROBE = false>
 __device__ __forceinline__ void ring_tile_halfchunk(const KernArgs &args, const PassDesc &P,
                                                     uint32_t tile, uint32_t wave_id) {
@@ -511,6 +525,8 @@ __device__ __forceinline__ void ring_tile_halfchunk(const KernArgs &args, const 
     store16_pol<SPOL>(dst + 32, u32x4{oh.x, oh.y, oh.z, oh.w});
   }
 }
+
+#endif  // BFRS_AB_VARIANTS
 
 // The ring kernel: workgroup wg owns tiles_per_wg consecutive 8 KiB tiles of
 // one pass (one by default); ROT picks the read order (ring_acc_halfchunk).
@@ -540,10 +556,14 @@ __global__ __launch_bounds__(256, 5) void gf_apply_ring_kernel(const KernArgs ar
   const uint32_t t_end = min(t_begin + args.tiles_per_wg, P.n_tiles);
   const uint32_t wave_id = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   for (uint32_t tile = t_begin; tile < t_end; ++tile) {
-    if constexpr (LAY == 1)
-      ring_tile_ct<LPOL, 1, ROT, PROBE, TAIL, SUB>(args, P, tile, wave_id);
-    else
+#ifdef BFRS_AB_VARIANTS
+    if constexpr (LAY == 0)
       ring_tile_halfchunk<0, 1, ROT, PROBE>(args, P, tile, wave_id);
+    else
+#else
+    static_assert(LAY == 1, "the half-chunk layout exists only in the A/B build");
+#endif
+    ring_tile_ct<LPOL, 1, ROT, PROBE, TAIL, SUB>(args, P, tile, wave_id);
   }
 }
 
@@ -834,39 +854,95 @@ __global__ __launch_bounds__(64) void gf_tail_kernel(const KernArgs args) {
 
 }  // namespace
 
-// Kernel variant selector for A/B measurement (tools/kbench.py).
-// 76 (default, round 2): contiguous-line loads/stores with lane-half swaps,
-// non-temporal loads, and for GF(2^8)-subfield launches (every RS(k<=30,3)
-// encode/decode) the fully unrolled SDWA-addressed kernel for n_in 30 / 8,
-// read groups of 64 consecutive tiles (512 KiB of every shard's columns) on
-// one XCD; other launches fall back to 75 (looped, subfield) or 73 (looped,
-// general).  77: 76 with 4-byte low-byte lookups (2-way LDS bank conflicts);
-// 78-80: read groups of 16 / 32 / 128 tiles; 81-83: group start moving by
-// 1 / 2 / 8 inputs instead of 4.
-// 70-75: the round-2 steps: 70 contiguous lines, 71 + nt loads,
-// 73 + hot-line past-the-end loads, 75 + subfield arithmetic; 72 / 74:
-// traffic-only probes of 71 / 73.
-// Round 1: 58: 41 with each read group's 16 workgroups on one XCD.
-// 41: one input rotation per group of 16 consecutive tiles (the 16
-// workgroups stream one shard's 128 KiB together); 36 / 40 / 42: groups of
-// 1 / 8 / 32 tiles; 5: one rotation per wave (each wave of a tile on its own
-// shard); 37: no rotation; 44: traffic-only probe of 58 (wrong output; refused
-// unless BFRS_ALLOW_PROBE=1).  Rejected variants were removed; their code is
-// in the git history and their results in DESIGN.md §9.
+// Kernel selection.  The product library carries the default (76) and the
+// two looped forms it falls back to: 75 (looped GF(2^8)-subfield ring) and 73
+// (looped general GF(2^16) ring).  BFRS_KERNEL_VARIANT may force 75 or 73 (the
+// parity suite runs them on BlockFrame's shapes); any other value is refused
+// with an error, never run.  The round-1/2 A/B variants and the traffic-only
+// probes (which write wrong bytes) exist only in the measurement build
+// (make ab -> libbfrs_ab.so, -DBFRS_AB_VARIANTS; tools/kbench.py).
+//   76: contiguous-line nt loads/stores with lane-half swaps; for GF(2^8)-
+//       subfield launches (every RS(k<=30,3) encode/decode) the fully unrolled
+//       SDWA-addressed kernel for n_in 30 / 20 / 8, read groups of 64
+//       consecutive tiles (512 KiB of every shard's columns) on one XCD;
+//       other launches run 75 or 73.
+#ifdef BFRS_AB_VARIANTS
+// A/B build only: 77 (76 with 4-byte low-byte lookups), 78-80 (read groups of
+// 16 / 32 / 128 tiles), 81-83 (group start moving by 1 / 2 / 8 inputs), the
+// round-2 steps 70 / 71, the round-1 kernels 58 / 41 / 36 / 37 / 40 / 42 / 5,
+// and the traffic-only probes 44 / 72 / 74 (wrong output; also need
+// BFRS_ALLOW_PROBE=1).  DESIGN.md §9 / §9b hold their results.
+static bool variant_known(int v) {
+  switch (v) {
+    case 5: case 36: case 37: case 40: case 41: case 42: case 58: case 70: case 71:
+    case 73: case 75: case 76: case 77: case 78: case 79: case 80: case 81: case 82: case 83:
+      return true;
+    case 44: case 72: case 74:
+      return std::getenv("BFRS_ALLOW_PROBE") != nullptr;
+    default:
+      return false;
+  }
+}
+#else
+static bool variant_known(int v) { return v == 76 || v == 75 || v == 73; }
+#endif
+
 int kernel_variant() {
   const char *e = std::getenv("BFRS_KERNEL_VARIANT");
-  int v = e ? atoi(e) : 76;
-  if ((v == 44 || v == 72 || v == 74) && !std::getenv("BFRS_ALLOW_PROBE")) v = 76;
-  return v;
+  if (!e || !*e) return 76;
+  char *end = nullptr;
+  const long v = std::strtol(e, &end, 10);
+  if (*end != '\0' || v < 0 || v > 1000 || !variant_known(int(v))) return -1;
+  return int(v);
+}
+
+bool ab_build() {
+#ifdef BFRS_AB_VARIANTS
+  return true;
+#else
+  return false;
+#endif
 }
 
 uint32_t tile_bytes() { return kTileHalfChunks * 32; }
+
+#ifdef BFRS_AB_VARIANTS
+static hipError_t launch_gf_default(const KernArgs &args, uint32_t n_wgs, size_t lds, bool subfield,
+                                    hipStream_t stream) {
+  if (subfield && args.tiles_per_wg == 1)
+    hipLaunchKernelGGL(gf_apply_unrolled_kernel<true>, dim3(n_wgs), dim3(256), lds, stream, args);
+  else if (subfield)
+    hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16, 1, 1, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
+  else
+    hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16, 1, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
+  return hipGetLastError();
+}
+#endif
 
 hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in, bool subfield,
                            hipStream_t stream) {
   if (n_wgs == 0) return hipSuccess;
   const size_t lds = size_t(max_in) * 64 * sizeof(uint2);
-  switch (kernel_variant()) {
+  const int v = kernel_variant();
+  if (v < 0) return hipErrorInvalidValue;  // Context::init reports it by name
+  const bool unrolled_ok = subfield && args.tiles_per_wg == 1;
+  switch (v) {
+    case 76:  // unrolled SDWA-addressed kernel where the launch allows it, else 75 / 73
+      if (unrolled_ok) {
+        hipLaunchKernelGGL(gf_apply_unrolled_kernel<true>, dim3(n_wgs), dim3(256), lds, stream, args);
+        break;
+      }
+      [[fallthrough]];
+    case 75:  // looped ring, GF(2^8)-subfield arithmetic when every pass allows it
+      if (subfield) {
+        hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16, 1, 1, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
+        break;
+      }
+      [[fallthrough]];
+    case 73:  // looped ring, general GF(2^16) arithmetic
+      hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16, 1, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
+      break;
+#ifdef BFRS_AB_VARIANTS
     case 5:
       hipLaunchKernelGGL((gf_apply_ring_kernel<0>), dim3(n_wgs), dim3(256), lds, stream, args);
       break;
@@ -888,6 +964,9 @@ hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in
     case 41:
       hipLaunchKernelGGL((gf_apply_ring_kernel<6>), dim3(n_wgs), dim3(256), lds, stream, args);
       break;
+    case 58:  // 41 with each read group's 16 workgroups on one XCD
+      hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16>), dim3(n_wgs), dim3(256), lds, stream, args);
+      break;
     case 70:  // 58 with contiguous-line loads/stores (LAY 1)
       hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16, 1, 0>), dim3(n_wgs), dim3(256), lds, stream, args);
       break;
@@ -897,57 +976,31 @@ hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in
     case 72:  // traffic-only probe of 71
       hipLaunchKernelGGL((gf_apply_ring_kernel<6, true, 16, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
       break;
-    case 73:  // 71 with the ring's past-the-end loads on one hot line
-      hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16, 1, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
-      break;
-    case 75:  // 73 with the GF(2^8)-subfield arithmetic when every pass allows it
-      if (subfield)
-        hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16, 1, 1, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
-      else
-        hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16, 1, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
-      break;
-    case 78:  // 76 with read groups of 16 tiles (the round-1 grouping)
-    case 79:  // 76 with read groups of 32 tiles
-    case 80:  // 76 with read groups of 128 tiles
-    case 81:  // 76 with the group start moving by 1 input
-    case 82:  // 76 with the group start moving by 2 inputs
-    case 83:  // 76 with the group start moving by 8 inputs
-      if (subfield && args.tiles_per_wg == 1) {
-        const int v = kernel_variant();
-        if (v == 78)
-          hipLaunchKernelGGL((gf_apply_unrolled_kernel<true, 4, 4>), dim3(n_wgs), dim3(256), lds, stream, args);
-        else if (v == 79)
-          hipLaunchKernelGGL((gf_apply_unrolled_kernel<true, 5, 4>), dim3(n_wgs), dim3(256), lds, stream, args);
-        else if (v == 80)
-          hipLaunchKernelGGL((gf_apply_unrolled_kernel<true, 7, 4>), dim3(n_wgs), dim3(256), lds, stream, args);
-        else if (v == 81)
-          hipLaunchKernelGGL((gf_apply_unrolled_kernel<true, 6, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
-        else if (v == 82)
-          hipLaunchKernelGGL((gf_apply_unrolled_kernel<true, 6, 2>), dim3(n_wgs), dim3(256), lds, stream, args);
-        else
-          hipLaunchKernelGGL((gf_apply_unrolled_kernel<true, 6, 8>), dim3(n_wgs), dim3(256), lds, stream, args);
-        break;
-      }
-      [[fallthrough]];
-    case 77:  // 76 with 4-byte low-byte lookups
-      if (subfield && args.tiles_per_wg == 1) {
-        hipLaunchKernelGGL(gf_apply_unrolled_kernel<false>, dim3(n_wgs), dim3(256), lds, stream, args);
-        break;
-      }
-      [[fallthrough]];
-    case 76:  // unrolled SDWA-addressed kernel where the launch allows it, else 75
-      if (subfield && args.tiles_per_wg == 1)
-        hipLaunchKernelGGL(gf_apply_unrolled_kernel<true>, dim3(n_wgs), dim3(256), lds, stream, args);
-      else if (subfield)
-        hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16, 1, 1, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
-      else
-        hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16, 1, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
-      break;
     case 74:  // traffic-only probe of 73
       hipLaunchKernelGGL((gf_apply_ring_kernel<6, true, 16, 1, 1, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
       break;
-    default:  // 58: 41 with each read group's 16 workgroups on one XCD
-      hipLaunchKernelGGL((gf_apply_ring_kernel<6, false, 16>), dim3(n_wgs), dim3(256), lds, stream, args);
+    case 77:  // 76 with 4-byte low-byte lookups
+      if (!unrolled_ok) return launch_gf_default(args, n_wgs, lds, subfield, stream);
+      hipLaunchKernelGGL(gf_apply_unrolled_kernel<false>, dim3(n_wgs), dim3(256), lds, stream, args);
+      break;
+    case 78: case 79: case 80: case 81: case 82: case 83:
+      if (!unrolled_ok) return launch_gf_default(args, n_wgs, lds, subfield, stream);
+      if (v == 78)  // read groups of 16 tiles (the round-1 grouping)
+        hipLaunchKernelGGL((gf_apply_unrolled_kernel<true, 4, 4>), dim3(n_wgs), dim3(256), lds, stream, args);
+      else if (v == 79)  // read groups of 32 tiles
+        hipLaunchKernelGGL((gf_apply_unrolled_kernel<true, 5, 4>), dim3(n_wgs), dim3(256), lds, stream, args);
+      else if (v == 80)  // read groups of 128 tiles
+        hipLaunchKernelGGL((gf_apply_unrolled_kernel<true, 7, 4>), dim3(n_wgs), dim3(256), lds, stream, args);
+      else if (v == 81)  // group start moving by 1 input
+        hipLaunchKernelGGL((gf_apply_unrolled_kernel<true, 6, 1>), dim3(n_wgs), dim3(256), lds, stream, args);
+      else if (v == 82)  // by 2 inputs
+        hipLaunchKernelGGL((gf_apply_unrolled_kernel<true, 6, 2>), dim3(n_wgs), dim3(256), lds, stream, args);
+      else  // by 8 inputs
+        hipLaunchKernelGGL((gf_apply_unrolled_kernel<true, 6, 8>), dim3(n_wgs), dim3(256), lds, stream, args);
+      break;
+#endif
+    default:
+      return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }

@@ -110,7 +110,8 @@ CodecSlot::~CodecSlot() {
 
 // Host copy into pinned memory: up to 8 threads of >= 4 MiB for large shards
 // (one core copies ~10-20 GB/s from pageable memory; the PCIe link takes
-// ~50 GB/s, and the crate-shaped path is bound by these copies).
+// ~50 GB/s).  A thread that fails to start (thread quota) leaves its part to
+// this thread; the started ones are always joined, so nothing terminates.
 void host_copy(uint8_t *dst, const uint8_t *src, size_t n) {
   constexpr size_t kPart = 4u << 20, kMaxParts = 8;
   const size_t parts = std::min<size_t>(kMaxParts, n / kPart);
@@ -120,23 +121,30 @@ void host_copy(uint8_t *dst, const uint8_t *src, size_t n) {
   }
   const size_t per = (n / parts + 63) / 64 * 64;
   std::thread th[kMaxParts];
+  bool started[kMaxParts] = {};
   for (size_t t = 1; t < parts; ++t) {
-    const size_t a = t * per, b = std::min(n, a + per);
-    th[t] = std::thread([=] { std::memcpy(dst + a, src + a, b - a); });
+    const size_t a = std::min(n, t * per), b = std::min(n, a + per);
+    try {
+      th[t] = std::thread([=] { std::memcpy(dst + a, src + a, b - a); });
+      started[t] = true;
+    } catch (...) {  // std::system_error: copy this part here instead
+      std::memcpy(dst + a, src + a, b - a);
+    }
   }
   std::memcpy(dst, src, std::min(n, per));
-  for (size_t t = 1; t < parts; ++t) th[t].join();
+  for (size_t t = 1; t < parts; ++t)
+    if (started[t]) th[t].join();
 }
 
-int Context::codec_acquire(size_t nshards, size_t shard_bytes, std::unique_ptr<CodecSlot> *out) {
+int CodecPool::acquire(size_t nshards, size_t shard_bytes, std::unique_ptr<CodecSlot> *out) {
   const size_t stride = (shard_bytes + 255) / 256 * 256;
   {
-    std::lock_guard<std::mutex> g(codec_mu);
-    for (size_t i = 0; i < codec_free.size(); ++i)
-      if (codec_free[i]->stride >= stride && codec_free[i]->nshards >= nshards &&
-          codec_free[i]->stride * codec_free[i]->nshards <= 2 * stride * nshards) {
-        *out = std::move(codec_free[i]);
-        codec_free.erase(codec_free.begin() + long(i));
+    std::lock_guard<std::mutex> g(mu);
+    for (size_t i = 0; i < free.size(); ++i)
+      if (free[i]->stride >= stride && free[i]->nshards >= nshards &&
+          free[i]->stride * free[i]->nshards <= 2 * stride * nshards) {
+        *out = std::move(free[i]);
+        free.erase(free.begin() + long(i));
         return BFRS_OK;
       }
   }
@@ -151,29 +159,37 @@ int Context::codec_acquire(size_t nshards, size_t shard_bytes, std::unique_ptr<C
   return BFRS_OK;
 }
 
-void Context::codec_release(std::unique_ptr<CodecSlot> slot) {
+void CodecPool::release(std::unique_ptr<CodecSlot> slot) {
   if (!slot) return;
   (void)hipStreamSynchronize(slot->stream);
-  std::unique_ptr<CodecSlot> drop;
-  std::lock_guard<std::mutex> g(codec_mu);
-  if (codec_free.size() < codec_cached) {
-    codec_free.push_back(std::move(slot));
-  } else {  // keep the larger slot
-    size_t small = 0;
-    for (size_t i = 1; i < codec_free.size(); ++i)
-      if (codec_free[i]->stride * codec_free[i]->nshards <
-          codec_free[small]->stride * codec_free[small]->nshards)
-        small = i;
-    if (codec_free[small]->stride * codec_free[small]->nshards < slot->stride * slot->nshards)
-      std::swap(codec_free[small], slot);
-    drop = std::move(slot);  // freed outside... after the lock guard (declared first)
+  std::unique_ptr<CodecSlot> drop;  // freed after the lock is released
+  {
+    std::lock_guard<std::mutex> g(mu);
+    if (free.size() < cached) {
+      free.push_back(std::move(slot));
+      return;
+    }
+    if (!free.empty()) {  // full: keep the larger of the smallest idle slot and this one
+      size_t small = 0;
+      for (size_t i = 1; i < free.size(); ++i)
+        if (free[i]->stride * free[i]->nshards < free[small]->stride * free[small]->nshards)
+          small = i;
+      if (free[small]->stride * free[small]->nshards < slot->stride * slot->nshards)
+        std::swap(free[small], slot);
+    }
+    drop = std::move(slot);
   }
+}
+
+CodecPool::~CodecPool() {
+  (void)hipSetDevice(device);
+  free.clear();
 }
 
 Context::~Context() {
   if (device >= 0) (void)hipSetDevice(device);
   if (stream) (void)hipStreamSynchronize(stream);
-  codec_free.clear();
+  codec_pool.reset();  // idle slots go now; live codec objects keep the pool
   staging.reset();  // archive staging arenas (pinned + device)
   plans.clear();
   for (auto &ps : pipe_stream)
@@ -188,13 +204,33 @@ Context::~Context() {
 }
 
 int Context::init(int dev) {
+  // a kernel this build does not carry is refused before anything else
+  // (the A/B variants and probes exist only in libbfrs_ab.so)
+  if (kernel_variant() < 0)
+    return set_error(BFRS_E_INVALID_ARGUMENT,
+                     std::string("BFRS_KERNEL_VARIANT=") + std::getenv("BFRS_KERNEL_VARIANT") +
+                         (ab_build() ? " is not a known kernel variant (probes need BFRS_ALLOW_PROBE=1)"
+                                     : " is not built into this library (product kernels: 76, 75, "
+                                       "73; A/B variants: make ab -> libbfrs_ab.so)"));
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
     return set_error(BFRS_E_NO_DEVICE, "no HIP device available (no CPU fallback)");
   if (dev < 0 || dev >= n) return set_error(BFRS_E_NO_DEVICE, "HIP device id out of range");
   device = dev;
   if (const char *e = std::getenv("BFRS_PLAN_CACHE")) max_plans = std::max(1, atoi(e));
-  if (const char *e = std::getenv("BFRS_CODEC_SLOTS")) codec_cached = size_t(std::max(0, atoi(e)));
+  codec_pool->device = dev;
+  if (const char *e = std::getenv("BFRS_CODEC_SLOTS")) {
+    char *end = nullptr;
+    const long v = std::strtol(e, &end, 10);
+    codec_pool->cached = (end != e && v > 0) ? size_t(std::min<long>(v, 1024)) : 0;
+  }
+  if (const char *e = std::getenv("BFRS_CODEC_STAGING")) {
+    if (std::strcmp(e, "pinned") == 0)
+      codec_pool->staging = Staging::kPinned;
+    else if (std::strcmp(e, "direct") != 0 && *e)
+      return set_error(BFRS_E_INVALID_ARGUMENT,
+                       std::string("BFRS_CODEC_STAGING=") + e + ": expected direct or pinned");
+  }
   HIP_TRY(hipSetDevice(dev));
   HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
   for (auto &ps : pipe_stream) HIP_TRY(hipStreamCreateWithFlags(&ps, hipStreamNonBlocking));
@@ -412,7 +448,12 @@ int Context::run_window(const std::vector<BlockIO> &blocks, size_t shard_bytes,
         wg += wgs_per_pass;
         max_in = std::max(max_in, n_pad);
       }
-      if (n_tiles) HIP_TRY(launch_gf_apply(ka, wg, max_in, subfield, s));
+      if (n_tiles) {
+        if (kernel_variant() < 0)
+          return set_error(BFRS_E_INVALID_ARGUMENT, "BFRS_KERNEL_VARIANT names a kernel this "
+                                                    "library does not carry");
+        HIP_TRY(launch_gf_apply(ka, wg, max_in, subfield, s));
+      }
       if (tail) HIP_TRY(launch_gf_tail(ka, s));
       first = last;
     }
@@ -450,6 +491,7 @@ const char *bfrs_strerror(int code) {
     case BFRS_E_NO_DEVICE: return "no HIP device";
     case BFRS_E_NOMEM: return "out of memory";
     case BFRS_E_NOT_RESTORED: return "original shard was not restored";
+    case BFRS_E_NOT_FOUND: return "not found";
     default: return "unknown error";
   }
 }

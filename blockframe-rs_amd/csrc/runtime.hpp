@@ -89,9 +89,9 @@ struct BlockIO {
 
 // Device + pinned-host shard slots of the streaming codec objects
 // (bfrs_encoder / bfrs_decoder), each with its own stream so objects on
-// different threads overlap.  Cached per context (Context::codec_*), so an
-// encoder per block -- BlockFrame's pattern, generate.rs:84 -- allocates and
-// pins nothing after the first few blocks.
+// different threads overlap.  Cached per context (CodecPool), so an encoder
+// per block -- BlockFrame's pattern, generate.rs:84 -- allocates and pins
+// nothing after the first few blocks.
 struct CodecSlot {
   void *d = nullptr;     // nshards x stride bytes of HBM
   uint8_t *h = nullptr;  // nshards x stride bytes of pinned host memory
@@ -100,7 +100,30 @@ struct CodecSlot {
   ~CodecSlot();
 };
 
+// How add_*_shard moves a caller's shard to the device (BFRS_CODEC_STAGING):
+//   kDirect: hipMemcpyAsync straight from the caller's (pageable) buffer on
+//            the slot stream, then a stream sync so the caller may reuse the
+//            buffer on return, as with the crate's copy (default: the PCIe
+//            link takes pageable sources at the pinned rate);
+//   kPinned: memcpy into the slot's pinned row, then an async H2D (round 2).
+enum class Staging { kDirect, kPinned };
+
+// The slot cache of one context.  Shared (shared_ptr) by the context and by
+// every live codec object, so an object freed after bfrs_close still returns
+// or frees its slot safely; the pool goes away with the last of them.
+struct CodecPool {
+  int device = 0;
+  Staging staging = Staging::kDirect;
+  std::mutex mu;
+  std::vector<std::unique_ptr<CodecSlot>> free;
+  size_t cached = 2;  // BFRS_CODEC_SLOTS: idle slots kept (0 = none)
+  int acquire(size_t nshards, size_t shard_bytes, std::unique_ptr<CodecSlot> *out);
+  void release(std::unique_ptr<CodecSlot> slot);
+  ~CodecPool();
+};
+
 // memcpy on up to 8 threads for large buffers (pageable <-> pinned staging).
+// Never throws: a thread that cannot start leaves its part to the caller.
 void host_copy(uint8_t *dst, const uint8_t *src, size_t n);
 
 struct Context {
@@ -134,15 +157,11 @@ struct Context {
   void *h_hash = nullptr;
   size_t h_hash_cap = 0;
 
-  // Codec-object slot cache: at most codec_cached idle slots are kept
+  // Codec-object slot cache: at most codec_pool->cached idle slots are kept
   // (BFRS_CODEC_SLOTS, default 2), which bounds a context's idle pinned +
   // HBM footprint to 2 x (k + m) x shard_bytes each; slots beyond that are
   // freed on release.  Any number of objects may be alive at once.
-  std::mutex codec_mu;
-  std::vector<std::unique_ptr<CodecSlot>> codec_free;
-  size_t codec_cached = 2;
-  int codec_acquire(size_t nshards, size_t shard_bytes, std::unique_ptr<CodecSlot> *out);
-  void codec_release(std::unique_ptr<CodecSlot> slot);
+  std::shared_ptr<CodecPool> codec_pool = std::make_shared<CodecPool>();
 
   ~Context();
   int init(int dev);
@@ -186,3 +205,13 @@ int decode_batch_on(bfrs_ctx *ctx, size_t nblocks, const uint32_t *ks, size_t m,
 struct bfrs_ctx {
   bfrs::Context impl;
 };
+
+namespace bfrs {
+// Wrapper fast paths (blockframe.cpp): the owned Vec outputs of
+// generate_parity / recover_segment_rs30_3 (generate.rs:95-96,
+// recovery.rs:166-170) are filled by D2H straight into the caller's buffers.
+// encode into m host buffers of shard_bytes each (object left encoded)
+int encoder_encode_to_host(bfrs_encoder *e, uint8_t *const *outs);
+// restored original `index` of a decoded decoder into a host buffer
+int decoder_restored_to_host(bfrs_decoder *d, size_t index, uint8_t *out);
+}  // namespace bfrs

@@ -25,9 +25,24 @@
  * encoder or decoder object is used by one thread at a time (as the crate's
  * &mut self API implies).  A context keeps at most BFRS_CODEC_SLOTS idle codec
  * slots (environment, read by bfrs_open; default 2): set it to the number of
- * worker threads to keep their pinned + device rows across blocks.  The archive calls (commit, repair, health check)
- * and an open archive handle are serialised inside the library; a handle may
- * be read from several threads.  Distinct contexts are independent.
+ * worker threads to keep their pinned + device rows across blocks.  The
+ * archive calls (commit, repair, health check) and an open archive handle are
+ * serialised inside the library; a handle may be read from several threads.
+ * Distinct contexts are independent.
+ *
+ * Lifetimes: an encoder or decoder may be freed before or after bfrs_close of
+ * its context (it shares the context's slot pool); every other call on it
+ * needs the context open.  Free archive handles before bfrs_close.
+ *
+ * Environment, read by bfrs_open:
+ *   BFRS_CODEC_SLOTS    idle codec slots kept (default 2; 0 = none)
+ *   BFRS_CODEC_STAGING  "direct" (default: add_*_shard DMAs straight from the
+ *                       caller's buffer) or "pinned" (memcpy into a pinned row
+ *                       first); either way the buffer is free on return
+ *   BFRS_KERNEL_VARIANT unset or 76 (default kernel); 75 / 73 force the looped
+ *                       subfield / general kernels; anything else fails
+ *                       bfrs_open with BFRS_E_INVALID_ARGUMENT (the A/B
+ *                       variants exist only in the measurement build)
  */
 #ifndef BFRS_H
 #define BFRS_H
@@ -106,7 +121,8 @@ int bfrs_plan_decode(size_t original_count, size_t recovery_count, const uint8_t
 /* replaces ReedSolomonEncoder::new (generate.rs:37,84) */
 int bfrs_encoder_new(bfrs_ctx *ctx, size_t original_count, size_t recovery_count,
                      size_t shard_bytes, bfrs_encoder **out);
-/* replaces add_original_shard (generate.rs:41,44,88); host memory, copied. */
+/* replaces add_original_shard (generate.rs:41,44,88); host memory, copied to
+ * the device before the call returns (the caller may reuse the buffer). */
 int bfrs_encoder_add_original_shard(bfrs_encoder *enc, const uint8_t *shard, size_t len);
 /* replaces encode() (generate.rs:47,92) */
 int bfrs_encoder_encode(bfrs_encoder *enc);
@@ -128,7 +144,9 @@ int bfrs_decoder_add_recovery_shard(bfrs_decoder *dec, size_t index, const uint8
 /* replaces decode() (recovery.rs:65,166; health.rs:746) */
 int bfrs_decoder_decode(bfrs_decoder *dec);
 /* replaces DecoderResult::restored_original(index) (recovery.rs:66-69,167-169):
- * BFRS_E_NOT_RESTORED plays the role of Option::None. */
+ * BFRS_E_NOT_RESTORED plays the role of Option::None.  The first call for an
+ * index copies that shard to host memory; the pointer is valid until the next
+ * add/decode call on this decoder. */
 int bfrs_decoder_restored_original(bfrs_decoder *dec, size_t index, const uint8_t **data,
                                    size_t *len);
 void bfrs_decoder_free(bfrs_decoder *dec);

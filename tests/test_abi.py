@@ -49,6 +49,63 @@ def test_abi_version_and_strerror(bfrs):
     L = bfrs.lib()
     assert L.bfrs_abi_version() == 1
     assert L.bfrs_strerror(bfrs.E_NOT_ENOUGH_SHARDS) == b"not enough shards"
+    assert L.bfrs_strerror(bfrs.E_NOT_FOUND) == b"not found"
+    # every code the header declares has its own text
+    codes = re.findall(r"\b(BFRS_E_[A-Z_]+)\s*=\s*(-\d+)", open(HEADER).read())
+    assert len(codes) == 17
+    for name, val in codes:
+        assert L.bfrs_strerror(int(val)) != b"unknown error", name
+
+
+PRODUCT_KERNELS = {
+    # v76: the unrolled SDWA-addressed GF(2^8)-subfield kernel (read groups of 64 tiles)
+    "void bfrs::(anonymous namespace)::gf_apply_unrolled_kernel<true, 6, 4>(bfrs::KernArgs)",
+    # v75 / v73: the looped subfield and general GF(2^16) rings
+    "void bfrs::(anonymous namespace)::gf_apply_ring_kernel<6, false, 16u, 1, 1, 1, 1>(bfrs::KernArgs)",
+    "void bfrs::(anonymous namespace)::gf_apply_ring_kernel<6, false, 16u, 1, 1, 1, 0>(bfrs::KernArgs)",
+    "bfrs::(anonymous namespace)::gf_tail_kernel(bfrs::KernArgs)",
+    # device BLAKE3 (the Merkle re-verify of the read/repair path)
+    "bfrs::(anonymous namespace)::blake3_group_kernel(bfrs::HashGroup const*, unsigned int*, "
+    "unsigned int*, unsigned int*)",
+    "bfrs::(anonymous namespace)::blake3_reduce_kernel(bfrs::HashReduce const*, unsigned int const*, "
+    "unsigned int*, unsigned int*, unsigned int*)",
+}
+
+
+def test_product_code_object_carries_only_product_kernels(bfrs):
+    """The A/B variant zoo and the traffic-only probes are not in libbfrs.so
+    (they live in the measurement build libbfrs_ab.so, make ab)."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import code_objects
+    product = os.path.join(ROOT, "blockframe-rs_amd", "libbfrs.so")
+    assert set(code_objects.kernels(product)) == PRODUCT_KERNELS
+    ab = os.path.join(ROOT, "blockframe-rs_amd", "libbfrs_ab.so")
+    if os.path.exists(ab):  # the measurement build carries more, never fewer
+        assert PRODUCT_KERNELS < set(code_objects.kernels(ab))
+
+
+@pytest.mark.parametrize("value", ["44", "58", "77", "74", "abc", "76x", "-1"])
+def test_unknown_kernel_variant_is_refused(bfrs, monkeypatch, value):
+    """A stray BFRS_KERNEL_VARIANT never silently changes the product's kernel:
+    anything but 76 / 75 / 73 fails bfrs_open with an error naming it."""
+    if os.environ.get("BFRS_LIB", "libbfrs.so") != "libbfrs.so":
+        pytest.skip("checks the product library")
+    monkeypatch.setenv("BFRS_KERNEL_VARIANT", value)
+    monkeypatch.setenv("BFRS_ALLOW_PROBE", "1")
+    with pytest.raises(bfrs.BfrsError) as e:
+        bfrs.Context(0)
+    assert e.value.code == bfrs.E_INVALID_ARGUMENT
+    assert "not built into this library" in str(e.value)
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-device path")
+@pytest.mark.parametrize("value", ["76", "75", "73", ""])
+def test_product_kernel_variants_pass_the_check(bfrs, monkeypatch, value):
+    monkeypatch.setenv("BFRS_KERNEL_VARIANT", value)
+    with pytest.raises(bfrs.BfrsError) as e:
+        bfrs.Context(0)
+    assert e.value.code == bfrs.E_NO_DEVICE
 
 
 @pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-device path")

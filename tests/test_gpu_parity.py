@@ -279,6 +279,7 @@ def test_streaming_encoder_decoder(ctx, bfrs, oracle):
         enc.add_original_shard(d)
     rec = list(enc.encode().recovery_iter())
     assert rec == [r.tobytes() for r in oracle.encode(data, 3)]
+    assert [enc.recovery_view(j).tobytes() for j in range(3)] == rec
     with pytest.raises(bfrs.BfrsError) as e:
         enc.add_original_shard(data[0][:64])
     assert e.value.code == bfrs.E_DIFFERENT_SHARD_SIZE
@@ -339,6 +340,52 @@ def test_codec_objects_share_one_context_across_threads(ctx, bfrs, oracle):
     for t in ts:
         t.join(timeout=120)
     assert not errors, errors
+
+
+@pytest.mark.parametrize("staging", ["direct", "pinned"])
+@pytest.mark.parametrize("slots", ["0", "1", "4"])
+def test_codec_staging_slots_and_lifetimes(bfrs, oracle, monkeypatch, staging, slots):
+    """Both staging modes of add_*_shard (BFRS_CODEC_STAGING) and any idle-slot
+    count (BFRS_CODEC_SLOTS=0 keeps none: ADVICE r2) give the oracle's bytes
+    through the objects and the wrappers; the caller's buffer is reusable as
+    soon as add returns; objects outlive bfrs_close and are freed safely."""
+    monkeypatch.setenv("BFRS_CODEC_STAGING", staging)
+    monkeypatch.setenv("BFRS_CODEC_SLOTS", slots)
+    c = bfrs.Context(0)
+    rng = np.random.default_rng(21)
+    n = 64 * 4096 + 64 * 3  # ragged against the 8 KiB tile
+    data = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(30)]
+    want = [r.tobytes() for r in oracle.encode(data, 3)]
+    for rep in range(2):
+        enc = bfrs.ReedSolomonEncoder(c, 30, 3, n)
+        buf = np.empty(n, np.uint8)
+        for d in data:
+            buf[:] = d
+            enc.add_original_shard(buf)  # the same buffer every time
+        assert list(enc.encode().recovery_iter()) == want, rep
+        del enc
+    outs = [np.empty(n, np.uint8) for _ in range(3)]
+    assert bfrs.Chunker(c).generate_parity_into(data, 30, 3, outs) == n
+    assert [o.tobytes() for o in outs] == want
+    par = [np.frombuffer(p, np.uint8) for p in want]
+    slots_ = [None if i in (2, 17, 29) else data[i] for i in range(30)]
+    for t in (2, 17, 29):
+        assert bfrs.recover_segment_rs30_3(c, slots_, par, t) == data[t].tobytes()
+    dec = bfrs.ReedSolomonDecoder(c, 30, 3, n)
+    for i in range(30):
+        if slots_[i] is not None:
+            dec.add_original_shard(i, slots_[i])
+    for j in range(3):
+        dec.add_recovery_shard(j, par[j])
+    dec.decode()
+    assert dec.restored_view(17).tobytes() == data[17].tobytes()
+    assert dec.restored_original(2) == data[2].tobytes()
+    assert dec.restored_view(0) is None
+    keep = bfrs.ReedSolomonEncoder(c, 8, 3, n)
+    c.close()  # objects still alive: freeing them later is safe
+    with pytest.raises(bfrs.BfrsError):
+        keep.add_original_shard(data[0])  # but no other call on a closed context
+    del dec, keep
 
 
 def test_codec_argument_errors(ctx, bfrs):

@@ -19,10 +19,11 @@ CSRC = os.path.join(ROOT, "blockframe-rs_amd", "csrc")
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 
 
-def _isa(src, tmp_path):
-    out = tmp_path / (os.path.basename(src) + ".s")
+def _isa(src, tmp_path, defines=()):
+    out = tmp_path / (os.path.basename(src) + "".join(defines) + ".s")
     subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "--cuda-device-only",
-                    "-S", "-I", CSRC, "-o", str(out), src], check=True, capture_output=True)
+                    *[f"-D{d}" for d in defines], "-S", "-I", CSRC, "-o", str(out), src],
+                   check=True, capture_output=True)
     return out.read_text().split("\n")
 
 
@@ -40,9 +41,11 @@ def _hazards(lines, window=6):
 
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
-@pytest.mark.parametrize("src", ["rs_kernels.hip", "blake3_kernels.hip"])
-def test_no_valu_sgpr_to_vmem_hazard(src, tmp_path):
-    lines = _isa(os.path.join(CSRC, src), tmp_path)
+@pytest.mark.parametrize("src,defines", [("rs_kernels.hip", ()),
+                                         ("rs_kernels.hip", ("BFRS_AB_VARIANTS",)),
+                                         ("blake3_kernels.hip", ())])
+def test_no_valu_sgpr_to_vmem_hazard(src, defines, tmp_path):
+    lines = _isa(os.path.join(CSRC, src), tmp_path, defines)
     assert any("global_" in l for l in lines)
     assert _hazards(lines) == []
 
@@ -71,21 +74,26 @@ def _inflight():
 
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
-def test_no_copy_of_inflight_asm_load_registers(tmp_path):
+@pytest.mark.parametrize("defines,n_kernels", [((), 4), (("BFRS_AB_VARIANTS",), 20)])
+def test_no_copy_of_inflight_asm_load_registers(tmp_path, defines, n_kernels):
     """The RS kernels' loads are inline asm waited for by a separate
     `s_waitcnt vmcnt` asm; a compiler copy, spill or address use of a
     destination register before its wait reads a stale value (a live-range
     split at a control-flow merge did exactly that in a first version of the
     streamed kernel, and a probe built the same way faulted the GPU).
-    The traffic-only probe (variant 44) is checked too: a probe that faults
-    costs a GPU box all the same."""
+    The product build carries 4 kernels (v76, the looped subfield and general
+    rings, the tail kernel); the A/B build's variants and traffic-only probes
+    are checked too: a probe that faults costs a GPU box all the same."""
     ic = _inflight()
-    src = "\n".join(_isa(os.path.join(CSRC, "rs_kernels.hip"), tmp_path))
+    src = "\n".join(_isa(os.path.join(CSRC, "rs_kernels.hip"), tmp_path, defines))
     checked = 0
     for name, body in ic.kernels(src):
         checked += 1
         assert ic.check(body) == [], name
-    assert checked >= 7  # ring kernel x 7 read orders / probe, tail kernel
+    if defines:
+        assert checked >= n_kernels
+    else:
+        assert checked == n_kernels
 
 
 def test_inflight_checker_flags_a_copy():

@@ -16,6 +16,8 @@ import time
 PROBES = ("44", "72", "74")  # traffic-only probes: no codec output to check
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "blockframe-rs_amd"))
+# the A/B variants live only in the measurement build (make -C blockframe-rs_amd/csrc ab)
+os.environ.setdefault("BFRS_LIB", "libbfrs_ab.so")
 
 
 def main():
@@ -144,7 +146,7 @@ def main():
         else:
             raise SystemExit(f"unknown io mode {io}")
 
-    os.environ["BFRS_KERNEL_VARIANT"] = "1"
+    os.environ["BFRS_KERNEL_VARIANT"] = "76"
     os.environ.pop("BFRS_TILES_PER_WG", None)
     for L in layouts.values():
         ctx.encode_batch_dev(shapes, 3, S, L["data"], L["par"], stream=stream)  # parity for decode

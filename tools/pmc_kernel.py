@@ -6,6 +6,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "blockframe-rs_amd"))
+# the A/B variants live only in the measurement build (make -C blockframe-rs_amd/csrc ab)
+os.environ.setdefault("BFRS_LIB", "libbfrs_ab.so")
 
 
 def main():
