@@ -57,7 +57,7 @@ EXPORTS = (
     "bfrs_generate_parity_segmented", "bfrs_recover_segment_rs13", "bfrs_recover_segment_rs30_3",
     "bfrs_blake3_hex", "bfrs_blake3_batch_dev", "bfrs_blake3_combine", "bfrs_merkle_root_hex", "bfrs_manifest_check", "bfrs_commit", "bfrs_repair", "bfrs_health_check",
     "bfrs_store_list", "bfrs_store_find", "bfrs_batch_health_check", "bfrs_archive_open",
-    "bfrs_archive_size", "bfrs_archive_read", "bfrs_archive_stats_get", "bfrs_archive_close",
+    "bfrs_archive_size", "bfrs_archive_stat", "bfrs_archive_read", "bfrs_archive_stats_get", "bfrs_archive_close",
 )
 
 SIZE_MAX = ctypes.c_size_t(-1).value
@@ -80,6 +80,16 @@ class RepairReport(ctypes.Structure):
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+class ArchiveAttr(ctypes.Structure):
+    """bfrs_archive_attr (include/bfrs.h)."""
+    _fields_ = [("size", ctypes.c_uint64), ("segment_size", ctypes.c_uint64),
+                ("segments", ctypes.c_uint64), ("blocks", ctypes.c_uint64),
+                ("tier", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}
 
 
 class ArchiveStats(ctypes.Structure):
@@ -185,6 +195,7 @@ def lib() -> ctypes.CDLL:
             "bfrs_archive_open": ([_vp, ctypes.c_char_p, _sz, ctypes.c_int, ctypes.POINTER(_vp)],
                                   ctypes.c_int),
             "bfrs_archive_size": ([_vp, ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
+            "bfrs_archive_stat": ([ctypes.c_char_p, ctypes.POINTER(ArchiveAttr)], ctypes.c_int),
             "bfrs_archive_read": ([_vp, ctypes.c_uint64, _sz, _vp, ctypes.POINTER(_sz)],
                                   ctypes.c_int),
             "bfrs_archive_stats_get": ([_vp, ctypes.POINTER(ArchiveStats)], ctypes.c_int),
@@ -673,6 +684,14 @@ def merkle_root_hex(leaves) -> str:
     out = ctypes.create_string_buffer(65)
     _check(lib().bfrs_merkle_root_hex("".join(leaves).encode(), len(leaves), out))
     return out.value.decode()
+
+
+def archive_stat(archive_dir: str) -> dict:
+    """The mount's getattr geometry of an archive (src/mount/filesystem_unix.rs:
+    153-174): size, tier, segment_size, segments, blocks.  Host only."""
+    a = ArchiveAttr()
+    _check(lib().bfrs_archive_stat(os.fsencode(archive_dir), ctypes.byref(a)))
+    return a.as_dict()
 
 
 def manifest_check(text) -> tuple:

@@ -1238,6 +1238,22 @@ int bfrs_archive_size(bfrs_archive *a, uint64_t *size) {
   BFRS_API_END
 }
 
+int bfrs_archive_stat(const char *archive_dir, bfrs_archive_attr *out) {
+  BFRS_API_BEGIN
+  if (!archive_dir || !out) return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_archive_stat: NULL argument");
+  Geometry g;
+  int rc = load_geometry(archive_dir, &g);
+  if (rc) return rc;
+  *out = bfrs_archive_attr{};
+  out->size = uint64_t(g.mf.size);
+  out->segment_size = g.mf.tier == 1 ? g.mf.segment_size : g.S;
+  out->segments = g.nseg;
+  out->blocks = g.mf.tier == 3 ? (g.nseg + kBlockSegments - 1) / kBlockSegments : 0;
+  out->tier = g.mf.tier;
+  return BFRS_OK;
+  BFRS_API_END
+}
+
 int bfrs_archive_read(bfrs_archive *a, uint64_t offset, size_t len, uint8_t *out, size_t *nread) {
   BFRS_API_BEGIN
   if (!a || (!out && len) || !nread) return set_error(BFRS_E_INVALID_ARGUMENT, "NULL argument");

@@ -155,17 +155,34 @@ int load_geometry(const std::string &dir, Geometry *g) {
   if (!Manifest::from_json(std::string(text.begin(), text.end()), &g->mf, &err))
     return set_error(BFRS_E_WRAPPER, err);
   g->dir = dir;
-  g->S = g->mf.tier == 1 ? uint64_t(std::max<int64_t>(g->mf.size, 1)) : g->mf.segment_size;
-  if (g->S == 0) return set_error(BFRS_E_WRAPPER, "manifest: segment_size is 0");
-  if (g->mf.size < 0) return set_error(BFRS_E_WRAPPER, "manifest: negative size");
-  g->nseg = g->mf.tier == 1 ? 1 : size_t((uint64_t(g->mf.size) + g->S - 1) / g->S);
-  if (g->mf.tier == 3) {  // blocks must cover the segments in order (commit.rs:359-402)
+  // Bounds before any arithmetic: a manifest is read from disk and may be
+  // damaged or hostile (tests/malformed_manifests).  The reference's serde
+  // types are i32 tier / usize sizes (manifest.rs:12-53); these limits only
+  // refuse shapes no commit writes.
+  const Manifest &mf = g->mf;
+  if (mf.tier < 1 || mf.tier > 3) return set_error(BFRS_E_WRAPPER, "manifest: tier must be 1, 2 or 3");
+  if (mf.size < 0) return set_error(BFRS_E_WRAPPER, "manifest: negative size");
+  if (uint64_t(mf.size) > kMaxFileBytes) return set_error(BFRS_E_WRAPPER, "manifest: size too large");
+  if (mf.tier != 1 && (mf.segment_size == 0 || mf.segment_size > kMaxSegmentBytes))
+    return set_error(BFRS_E_WRAPPER, mf.segment_size == 0 ? "manifest: segment_size is 0"
+                                                          : "manifest: segment_size too large");
+  g->S = mf.tier == 1 ? uint64_t(std::max<int64_t>(mf.size, 1)) : mf.segment_size;
+  g->nseg = mf.tier == 1 ? 1 : size_t((uint64_t(mf.size) + g->S - 1) / g->S);
+  if (mf.tier == 2) {  // one entry per segment, keys 0..n-1 (commit.rs:124-309)
+    if (mf.segments.size() != g->nseg) return set_error(BFRS_E_WRAPPER, "manifest: segment count");
+    for (size_t i = 0; i < g->nseg; ++i) {
+      auto it = mf.segments.find(int64_t(i));
+      if (it == mf.segments.end() || it->second.parity.size() != kParity)
+        return set_error(BFRS_E_WRAPPER, "manifest: segment " + std::to_string(i) + " shape");
+    }
+  }
+  if (mf.tier == 3) {  // blocks must cover the segments in order (commit.rs:359-402)
     const size_t nblocks = (g->nseg + kBlockSegments - 1) / kBlockSegments;
-    if (g->mf.blocks.size() != nblocks) return set_error(BFRS_E_WRAPPER, "manifest: block count");
+    if (mf.blocks.size() != nblocks) return set_error(BFRS_E_WRAPPER, "manifest: block count");
     for (size_t b = 0; b < nblocks; ++b) {
-      auto it = g->mf.blocks.find(int64_t(b));
+      auto it = mf.blocks.find(int64_t(b));
       const size_t want = std::min(kBlockSegments, g->nseg - b * kBlockSegments);
-      if (it == g->mf.blocks.end() || it->second.segments.size() != want ||
+      if (it == mf.blocks.end() || it->second.segments.size() != want ||
           it->second.parity.size() != kParity)
         return set_error(BFRS_E_WRAPPER, "manifest: block " + std::to_string(b) + " shape");
     }

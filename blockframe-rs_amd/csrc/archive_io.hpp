@@ -20,6 +20,10 @@ namespace bfrs {
 
 constexpr size_t kBlockSegments = 30;  // commit.rs:359,402
 constexpr size_t kParity = 3;
+// Geometry limits a manifest must respect (load_geometry): 2^50 B files
+// (1 PiB) and 2^36 B segments (64 GiB; BlockFrame writes 32 MiB, utils.rs:68).
+constexpr uint64_t kMaxFileBytes = uint64_t(1) << 50;
+constexpr uint64_t kMaxSegmentBytes = uint64_t(1) << 36;
 
 int io_error(const std::string &what);  // BFRS_E_WRAPPER + strerror(errno)
 int hw_threads();                        // host worker threads (<= 16)

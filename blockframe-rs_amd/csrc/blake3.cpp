@@ -76,7 +76,7 @@ void load_block(const uint8_t *p, size_t n, uint32_t m[16]) {
   uint8_t buf[kBlockLen];
   if (n < kBlockLen) {
     std::memset(buf, 0, sizeof buf);
-    std::memcpy(buf, p, n);
+    if (n) std::memcpy(buf, p, n);  // p is NULL for the empty message
     p = buf;
   }
   for (int i = 0; i < 16; ++i)

@@ -2,6 +2,8 @@
 #include "manifest.hpp"
 
 #include <cctype>
+#include <climits>
+#include <cstdint>
 #include <chrono>
 #include <cstdio>
 #include <ctime>
@@ -39,6 +41,8 @@ void dump_to(const Json &j, std::string *out) {
     case Json::kNull: *out += "null"; break;
     case Json::kBool: *out += j.b ? "true" : "false"; break;
     case Json::kInt: *out += std::to_string(j.i); break;
+    case Json::kUInt: *out += std::to_string(j.u); break;
+    case Json::kFloat: *out += j.s; break;
     case Json::kString: dump_string(j.s, out); break;
     case Json::kArray: {
       out->push_back('[');
@@ -65,13 +69,38 @@ void dump_to(const Json &j, std::string *out) {
   }
 }
 
+// Length of the UTF-8 sequence at t[p..] (RFC 3629: no overlongs, no
+// surrogates, <= U+10FFFF), 0 if invalid.
+size_t utf8_len(const std::string &t, size_t p) {
+  const auto c = [&](size_t k) { return static_cast<unsigned char>(t[p + k]); };
+  const size_t left = t.size() - p;
+  const unsigned char b0 = c(0);
+  if (b0 < 0x80) return 1;
+  auto cont = [&](size_t k) { return k < left && (c(k) & 0xC0) == 0x80; };
+  if (b0 >= 0xC2 && b0 <= 0xDF) return cont(1) ? 2 : 0;
+  if (b0 >= 0xE0 && b0 <= 0xEF) {
+    if (!cont(1) || !cont(2)) return 0;
+    if (b0 == 0xE0 && c(1) < 0xA0) return 0;  // overlong
+    if (b0 == 0xED && c(1) >= 0xA0) return 0;  // surrogate
+    return 3;
+  }
+  if (b0 >= 0xF0 && b0 <= 0xF4) {
+    if (!cont(1) || !cont(2) || !cont(3)) return 0;
+    if (b0 == 0xF0 && c(1) < 0x90) return 0;  // overlong
+    if (b0 == 0xF4 && c(1) >= 0x90) return 0;  // > U+10FFFF
+    return 4;
+  }
+  return 0;
+}
+
 struct Parser {
+  static constexpr int kMaxDepth = 128;  // serde_json's recursion limit
   const std::string &t;
   size_t p = 0;
   std::string err;
   explicit Parser(const std::string &text) : t(text) {}
-  void ws() {
-    while (p < t.size() && std::isspace(static_cast<unsigned char>(t[p]))) ++p;
+  void ws() {  // JSON whitespace only (RFC 8259: space, tab, LF, CR)
+    while (p < t.size() && (t[p] == ' ' || t[p] == '\t' || t[p] == '\n' || t[p] == '\r')) ++p;
   }
   bool fail(const char *m) {
     if (err.empty()) err = std::string(m) + " at offset " + std::to_string(p);
@@ -95,7 +124,7 @@ struct Parser {
     }
   }
   bool hex4(uint32_t *v) {
-    if (p + 4 > t.size()) return fail("short \\u escape");
+    if (t.size() - p < 4) return fail("short \\u escape");
     *v = 0;
     for (int n = 0; n < 4; ++n) {
       const char c = t[p++];
@@ -111,14 +140,17 @@ struct Parser {
     if (p >= t.size() || t[p] != '"') return fail("expected string");
     ++p;
     while (p < t.size() && t[p] != '"') {
-      char c = t[p++];
+      const unsigned char c = static_cast<unsigned char>(t[p]);
+      if (c < 0x20) return fail("control character in string");
       if (c != '\\') {
-        out->push_back(c);
+        const size_t n = utf8_len(t, p);
+        if (!n) return fail("invalid UTF-8");
+        out->append(t, p, n);
+        p += n;
         continue;
       }
-      if (p >= t.size()) return fail("bad escape");
-      c = t[p++];
-      switch (c) {
+      if (++p >= t.size()) return fail("bad escape");
+      switch (t[p++]) {
         case '"': out->push_back('"'); break;
         case '\\': out->push_back('\\'); break;
         case '/': out->push_back('/'); break;
@@ -130,10 +162,14 @@ struct Parser {
         case 'u': {
           uint32_t cp;
           if (!hex4(&cp)) return false;
-          if (cp >= 0xD800 && cp < 0xDC00 && p + 6 <= t.size() && t[p] == '\\' && t[p + 1] == 'u') {
+          if (cp >= 0xDC00 && cp < 0xE000) return fail("lone trailing surrogate");
+          if (cp >= 0xD800 && cp < 0xDC00) {  // must pair with \uDC00-\uDFFF
+            if (t.size() - p < 6 || t[p] != '\\' || t[p + 1] != 'u')
+              return fail("lone leading surrogate");
             p += 2;
             uint32_t lo;
             if (!hex4(&lo)) return false;
+            if (lo < 0xDC00 || lo >= 0xE000) return fail("invalid surrogate pair");
             cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
           }
           put_utf8(cp, out);
@@ -146,8 +182,68 @@ struct Parser {
     ++p;
     return true;
   }
+  static bool digit(char c) { return c >= '0' && c <= '9'; }
+  // RFC 8259 number; integers are classified as serde_json does.
+  bool number(Json *v) {
+    const size_t s0 = p;
+    const bool neg = t[p] == '-';
+    if (neg) ++p;
+    if (p >= t.size() || !digit(t[p])) return fail("invalid number");
+    if (t[p] == '0') {
+      ++p;
+      if (p < t.size() && digit(t[p])) return fail("invalid number (leading zero)");
+    } else {
+      while (p < t.size() && digit(t[p])) ++p;
+    }
+    bool integer = true;
+    if (p < t.size() && t[p] == '.') {
+      integer = false;
+      ++p;
+      if (p >= t.size() || !digit(t[p])) return fail("invalid number");
+      while (p < t.size() && digit(t[p])) ++p;
+    }
+    if (p < t.size() && (t[p] == 'e' || t[p] == 'E')) {
+      integer = false;
+      ++p;
+      if (p < t.size() && (t[p] == '+' || t[p] == '-')) ++p;
+      if (p >= t.size() || !digit(t[p])) return fail("invalid number");
+      while (p < t.size() && digit(t[p])) ++p;
+    }
+    const std::string text = t.substr(s0, p - s0);
+    if (integer) {
+      // magnitude with overflow detection (no strtoll clamping)
+      uint64_t mag = 0;
+      bool fits = true;
+      for (size_t k = neg ? 1 : 0; k < text.size(); ++k) {
+        const uint64_t d = uint64_t(text[k] - '0');
+        if (mag > (UINT64_MAX - d) / 10) {
+          fits = false;
+          break;
+        }
+        mag = mag * 10 + d;
+      }
+      if (fits && !neg && mag <= uint64_t(INT64_MAX)) {
+        v->kind = Json::kInt;
+        v->i = int64_t(mag);
+        return true;
+      }
+      if (fits && !neg) {
+        v->kind = Json::kUInt;
+        v->u = mag;
+        return true;
+      }
+      if (fits && neg && mag <= uint64_t(INT64_MAX) + 1) {
+        v->kind = Json::kInt;
+        v->i = mag == uint64_t(INT64_MAX) + 1 ? INT64_MIN : -int64_t(mag);
+        return true;
+      }
+    }
+    v->kind = Json::kFloat;  // serde_json: f64 (never a valid integer field)
+    v->s = text;
+    return true;
+  }
   bool value(Json *v, int depth) {
-    if (depth > 64) return fail("nesting too deep");
+    if (depth > kMaxDepth) return fail("recursion limit exceeded");
     ws();
     if (p >= t.size()) return fail("unexpected end");
     const char c = t[p];
@@ -166,7 +262,12 @@ struct Parser {
         ws();
         if (p >= t.size() || t[p] != ':') return fail("expected ':'");
         ++p;
-        if (!value(&v->o[k], depth + 1)) return false;
+        auto ins = v->o.emplace(k, Json());
+        if (!ins.second) {  // repeated key: the last value wins, noted
+          v->dup = true;
+          ins.first->second = Json();
+        }
+        if (!value(&ins.first->second, depth + 1)) return false;
         ws();
         if (p < t.size() && t[p] == ',') {
           ++p;
@@ -221,19 +322,8 @@ struct Parser {
       p += 4;
       return true;
     }
-    if (c == '-' || std::isdigit(static_cast<unsigned char>(c))) {
-      const size_t s0 = p;
-      if (t[p] == '-') ++p;
-      while (p < t.size() && std::isdigit(static_cast<unsigned char>(t[p]))) ++p;
-      // fractions/exponents are not produced by the manifest writer; accept and truncate
-      while (p < t.size() && (t[p] == '.' || t[p] == 'e' || t[p] == 'E' || t[p] == '+' ||
-                              t[p] == '-' || std::isdigit(static_cast<unsigned char>(t[p]))))
-        ++p;
-      v->kind = Json::kInt;
-      v->i = std::strtoll(t.substr(s0, p - s0).c_str(), nullptr, 10);
-      return true;
-    }
-    return fail("unexpected character");
+    if (c == '-' || digit(c)) return number(v);
+    return fail("expected value");
   }
 };
 
@@ -241,15 +331,6 @@ Json str_array(const std::vector<std::string> &v) {
   Json a = Json::arr();
   for (const auto &s : v) a.a.push_back(Json::str(s));
   return a;
-}
-
-bool read_str_array(const Json *j, std::vector<std::string> *out) {
-  if (!j || j->kind != Json::kArray) return false;
-  for (const auto &e : j->a) {
-    if (e.kind != Json::kString) return false;
-    out->push_back(e.s);
-  }
-  return true;
 }
 
 }  // namespace
@@ -316,89 +397,136 @@ std::string Manifest::to_json() const {
 }
 
 namespace {
-// Map keys of leaves/segments/blocks are decimal integers (serde's
-// HashMap<i32|usize, _> keys); anything else is a parse error, never an
-// exception across the C-ABI.
-bool parse_key(const std::string &k, int64_t *out) {
-  if (k.empty() || k.size() > 18) return false;
-  size_t i = k[0] == '-' ? 1 : 0;
-  if (i == k.size()) return false;
-  int64_t v = 0;
-  for (; i < k.size(); ++i) {
-    if (k[i] < '0' || k[i] > '9') return false;
-    v = v * 10 + (k[i] - '0');
+
+// serde field readers: a missing field or a value of the wrong type / range
+// is the error serde_json reports ("missing field", "invalid type",
+// "invalid value").
+struct Reader {
+  std::string *err;
+  bool fail(const std::string &m) {
+    if (err) *err = "manifest: " + m;
+    return false;
   }
-  *out = k[0] == '-' ? -v : v;
-  return true;
-}
+  bool object(const Json *v, const char *name, bool check_dup = true) {
+    if (!v) return fail(std::string("missing field '") + name + "'");
+    if (v->kind != Json::kObject) return fail(std::string("invalid type for '") + name + "'");
+    if (check_dup && v->dup) return fail(std::string("duplicate field in '") + name + "'");
+    return true;
+  }
+  bool str(const Json &o, const char *name, std::string *out) {
+    const Json *v = o.get(name);
+    if (!v) return fail(std::string("missing field '") + name + "'");
+    if (v->kind != Json::kString) return fail(std::string("invalid type for '") + name + "'");
+    *out = v->s;
+    return true;
+  }
+  // integer field within [lo, hi] (i64 range); kUInt only for u64 fields
+  bool int_field(const Json &o, const char *name, int64_t lo, int64_t hi, int64_t *out) {
+    const Json *v = o.get(name);
+    if (!v) return fail(std::string("missing field '") + name + "'");
+    if (v->kind != Json::kInt && v->kind != Json::kUInt)
+      return fail(std::string("invalid type for '") + name + "': expected an integer");
+    if (v->kind == Json::kUInt || v->i < lo || v->i > hi)
+      return fail(std::string("invalid value for '") + name + "': out of range");
+    *out = v->i;
+    return true;
+  }
+  bool u64_field(const Json &o, const char *name, uint64_t *out) {
+    const Json *v = o.get(name);
+    if (!v) return fail(std::string("missing field '") + name + "'");
+    if (v->kind == Json::kUInt) {
+      *out = v->u;
+      return true;
+    }
+    if (v->kind != Json::kInt) return fail(std::string("invalid type for '") + name + "': expected u64");
+    if (v->i < 0) return fail(std::string("invalid value for '") + name + "': negative");
+    *out = uint64_t(v->i);
+    return true;
+  }
+  bool str_array(const Json *v, const char *name, std::vector<std::string> *out) {
+    if (!v) return fail(std::string("missing field '") + name + "'");
+    if (v->kind != Json::kArray) return fail(std::string("invalid type for '") + name + "'");
+    for (const auto &e : v->a) {
+      if (e.kind != Json::kString) return fail(std::string("invalid type in '") + name + "'");
+      out->push_back(e.s);
+    }
+    return true;
+  }
+  // map key: decimal integer in [lo, hi] (serde_json parses map keys of
+  // integer type from their string form: optional '-', digits)
+  bool key(const std::string &k, int64_t lo, int64_t hi, int64_t *out) {
+    size_t i = !k.empty() && k[0] == '-' ? 1 : 0;
+    bool ok = i < k.size() && k.size() - i <= 19;
+    uint64_t mag = 0;
+    for (; ok && i < k.size(); ++i) {
+      if (k[i] < '0' || k[i] > '9') ok = false;
+      else mag = mag * 10 + uint64_t(k[i] - '0');
+    }
+    const bool neg = !k.empty() && k[0] == '-';
+    ok = ok && mag <= uint64_t(INT64_MAX);
+    const int64_t v = neg ? -int64_t(mag) : int64_t(mag);
+    if (!ok || v < lo || v > hi) return fail("map key '" + k + "' is not a valid integer key");
+    *out = v;
+    return true;
+  }
+};
+
 }  // namespace
 
 bool Manifest::from_json(const std::string &text, Manifest *m, std::string *err) {
   Json j;
   if (!Json::parse(text, &j, err)) return false;
-  auto need = [&](const Json *v, Json::Kind k, const char *name) {
-    if (!v || v->kind != k) {
-      if (err) *err = std::string("manifest: missing or invalid '") + name + "'";
-      return false;
-    }
-    return true;
-  };
-  if (!need(&j, Json::kObject, "<root>")) return false;
-  const Json *v;
-  if (!need(v = j.get("original_hash"), Json::kString, "original_hash")) return false;
-  m->original_hash = v->s;
-  if (!need(v = j.get("name"), Json::kString, "name")) return false;
-  m->name = v->s;
-  if (!need(v = j.get("size"), Json::kInt, "size")) return false;
-  m->size = v->i;
-  if ((v = j.get("time_of_creation")) && v->kind == Json::kString) m->time_of_creation = v->s;
-  if (!need(v = j.get("tier"), Json::kInt, "tier")) return false;
-  m->tier = int(v->i);
-  if (!need(v = j.get("segment_size"), Json::kInt, "segment_size")) return false;
-  m->segment_size = uint64_t(v->i);
-  const Json *ec = j.get("erasure_coding");
-  if (!need(ec, Json::kObject, "erasure_coding")) return false;
-  if ((v = ec->get("data_shards")) && v->kind == Json::kInt) m->data_shards = int(v->i);
-  if ((v = ec->get("parity_shards")) && v->kind == Json::kInt) m->parity_shards = int(v->i);
-  if ((v = ec->get("type")) && v->kind == Json::kString) m->ec_type = v->s;
-  const Json *mt = j.get("merkle_tree");
-  if (!need(mt, Json::kObject, "merkle_tree")) return false;
-  if (!need(v = mt->get("root"), Json::kString, "merkle_tree.root")) return false;
-  m->root = v->s;
-  auto key = [&](const std::string &k, int64_t *out) {
-    if (parse_key(k, out)) return true;
-    if (err) *err = "manifest: map key '" + k + "' is not an integer";
+  Reader r{err};
+  if (!r.object(&j, "<root>")) return false;
+  int64_t v;
+  if (!r.str(j, "original_hash", &m->original_hash) || !r.str(j, "name", &m->name) ||
+      !r.int_field(j, "size", INT64_MIN, INT64_MAX, &m->size) ||
+      !r.str(j, "time_of_creation", &m->time_of_creation) ||
+      !r.int_field(j, "tier", 0, 255, &v))  // u8
     return false;
-  };
+  m->tier = int(v);
+  if (!r.u64_field(j, "segment_size", &m->segment_size)) return false;
+  const Json *ec = j.get("erasure_coding");
+  if (!r.object(ec, "erasure_coding") || !r.int_field(*ec, "data_shards", -128, 127, &v))  // i8
+    return false;
+  m->data_shards = int(v);
+  if (!r.int_field(*ec, "parity_shards", -128, 127, &v)) return false;
+  m->parity_shards = int(v);
+  if (!r.str(*ec, "type", &m->ec_type)) return false;
+  const Json *mt = j.get("merkle_tree");
+  if (!r.object(mt, "merkle_tree") || !r.str(*mt, "root", &m->root)) return false;
   int64_t id;
-  if ((v = mt->get("leaves")) && v->kind == Json::kObject)
-    for (const auto &kv : v->o) {
-      if (!key(kv.first, &id)) return false;
-      if (kv.second.kind == Json::kString) m->leaves[id] = kv.second.s;
+  if (const Json *lv = mt->get("leaves")) {  // HashMap<i32, String>, #[serde(default)]
+    if (!r.object(lv, "leaves", false)) return false;
+    for (const auto &kv : lv->o) {
+      if (!r.key(kv.first, INT32_MIN, INT32_MAX, &id)) return false;
+      if (kv.second.kind != Json::kString) return r.fail("invalid type in 'leaves'");
+      m->leaves[id] = kv.second.s;
     }
-  if ((v = mt->get("segments")) && v->kind == Json::kObject)
-    for (const auto &kv : v->o) {
+  }
+  if (const Json *sg = mt->get("segments")) {  // HashMap<usize, SegmentHashes>
+    if (!r.object(sg, "segments", false)) return false;
+    for (const auto &kv : sg->o) {
+      if (!r.key(kv.first, 0, INT64_MAX, &id)) return false;
       SegmentHashes sh;
-      const Json *d = kv.second.get("data");
-      if (!d || d->kind != Json::kString || !read_str_array(kv.second.get("parity"), &sh.parity)) {
-        if (err) *err = "manifest: bad segments entry";
+      if (!r.object(&kv.second, "segments entry") || !r.str(kv.second, "data", &sh.data) ||
+          !r.str_array(kv.second.get("parity"), "parity", &sh.parity))
         return false;
-      }
-      sh.data = d->s;
-      if (!key(kv.first, &id)) return false;
-      m->segments[id] = sh;
+      m->segments[id] = std::move(sh);
     }
-  if ((v = mt->get("blocks")) && v->kind == Json::kObject)
-    for (const auto &kv : v->o) {
+  }
+  if (const Json *bl = mt->get("blocks")) {  // HashMap<usize, BlockHashes>
+    if (!r.object(bl, "blocks", false)) return false;
+    for (const auto &kv : bl->o) {
+      if (!r.key(kv.first, 0, INT64_MAX, &id)) return false;
       BlockHashes bh;
-      if (!read_str_array(kv.second.get("segments"), &bh.segments) ||
-          !read_str_array(kv.second.get("parity"), &bh.parity)) {
-        if (err) *err = "manifest: bad blocks entry";
+      if (!r.object(&kv.second, "blocks entry") ||
+          !r.str_array(kv.second.get("segments"), "segments", &bh.segments) ||
+          !r.str_array(kv.second.get("parity"), "parity", &bh.parity))
         return false;
-      }
-      if (!key(kv.first, &id)) return false;
-      m->blocks[id] = bh;
+      m->blocks[id] = std::move(bh);
     }
+  }
   return true;
 }
 

@@ -16,10 +16,18 @@
 
 namespace bfrs {
 
+// JSON value.  Numbers keep serde_json's three classes: kInt (an integer that
+// fits i64), kUInt (a non-negative integer above i64's range that fits u64)
+// and kFloat (a fraction, an exponent, or an integer beyond u64; its text is
+// kept in `s`), so a typed field refuses what serde would.  `dup`: the object
+// had a repeated key (serde: "duplicate field" for a struct; a map keeps the
+// last value).
 struct Json {
-  enum Kind { kNull, kBool, kInt, kString, kArray, kObject } kind = kNull;
+  enum Kind { kNull, kBool, kInt, kUInt, kFloat, kString, kArray, kObject } kind = kNull;
   bool b = false;
+  bool dup = false;
   int64_t i = 0;
+  uint64_t u = 0;
   std::string s;
   std::vector<Json> a;
   std::map<std::string, Json> o;
@@ -52,6 +60,9 @@ struct Json {
     return it == o.end() ? nullptr : &it->second;
   }
   std::string dump() const;                       // compact, sorted keys
+  // RFC 8259 JSON as serde_json::from_str takes it: valid UTF-8, no raw
+  // control characters in strings, paired surrogate escapes, strict number
+  // grammar, nesting depth <= 128 (serde_json's recursion limit).
   static bool parse(const std::string &text, Json *out, std::string *err);
 };
 
@@ -77,6 +88,12 @@ struct Manifest {
   // tier 1 writes merkle_tree = {leaves, root} (MerkleTree::get_json,
   // src/merkle_tree/mod.rs:240-251); tiers 2/3 the full MerkleTreeStructure.
   std::string to_json() const;
+  // ManifestFile::new (manifest.rs:47-53): serde's derive rules for the
+  // structs at manifest.rs:6-45 -- every field required except the three
+  // merkle_tree maps (#[serde(default)]), exact integer types (size i64,
+  // tier u8, segment_size u64, shard counts i8, leaf keys i32, segment /
+  // block keys usize), unknown fields ignored, duplicate struct fields an
+  // error.  Never throws.
   static bool from_json(const std::string &text, Manifest *m, std::string *err);
 };
 

@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "../../include/bfrs.h"
+#include "host_copy.hpp"
 #include "kernels.hpp"
 #include "plan.hpp"
 
@@ -121,10 +122,6 @@ struct CodecPool {
   void release(std::unique_ptr<CodecSlot> slot);
   ~CodecPool();
 };
-
-// memcpy on up to 8 threads for large buffers (pageable <-> pinned staging).
-// Never throws: a thread that cannot start leaves its part to the caller.
-void host_copy(uint8_t *dst, const uint8_t *src, size_t n);
 
 struct Context {
   int device = 0;

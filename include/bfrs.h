@@ -321,6 +321,18 @@ typedef struct {
 int bfrs_archive_open(bfrs_ctx *ctx, const char *archive_dir, size_t cache_segments,
                       int write_back, bfrs_archive **out);
 int bfrs_archive_size(bfrs_archive *a, uint64_t *size);
+/* The mount's getattr / read geometry of an archive directory (host only, no
+ * context): the manifest's size, tier and segment size
+ * (src/mount/filesystem_unix.rs:153-174 get_file_attr, :428-434 read), with
+ * the derived segment and block counts.  The manifest is validated first
+ * (tier 1..3, size <= 2^50, 0 < segment_size <= 2^36 for tiers 2/3, one
+ * manifest entry per segment / block of the right shape); a damaged or
+ * hostile manifest fails with BFRS_E_WRAPPER, never a crash. */
+typedef struct {
+  uint64_t size, segment_size, segments, blocks;
+  int32_t tier, reserved;
+} bfrs_archive_attr;
+int bfrs_archive_stat(const char *archive_dir, bfrs_archive_attr *out);
 /* Reads up to len bytes at offset (clamped at EOF; *nread = bytes copied). */
 int bfrs_archive_read(bfrs_archive *a, uint64_t offset, size_t len, uint8_t *out, size_t *nread);
 int bfrs_archive_stats_get(bfrs_archive *a, bfrs_archive_stats *out);

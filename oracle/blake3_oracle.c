@@ -64,7 +64,7 @@ static void compress(const uint32_t cv[8], const uint32_t block[16], uint64_t co
 
 static void words_le(const uint8_t *p, size_t n, uint32_t w[16]) {
   uint8_t buf[64] = {0};
-  memcpy(buf, p, n);
+  if (n) memcpy(buf, p, n); /* p is NULL for the empty message */
   for (int i = 0; i < 16; ++i)
     w[i] = (uint32_t)buf[4 * i] | (uint32_t)buf[4 * i + 1] << 8 | (uint32_t)buf[4 * i + 2] << 16 |
            (uint32_t)buf[4 * i + 3] << 24;

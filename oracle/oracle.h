@@ -49,6 +49,10 @@ int oracle_decode_rate(int engine, int rate, uint32_t k, uint32_t m, size_t shar
 int oracle_batch(int engine, int decode, int threads, uint32_t nblocks, const uint32_t *k,
                  uint32_t m, size_t shard_bytes, const uint8_t *const *const *orig,
                  const uint8_t *const *const *rec, uint8_t *const *const *out);
+/* copies = 1: each block also pays the reference wrappers' copies (bench.py) */
+int oracle_batch2(int engine, int decode, int threads, uint32_t nblocks, const uint32_t *k,
+                  uint32_t m, size_t shard_bytes, const uint8_t *const *const *orig,
+                  const uint8_t *const *const *rec, uint8_t *const *const *out, int copies);
 
 uint16_t oracle_gf_exp(uint16_t i);
 uint16_t oracle_gf_log(uint16_t x);

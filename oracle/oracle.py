@@ -14,7 +14,8 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liboracle.so")
+# ORACLE_LIB: the sanitizer build (make -C oracle sanitize -> liboracle_asan.so)
+LIB_PATH = os.path.join(HERE, os.environ.get("ORACLE_LIB", "liboracle.so"))
 
 ENGINE_SCALAR = 0
 ENGINE_AVX2 = 1

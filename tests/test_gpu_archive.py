@@ -669,3 +669,46 @@ def test_config5_full_size_corrupted_read(ctx, bfrs, oracle, tmp_path):
         assert segs == blk["segments"], b
         roots.append(oracle.merkle_root_hex(segs + blk["parity"]))
     assert oracle.merkle_root_hex(roots) == m["merkle_tree"]["root"]
+
+
+# ---------------------------------------------------------------- malformed manifests
+def test_malformed_manifests_through_gpu_entry_points(ctx, bfrs, tmp_path):
+    """tests/malformed_manifests through the entry points that need a device:
+    archive open + read (the mount's read path), health check and repair, on
+    a real tier-3 archive of the corpus's geometry (35 segments of 64 KiB,
+    blocks of 30 + 5) whose manifest is replaced by each corpus file.  Every
+    call returns a verdict or an error code; nothing crashes or hangs, and
+    no manifest makes repair write outside the archive."""
+    import glob
+    import shutil
+    corpus = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "malformed_manifests",
+                                           "*.json")))
+    assert len(corpus) >= 100
+    S = 65536
+    path, d = _file(tmp_path, 35 * S - 100, seed=31, name="big.bin")
+    src = bfrs.commit(ctx, path, str(tmp_path / "archive"), segment_size=S, tier=3)
+    outcomes = {}
+    for f in corpus:
+        name = os.path.basename(f)[:-5]
+        adir = str(tmp_path / "work" / name)
+        shutil.copytree(src, adir)
+        shutil.copyfile(f, os.path.join(adir, "manifest.json"))
+        before = sorted(os.listdir(tmp_path))
+        got = []
+        for call in (lambda: bfrs.Archive(ctx, adir, cache_segments=4).read(0, 4096),
+                     lambda: bfrs.health_check(ctx, adir)["status"],
+                     lambda: bfrs.repair(ctx, adir)):
+            try:
+                call()
+                got.append("ok")
+            except bfrs.BfrsError as e:
+                assert e.code in (bfrs.E_WRAPPER, bfrs.E_NOT_ENOUGH_SHARDS,
+                                  bfrs.E_INVALID_SHARD_SIZE), (name, e.code, str(e))
+                got.append(e.code)
+        assert sorted(os.listdir(tmp_path)) == before, name
+        outcomes[name] = got
+        shutil.rmtree(adir)
+    # the controls open; a manifest that does not parse fails every call
+    assert outcomes["valid_tier3"][0] in ("ok", bfrs.E_NOT_ENOUGH_SHARDS)
+    for name in ("empty", "deep_arrays", "size_negative", "tier_four", "blocks_too_few"):
+        assert outcomes[name] == [bfrs.E_WRAPPER] * 3, (name, outcomes[name])
