@@ -373,6 +373,29 @@ def check_parity_golden(parity_rows, shapes, S, seed, name):
             "mismatched": bad, "match": not bad}
 
 
+def check_config1(ctx):
+    """BASELINE configs[0]: a single 8 MB file's RS(1,3) through the product
+    (Chunker::generate_parity_segmented, generate.rs:26-57, then
+    recover_segment_rs13, recovery.rs:43-79): the 3 parity shards are the
+    data zero-padded to a multiple of 64 (LowRate RS(1,3) = replication,
+    src/filestore/README.md:178; tests/golden/rs_small.json's RS(1,3) cases)
+    and the recovery returns the file's bytes.  8 MiB, 8,000,000 B and an
+    unaligned 8,000,002 B (seed 1, bfrs/synth.py)."""
+    import numpy as np
+    import bfrs
+    from bfrs import synth
+    res = {}
+    for n in (8 * 1024 * 1024, 8_000_000, 8_000_002):
+        data = synth.segment_np(1, 0, n)
+        par = bfrs.Chunker(ctx).generate_parity_segmented(data)
+        padded = np.pad(data, (0, (n + 63) // 64 * 64 - n)).tobytes()
+        ok = par == [padded] * 3
+        ok = ok and bfrs.recover_segment_rs13(ctx, par, expected_size=n) == data.tobytes()
+        res[str(n)] = bool(ok)
+    return {"sizes": res, "match": all(res.values()),
+            "what": "RS(1,3) parity == pad64(data) x 3, and recover_segment_rs13 == data"}
+
+
 def check_restored(sets):
     """The restored shards of the timed decodes equal the erased originals."""
     seg, bad = 0, []
@@ -583,6 +606,7 @@ def crate_api(ctx, sets, reps=3, staging_ab=True):
                                                     [np.empty(S, np.uint8) for _ in range(3)]))
         par = [np.empty(S, np.uint8) for _ in range(3)]
         chk.generate_parity_into(segs, k, 3, par)
+        tg_reuse = timed(lambda: chk.generate_parity_into(segs, k, 3, par))
         target = sets.erased[0][0]
         slots = [None if i == target else segs[i] for i in range(k)] + [None] * (30 - k)
         tr = timed(lambda: bfrs.recover_segment_rs30_3_into(c, slots, par, target,
@@ -590,9 +614,10 @@ def crate_api(ctx, sets, reps=3, staging_ab=True):
         got = np.empty(S, np.uint8)
         assert bfrs.recover_segment_rs30_3_into(c, slots, par, target, got) == S
         assert np.array_equal(got, segs[target]), "crate_api recover mismatch"
-        return tg, tr, par, slots, target
+        tr_reuse = timed(lambda: bfrs.recover_segment_rs30_3_into(c, slots, par, target, got))
+        return tg, tr, par, slots, target, tg_reuse, tr_reuse
 
-    tg, tr, par, slots, target = wrappers(ctx)
+    tg, tr, par, slots, target, tg_reuse, tr_reuse = wrappers(ctx)
     tg_py = timed(lambda: ch.generate_parity(segs, k, 3))
     tr_py = timed(lambda: bfrs.recover_segment_rs30_3(ctx, slots, par, target))
     gib = k * S / 2**30
@@ -674,9 +699,11 @@ def crate_api(ctx, sets, reps=3, staging_ab=True):
     res = {
         "staging": os.environ.get("BFRS_CODEC_STAGING", "direct"),
         "generate_parity": {"ms": round(tg * 1e3, 2), "GiBps": round(gib / tg, 2),
+                            "touched_outputs_ms": round(tg_reuse * 1e3, 2),
                             "python_wrapper_ms": round(tg_py * 1e3, 2),
                             "what": f"RS({k},3) block of {S >> 20} MiB segments, pageable host in/out"},
         "recover_segment_rs30_3": {"ms": round(tr * 1e3, 2), "GiBps_of_block": round(gib / tr, 2),
+                                   "touched_output_ms": round(tr_reuse * 1e3, 2),
                                    "python_wrapper_ms": round(tr_py * 1e3, 2),
                                    "what": "one erased segment of that block, pageable host in/out"},
         "breakdown": bd,
@@ -700,10 +727,11 @@ def crate_api(ctx, sets, reps=3, staging_ab=True):
             else:
                 os.environ["BFRS_CODEC_STAGING"] = old
         try:
-            pg, pr, *_ = wrappers(c2)
+            pg, pr, _, _, _, pg_reuse, pr_reuse = wrappers(c2)
         finally:
             c2.close()
         res["pinned_staging"] = {"generate_parity_ms": round(pg * 1e3, 2),
+                                 "generate_parity_touched_outputs_ms": round(pg_reuse * 1e3, 2),
                                  "recover_segment_rs30_3_ms": round(pr * 1e3, 2),
                                  "what": "BFRS_CODEC_STAGING=pinned (round 2: memcpy into pinned "
                                          "rows, then H2D), second context, same block"}
@@ -1059,6 +1087,7 @@ def main():
         except (OSError, MemoryError, RuntimeError) as e:  # not AssertionError: a wrong result fails the run
             return {"error": f"{type(e).__name__}: {e}"}
 
+    c1 = check_config1(ctx) if not rt.stub else None
     if n1 and args.pcie == "auto" and not args.strong:
         pcie = guarded(pcie_inclusive, ctx, sets)
     if n1 and args.crate == "auto" and not args.strong:
@@ -1129,6 +1158,7 @@ def main():
         line["c5"] = c5
     line["c4_strong"] = c4
     line["parity_check"] = {
+        "c1_rs13": c1,
         "c2_encode": my_check["encode"], "c3_decode": my_check["decode"],
         "ranks_ok": [bool(x) for x in ranks_ok],
         "c4_encode": (c4 or {}).get("parity_check", {}).get("encode"),
@@ -1136,7 +1166,7 @@ def main():
         "c5_blake3": None if c5 is None else c5.get("blake3_match"),
         "when": "after the timed region, on the buffers the timed launches wrote",
     }
-    flags = [all(ranks_ok), (my_check["encode"] or {}).get("match"),
+    flags = [all(ranks_ok), (my_check["encode"] or {}).get("match"), (c1 or {}).get("match"),
              (c4 or {}).get("parity_check", {}).get("encode", {}).get("match"),
              (c4 or {}).get("parity_check", {}).get("decode", {}).get("match"),
              None if c5 is None else c5.get("blake3_match")]

@@ -20,12 +20,13 @@ namespace {
 
 int wrapper_error(const std::string &msg) { return set_error(BFRS_E_WRAPPER, msg); }
 
-// First-touch of the caller's output buffers on a helper thread while the
-// input shards stream to the device.  The reference's outputs are fresh Vecs
-// (generate.rs:95-96, recovery.rs:167-169), and faulting ~100 MiB of fresh
-// pages inside the D2H halves its rate (bench crate_api); done
-// here the faults overlap the H2D, which is PCIe-bound and leaves the CPU
-// idle.  The bytes written are overwritten by the D2H.
+// First-touch of the caller's output buffer on a helper thread while the
+// input shards stream to the device (recover_segment_rs30_3: one 32 MiB
+// shard).  The reference's outputs are fresh Vecs (recovery.rs:167-169), and
+// faulting fresh pages inside a D2H runs at a fraction of the link rate; done
+// here the faults overlap the PCIe-bound H2D.  The bytes written are
+// overwritten by the D2H.  (generate_parity's three outputs take the pinned
+// rows + threaded copy-out instead: codec_objects.cpp)
 class Prefault {
  public:
   Prefault(uint8_t *const *bufs, size_t n, size_t len) {
@@ -83,7 +84,6 @@ int bfrs_generate_parity(bfrs_ctx *ctx, const uint8_t *const *segments, const si
   if (!parity_out) return set_error(BFRS_E_INVALID_ARGUMENT, "generate_parity: parity_out NULL");
   for (size_t j = 0; j < parity_shards; ++j)
     if (!parity_out[j]) return set_error(BFRS_E_INVALID_ARGUMENT, "parity buffer is NULL");
-  Prefault pf(parity_out, parity_shards, max_len);
   // generate.rs:75-82 + 87-89 — zero-pad each segment to max_len and add it
   std::vector<uint8_t> padded;
   for (size_t i = 0; i < n_segments; ++i) {
@@ -95,9 +95,9 @@ int bfrs_generate_parity(bfrs_ctx *ctx, const uint8_t *const *segments, const si
     }
     if ((rc = bfrs_encoder_add_original_shard(enc.p, src, max_len))) return rc;
   }
-  pf.join();
-  // generate.rs:92 + 95-96: encode, the recovery shards straight into the
-  // caller's buffers (the reference's to_vec copies)
+  // generate.rs:92 + 95-96: encode; the recovery shards come back into the
+  // slot's pinned rows and are copied out on several threads, which is also
+  // where a fresh Vec's pages fault in (the reference's to_vec copies)
   return encoder_encode_to_host(enc.p, parity_out);
   BFRS_API_END
 }

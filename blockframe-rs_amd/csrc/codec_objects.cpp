@@ -146,23 +146,36 @@ int encoder_run(bfrs_encoder *e) {
 }  // namespace
 
 int bfrs::encoder_encode_to_host(bfrs_encoder *e, uint8_t *const *outs) {
+  // D2H into the pinned rows, then host_copy (up to 8 threads per shard) into
+  // the caller's buffers.  A D2H straight into a fresh pageable buffer faults
+  // its pages inside the copy at a fraction of the link rate, and touching
+  // them on a helper thread during the H2D of the inputs contended with the
+  // pageable H2D (bench crate_api).  Shard j's copy-out
+  // overlaps the D2H of shard j + 1.
   int rc = encoder_run(e);
   if (rc) return rc;
   hipStream_t st = e->slot->stream;
+  std::vector<hipEvent_t> done(e->m, nullptr);
+  struct Events {
+    std::vector<hipEvent_t> &v;
+    ~Events() {
+      for (hipEvent_t x : v)
+        if (x) (void)hipEventDestroy(x);
+    }
+  } guard{done};
   for (size_t j = 0; j < e->m; ++j) {
-    if (e->pool->staging == Staging::kPinned)  // round 2: pinned row, then a host copy
-      HIP_TRY(hipMemcpyAsync(e->h_row(e->k + j), e->d_row(e->k + j), e->shard_bytes,
-                             hipMemcpyDeviceToHost, st));
-    else
-      HIP_TRY(hipMemcpyAsync(outs[j], e->d_row(e->k + j), e->shard_bytes, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(e->h_row(e->k + j), e->d_row(e->k + j), e->shard_bytes,
+                           hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipEventCreateWithFlags(&done[j], hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(done[j], st));
   }
-  HIP_TRY(hipStreamSynchronize(st));
-  if (e->pool->staging == Staging::kPinned)
-    for (size_t j = 0; j < e->m; ++j) host_copy(outs[j], e->h_row(e->k + j), e->shard_bytes);
-  // the pinned rows do not hold the recovery shards: the object is spent
-  // (the next add_original_shard starts a new round, as after encode())
+  for (size_t j = 0; j < e->m; ++j) {
+    HIP_TRY(hipEventSynchronize(done[j]));
+    host_copy(outs[j], e->h_row(e->k + j), e->shard_bytes);
+  }
+  // the pinned rows hold the recovery shards too, as after encode()
   e->encoded = true;
-  e->fetched_to_pinned = e->pool->staging == Staging::kPinned;
+  e->fetched_to_pinned = true;
   return BFRS_OK;
 }
 
