@@ -8,6 +8,8 @@
 // The reference's println! calls inside the hot path (generate.rs:51-54,
 // 98-101) are deliberately not reproduced.
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstring>
 #include <sstream>
 #include <thread>
@@ -85,6 +87,7 @@ int bfrs_generate_parity(bfrs_ctx *ctx, const uint8_t *const *segments, const si
   for (size_t j = 0; j < parity_shards; ++j)
     if (!parity_out[j]) return set_error(BFRS_E_INVALID_ARGUMENT, "parity buffer is NULL");
   // generate.rs:75-82 + 87-89 — zero-pad each segment to max_len and add it
+  const auto t_add = std::chrono::steady_clock::now();
   std::vector<uint8_t> padded;
   for (size_t i = 0; i < n_segments; ++i) {
     const uint8_t *src = segments[i];
@@ -95,6 +98,10 @@ int bfrs_generate_parity(bfrs_ctx *ctx, const uint8_t *const *segments, const si
     }
     if ((rc = bfrs_encoder_add_original_shard(enc.p, src, max_len))) return rc;
   }
+  if (std::getenv("BFRS_TRACE"))  // measurement aid (tools/crate_probe.py)
+    std::fprintf(stderr, "bfrs trace: generate_parity adds %.3f ms\n",
+                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_add)
+                     .count());
   // generate.rs:92 + 95-96: encode; the recovery shards come back into the
   // slot's pinned rows and are copied out on several threads, which is also
   // where a fresh Vec's pages fault in (the reference's to_vec copies)

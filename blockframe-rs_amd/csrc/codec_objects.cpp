@@ -5,12 +5,12 @@
 //
 // Each object holds a CodecSlot from its context's pool (runtime.hpp): k + m
 // shard rows of HBM, the same rows of pinned host memory, and a stream of its
-// own.  add_*_shard moves the caller's bytes to the shard's device row before
-// it returns (the crate likewise copies each added shard into its work area,
-// so the caller may reuse its buffer at once): by default one DMA straight
-// from the caller's buffer (Staging::kDirect); BFRS_CODEC_STAGING=pinned
-// copies into the pinned row first and queues its H2D (round 2's path,
-// DESIGN.md §7c).  encode() queues the HIP pass and the D2H of the recovery
+// own.  add_*_shard takes the caller's bytes before it returns (the crate
+// likewise copies each added shard into its work area, so the caller may
+// reuse its buffer at once): by default a threaded memcpy into the slot's
+// pinned row and an async H2D that overlaps the next shard's copy
+// (Staging::kPinned); BFRS_CODEC_STAGING=direct DMAs straight from the
+// caller's buffer instead.  encode() queues the HIP pass and the D2H of the recovery
 // shards into pinned rows; decode() runs the pass and restored_original(i)
 // fetches row i on first use (BlockFrame asks for one target,
 // recovery.rs:166-170).  Results stay valid until the next call on the
@@ -19,6 +19,8 @@
 // (shared), so it may be freed after bfrs_close; every other call needs the
 // context open.
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstring>
 #include <sstream>
 #include <thread>
@@ -169,10 +171,19 @@ int bfrs::encoder_encode_to_host(bfrs_encoder *e, uint8_t *const *outs) {
     HIP_TRY(hipEventCreateWithFlags(&done[j], hipEventDisableTiming));
     HIP_TRY(hipEventRecord(done[j], st));
   }
+  using clk = std::chrono::steady_clock;
+  double wait_ms = 0, copy_ms = 0;
   for (size_t j = 0; j < e->m; ++j) {
+    const auto t0 = clk::now();
     HIP_TRY(hipEventSynchronize(done[j]));
+    const auto t1 = clk::now();
     host_copy(outs[j], e->h_row(e->k + j), e->shard_bytes);
+    wait_ms += std::chrono::duration<double, std::milli>(t1 - t0).count();
+    copy_ms += std::chrono::duration<double, std::milli>(clk::now() - t1).count();
   }
+  if (std::getenv("BFRS_TRACE"))  // measurement aid (tools/crate_probe.py)
+    std::fprintf(stderr, "bfrs trace: encode_to_host wait %.3f ms, copy-out %.3f ms\n", wait_ms,
+                 copy_ms);
   // the pinned rows hold the recovery shards too, as after encode()
   e->encoded = true;
   e->fetched_to_pinned = true;

@@ -197,9 +197,9 @@ int Context::init(int dev) {
     codec_pool->cached = (end != e && v > 0) ? size_t(std::min<long>(v, 1024)) : 0;
   }
   if (const char *e = std::getenv("BFRS_CODEC_STAGING")) {
-    if (std::strcmp(e, "pinned") == 0)
-      codec_pool->staging = Staging::kPinned;
-    else if (std::strcmp(e, "direct") != 0 && *e)
+    if (std::strcmp(e, "direct") == 0)
+      codec_pool->staging = Staging::kDirect;
+    else if (std::strcmp(e, "pinned") != 0 && *e)
       return set_error(BFRS_E_INVALID_ARGUMENT,
                        std::string("BFRS_CODEC_STAGING=") + e + ": expected direct or pinned");
   }

@@ -102,11 +102,16 @@ struct CodecSlot {
 };
 
 // How add_*_shard moves a caller's shard to the device (BFRS_CODEC_STAGING):
-//   kDirect: hipMemcpyAsync straight from the caller's (pageable) buffer on
-//            the slot stream, then a stream sync so the caller may reuse the
-//            buffer on return, as with the crate's copy (default: the PCIe
-//            link takes pageable sources at the pinned rate);
-//   kPinned: memcpy into the slot's pinned row, then an async H2D (round 2).
+//   kPinned: memcpy into the slot's pinned row on up to 8 threads, then an
+//            async H2D, so copying shard i+1 overlaps the DMA of shard i
+//            (default);
+//   kDirect: hipMemcpyAsync straight from the caller's pageable buffer, then
+//            a stream sync.  Equal on buffers HIP has seen before, but the
+//            runtime locks a new buffer's pages on first use, and BlockFrame
+//            hands over new mmap'd segments for every block: measured 27-51 ms
+//            against 26-28 ms for kPinned per 32 MiB RS(30,3) block in the
+//            bench process.
+// Either way the caller's buffer is free again when add returns.
 enum class Staging { kDirect, kPinned };
 
 // The slot cache of one context.  Shared (shared_ptr) by the context and by
@@ -114,7 +119,7 @@ enum class Staging { kDirect, kPinned };
 // or frees its slot safely; the pool goes away with the last of them.
 struct CodecPool {
   int device = 0;
-  Staging staging = Staging::kDirect;
+  Staging staging = Staging::kPinned;
   std::mutex mu;
   std::vector<std::unique_ptr<CodecSlot>> free;
   size_t cached = 2;  // BFRS_CODEC_SLOTS: idle slots kept (0 = none)

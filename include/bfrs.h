@@ -36,9 +36,10 @@
  *
  * Environment, read by bfrs_open:
  *   BFRS_CODEC_SLOTS    idle codec slots kept (default 2; 0 = none)
- *   BFRS_CODEC_STAGING  "direct" (default: add_*_shard DMAs straight from the
- *                       caller's buffer) or "pinned" (memcpy into a pinned row
- *                       first); either way the buffer is free on return
+ *   BFRS_CODEC_STAGING  "pinned" (default: add_*_shard copies into a pinned
+ *                       row on several threads and queues its H2D) or
+ *                       "direct" (one DMA straight from the caller's buffer);
+ *                       either way the buffer is free on return
  *   BFRS_KERNEL_VARIANT unset or 76 (default kernel); 75 / 73 force the looped
  *                       subfield / general kernels; anything else fails
  *                       bfrs_open with BFRS_E_INVALID_ARGUMENT (the A/B

@@ -25,11 +25,12 @@ from bfrs import _ptr_array, _sz, lib  # noqa: E402
 K, S, REPS = 30, 32 << 20, 5
 
 
-def best(f, reps=REPS):
+def best(f, reps=REPS, prep=None):
     ts = []
     for _ in range(reps):
+        arg = prep() if prep else None
         t0 = time.perf_counter()
-        f()
+        f(arg) if prep else f()
         ts.append(time.perf_counter() - t0)
     return round(min(ts) * 1e3, 2), round(float(np.median(ts)) * 1e3, 2)
 
@@ -55,6 +56,10 @@ def main():
         del t
     rng = np.random.default_rng(7)
     segs = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(K)]
+    if os.environ.get("PROBE_TORCH_SEGS"):  # segments as bench.py makes them: .cpu() of device rows
+        dev = torch.from_numpy(np.stack(segs)).cuda()
+        segs = [dev[i].cpu().numpy() for i in range(K)]
+        del dev
     res = {"what": f"RS({K},3), {S >> 20} MiB segments, ms (best, median of {REPS})"}
     ps, _k1 = _ptr_array([s.ctypes.data for s in segs])
     lens = (_sz * K)(*[S] * K)
@@ -68,6 +73,22 @@ def main():
             assert rc == 0, rc
 
         res[f"cabi_fresh_{mode}"] = best(lambda: cabi([np.empty(S, np.uint8) for _ in range(3)]))
+
+        # fresh INPUT buffers too (untimed copies): BlockFrame's segments are
+        # new mmap'd file pages for every block, never seen by HIP before
+        def fresh_inputs():
+            return [np.array(x) for x in segs]
+
+        def cabi_new_inputs(xs):
+            p2, _k3 = _ptr_array([x.ctypes.data for x in xs])
+            outs_now = outs_fresh()  # kept alive across the call
+            po, _k2 = _ptr_array([o.ctypes.data for o in outs_now])
+            rc = lib().bfrs_generate_parity(ctx.handle, p2, lens, K, K, 3, po, ctypes.byref(plen))
+            assert rc == 0, rc
+
+        def outs_fresh():
+            return [np.empty(S, np.uint8) for _ in range(3)]
+        res[f"cabi_fresh_inputs_{mode}"] = best(cabi_new_inputs, prep=fresh_inputs)
         outs = [np.zeros(S, np.uint8) for _ in range(3)]
         res[f"cabi_reuse_{mode}"] = best(lambda: cabi(outs))
         if mode == "direct":
