@@ -28,10 +28,15 @@ def _run(args, env_extra=None, timeout=120):
     return res
 
 
-def test_codec_soak_short():
-    res = _run(["tools/soak.py", "--seconds", "8", "--threads", "4", "--seed", "7"],
-               {"BFRS_PLAN_CACHE": "16"})
-    assert res["cases"] > 100 and set(res["by_api"]) == {"host", "host_batch", "dev_batch", "objects"}
+@pytest.mark.parametrize("staging,slots", [("pinned", "2"), ("direct", "0")])
+def test_codec_soak_short(staging, slots):
+    """Both codec-object stagings; slots 0 = every object frees its slot on
+    release (the empty-pool path)."""
+    res = _run(["tools/soak.py", "--seconds", "6", "--threads", "4", "--seed", "7"],
+               {"BFRS_PLAN_CACHE": "16", "BFRS_CODEC_STAGING": staging, "BFRS_CODEC_SLOTS": slots})
+    assert res["cases"] > 100 and set(res["by_api"]) == {"host", "host_batch", "dev_batch", "objects",
+                                                         "wrappers"}
+    assert res["codec_staging"] == staging
 
 
 def test_blake3_soak_short():

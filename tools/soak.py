@@ -49,9 +49,11 @@ def main():
         rng = np.random.default_rng(a.seed + tid)
         stream = torch.cuda.Stream()
         while time.perf_counter() < stop:
-            api = str(rng.choice(["host", "host_batch", "dev_batch", "objects"]))
+            api = str(rng.choice(["host", "host_batch", "dev_batch", "objects", "wrappers"]))
             k, m = one_block(rng)
-            nblocks = 1 if api in ("host", "objects") else int(rng.integers(1, 5))
+            if api == "wrappers" and rng.random() < 0.5:  # recover_segment_rs30_3's shape
+                k, m = 30, 3
+            nblocks = 1 if api in ("host", "objects", "wrappers") else int(rng.integers(1, 5))
             n = int(rng.choice([64, 128, 4096, 65536, int(rng.integers(1, 3000)) * 2]))
             if a.large and rng.random() < 0.1:  # multi-tile grids: 1-3 MiB with a ragged tail
                 n = int(rng.integers(1, 4)) * (1 << 20) + int(rng.integers(0, 64)) * 2
@@ -110,6 +112,25 @@ def main():
                         ok = ok and all(dec.restored_original(i) is None
                                         for i in range(k) if orig_in[i] is not None)
                         del dec
+                elif api == "wrappers":
+                    # generate_parity (generate.rs:59-104) with a short last segment
+                    # zero-padded by the wrapper, and recover_segment_rs30_3
+                    # (recovery.rs:118-173) of every erased target
+                    data, rec, orig_in, rec_in, er = blocks[0]
+                    cut = int(rng.integers(0, n // 2 + 1)) * 2 if k > 1 else 0
+                    segs = data[:-1] + [data[-1][:n - cut]]
+                    padded = data[:-1] + [np.pad(segs[-1], (0, cut))]
+                    want = oracle.encode(padded, m, oracle.ENGINE_AVX2) if cut else rec
+                    outs = [np.empty(n, np.uint8) for _ in range(m)]
+                    bfrs.Chunker(ctx).generate_parity_into(segs, k, m, outs)
+                    ok = all(np.array_equal(o, w) for o, w in zip(outs, want))
+                    if k == 30 and m == 3 and er and not cut:
+                        want_d = oracle.decode(orig_in, rec_in, oracle.ENGINE_AVX2)
+                        par = [r if r is not None else rec[j] for j, r in enumerate(rec_in)]
+                        if all(r is not None for r in rec_in):
+                            for t in er:
+                                got = bfrs.recover_segment_rs30_3(ctx, orig_in, par, t)
+                                ok = ok and got == want_d[t].tobytes()
                 elif api == "host_batch":
                     # one shape per batch (the batch API shares k across blocks only via ks)
                     ks = [k] * nblocks
@@ -171,6 +192,8 @@ def main():
         t.join()
     ctx.close()
     stats["plan_cache"] = int(os.environ["BFRS_PLAN_CACHE"])
+    stats["codec_staging"] = os.environ.get("BFRS_CODEC_STAGING", "pinned")
+    stats["codec_slots"] = os.environ.get("BFRS_CODEC_SLOTS", "2")
     stats["threads"] = a.threads
     stats["seconds"] = a.seconds
     print(json.dumps(stats))
