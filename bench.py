@@ -86,6 +86,10 @@ def parse(argv=None):
                     help="every rank uses device 0 (tests: 2 ranks on one GPU over gloo)")
     ap.add_argument("--dump-dir", default=None,
                     help="each rank writes its C4 parity stripes here (tests assemble them)")
+    ap.add_argument("--pmc", choices=["auto", "off"], default="auto",
+                    help="N=1: measure roofline.traffic live with two rocprofv3 --pmc child "
+                         "passes before the timed run (off: the committed profiles/ record)")
+    ap.add_argument("--traffic-probe", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--stub", action="store_true",
                     help="CPU-only rehearsal of the launcher/partition/timing path: no GPU, "
                          "the codec calls replaced by a stand-in (tests only, never a bench line)")
@@ -840,9 +844,101 @@ def pcie_inclusive(ctx, sets, steps=2, rt=None, job_bytes=None):
     }
 
 
+PMC_PASS_TIMEOUT_S = 150
+
+
+def under_rocprof() -> bool:
+    """rocprofv3 exports ROCPROF_* variables to the program it profiles."""
+    return any(k.startswith("ROCPROF_") for k in os.environ)
+
+
+def traffic_probe(args):
+    """--traffic-probe: the child process of one live PMC pass.  The bench's
+    C2 batch (same shapes, pitch, layout, seed), 3 encode + 3 decode launches,
+    nothing timed; rocprofv3 counts every dispatch."""
+    from bfrs import synth
+    import bfrs
+    rt = Runtime(args)
+    sets = ShardSets(rt, synth.block_shapes(args.segments), args.segment_bytes, args.layout,
+                     args.pitch)
+    fill(rt, sets, 0xB10C)
+    ctx = bfrs.Context(rt.device.index)
+    enc, dec = codec_calls(rt, ctx, sets)
+    sh = rt.torch.cuda.current_stream().cuda_stream
+    for _ in range(3):
+        enc(sh)
+        dec(sh)
+    rt.sync()
+    return 0
+
+
+def _pmc_pass(counter, args, workdir):
+    """One `rocprofv3 --pmc <counter>` pass over the traffic probe; returns the
+    per-dispatch counter values of the full-size gf_apply launches."""
+    import csv
+    import glob
+    out = os.path.join(workdir, counter)
+    cmd = ["timeout", "-s", "KILL", str(PMC_PASS_TIMEOUT_S), "rocprofv3", "--pmc", counter,
+           "--output-format", "csv", "-d", out, "-o", "pmc", "--",
+           sys.executable, os.path.abspath(__file__), "--traffic-probe",
+           "--segments", str(args.segments), "--segment-bytes", str(args.segment_bytes),
+           "--pitch", str(args.pitch), "--layout", args.layout]
+    env = dict(os.environ, TMPDIR=workdir, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    env.pop("TORCHELASTIC_RUN_ID", None)  # the probe never joins a process group
+    with open(os.path.join(workdir, f"{counter}.log"), "w") as log:
+        rc = subprocess.call(cmd, stdout=log, stderr=subprocess.STDOUT, env=env, cwd=workdir)
+    if rc != 0:
+        raise RuntimeError(f"rocprofv3 --pmc {counter} exited {rc}")
+    rows = [r for f in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True)
+            for r in csv.DictReader(open(f))
+            if "gf_apply" in r["Kernel_Name"] and r["Counter_Name"] == counter]
+    if not rows:
+        raise RuntimeError(f"no gf_apply dispatches with {counter} in the rocprofv3 output")
+    grid = max(int(r["Grid_Size"]) for r in rows)
+    per = {}
+    for r in rows:
+        if int(r["Grid_Size"]) == grid:  # the C2 launches (encode and decode share the grid)
+            per[r["Dispatch_Id"]] = per.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
+    return list(per.values())
+
+
+def live_pmc_traffic(args):
+    """HBM bytes per gf_apply launch measured in this run: two rocprofv3 child
+    passes (--pmc FETCH_SIZE, then --pmc WRITE_SIZE: separate runs, no trace
+    domains) over the bench's own C2 batch, started before this process touches
+    the GPU.  Corrections of MI355X_MICROARCH.md's HBM section: both counters
+    are KiB, and gfx950's FETCH_SIZE counts half of a 16 B/lane streaming read
+    (x2).  Returns (bytes, source) or (None, {"error": ...})."""
+    import shutil
+    import statistics
+    import tempfile
+    if shutil.which("rocprofv3") is None or shutil.which("timeout") is None:
+        return None, {"error": "rocprofv3 not on PATH"}
+    t0 = time.perf_counter()
+    workdir = tempfile.mkdtemp(prefix="bfrs_pmc_")
+    try:
+        fetch = _pmc_pass("FETCH_SIZE", args, workdir)
+        write = _pmc_pass("WRITE_SIZE", args, workdir)
+    except (OSError, RuntimeError, ValueError, KeyError) as e:
+        return None, {"error": f"{type(e).__name__}: {e}"}
+    finally:
+        shutil.rmtree(workdir, ignore_errors=True)
+    rd = int(statistics.median(fetch) * 1024 * 2)
+    wr = int(statistics.median(write) * 1024)
+    return rd + wr, {
+        "how": "measured in this run: rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate "
+               "child passes, before this process touched the GPU) over the same C2 batch "
+               "(3 encode + 3 decode launches each), median per dispatch",
+        "correction": "KiB; gfx950 FETCH_SIZE x2 (MI355X_MICROARCH.md HBM section)",
+        "dispatches": [len(fetch), len(write)],
+        "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
+        "seconds": round(time.perf_counter() - t0, 1)}
+
+
 def pmc_traffic(alg_bytes):
     """HBM bytes per launch from the committed rocprofv3 PMC record of this
-    launch shape (FETCH_SIZE / WRITE_SIZE, separate passes), with its source."""
+    launch shape (FETCH_SIZE / WRITE_SIZE, separate passes), with its source.
+    Used only when the live passes (live_pmc_traffic) are off or failed."""
     if not os.path.exists(PMC_FILE):
         return None, None
     try:
@@ -1024,6 +1120,13 @@ def main():
         return 0 if line["blake3_match"] else 1
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return launch_ranks(args)
+    if args.traffic_probe:
+        return traffic_probe(args)
+    live_traffic = None
+    if (args.pmc == "auto" and args.gpus == 1 and not args.stub and not args.strong
+            and int(os.environ.get("WORLD_SIZE", "1")) == 1 and not under_rocprof()):
+        # before anything in this process touches the GPU: the passes are child processes
+        live_traffic = live_pmc_traffic(args)
     from bfrs import parallel, synth
 
     rt = Runtime(args)
@@ -1185,7 +1288,14 @@ def main():
     }
     if not rt.stub:
         achieved = alg_bytes / (launch_ms * 1e-3) / 1e9
-        traffic, traffic_src = pmc_traffic(alg_bytes)
+        traffic, traffic_src = live_traffic if live_traffic else (None, None)
+        if traffic is not None:
+            traffic_src["ratio_to_algorithmic"] = round(traffic / alg_bytes, 4)
+        else:
+            live_err = (traffic_src or {}).get("error")
+            traffic, traffic_src = pmc_traffic(alg_bytes)
+            live_note = live_err or ("skipped under rocprofv3" if under_rocprof() else "off")
+            traffic_src = dict(traffic_src or {}, live_pass=live_note)
         line["encode_GiBps_per_gpu"] = round(data_bytes / 2**30 / (enc_ms * 1e-3), 2)
         line["decode_GiBps_per_gpu"] = round(data_bytes / 2**30 / (dec_ms * 1e-3), 2)
         line["roofline"] = {

@@ -82,3 +82,62 @@ def test_stub_bench_line_carries_parity_check(argv, capfd):
     pc = line["parity_check"]
     assert pc["c3_decode"]["match"] and pc["all_ok"] and pc["ranks_ok"] == [True]
     assert pc["c2_encode"] is None
+
+
+def test_live_pmc_passes_parse_and_correct(monkeypatch):
+    """roofline.traffic measured in the run: bench.py runs two rocprofv3 --pmc
+    child passes; stand in for rocprofv3 with a CSV of the shape it writes and
+    check the dispatch filter (full-size gf_apply only) and the corrections
+    (KiB, gfx950 FETCH_SIZE x2)."""
+    import csv
+    import shutil
+    import subprocess as sp
+    calls = []
+
+    def fake_call(cmd, stdout=None, stderr=None, env=None, cwd=None):
+        calls.append(cmd)
+        assert cmd[:4] == ["timeout", "-s", "KILL", str(bench.PMC_PASS_TIMEOUT_S)]
+        assert "--traffic-probe" in cmd and cmd[cmd.index("--") + 1] == sys.executable
+        assert "TORCHELASTIC_RUN_ID" not in env and env["WORLD_SIZE"] == "1"
+        counter = cmd[cmd.index("--pmc") + 1]
+        out = os.path.join(cmd[cmd.index("-d") + 1], "host", "123")
+        os.makedirs(out)
+        rows = [("fill_kernel", 4096, 1, 5.0),
+                ("void bfrs::gf_apply_unrolled_kernel<true, 6, 4>(bfrs::KernArgs)", 5242880, 2, 1000.0),
+                ("void bfrs::gf_apply_unrolled_kernel<true, 6, 4>(bfrs::KernArgs)", 5242880, 3, 1002.0),
+                ("void bfrs::gf_apply_unrolled_kernel<true, 6, 4>(bfrs::KernArgs)", 5242880, 4, 998.0),
+                ("void bfrs::gf_tail_kernel(bfrs::KernArgs)", 256, 5, 1.0)]
+        with open(os.path.join(out, "pmc_counter_collection.csv"), "w", newline="") as f:
+            w = csv.writer(f)
+            w.writerow(["Dispatch_Id", "Kernel_Name", "Grid_Size", "Counter_Name", "Counter_Value"])
+            for name, grid, d, v in rows:
+                # two dimension rows per dispatch, summed by the parser
+                w.writerow([d, name, grid, counter, v / 2])
+                w.writerow([d, name, grid, counter, v / 2])
+        return 0
+
+    monkeypatch.setattr(sp, "call", fake_call)
+    monkeypatch.setattr(shutil, "which", lambda name: "/usr/bin/" + name)
+    monkeypatch.setenv("TORCHELASTIC_RUN_ID", "x")
+    args = bench.parse(["--segments", "128"])
+    traffic, src = bench.live_pmc_traffic(args)
+    assert [c[c.index("--pmc") + 1] for c in calls] == ["FETCH_SIZE", "WRITE_SIZE"]
+    assert src["dispatches"] == [3, 3]
+    assert src["hbm_read_bytes_per_launch"] == 1000 * 1024 * 2
+    assert src["hbm_write_bytes_per_launch"] == 1000 * 1024
+    assert traffic == 3000 * 1024
+
+    def failing(cmd, **kw):
+        return 137
+    monkeypatch.setattr(sp, "call", failing)
+    traffic, src = bench.live_pmc_traffic(args)
+    assert traffic is None and "exited 137" in src["error"]
+
+
+def test_live_pmc_skipped_under_rocprof(monkeypatch):
+    monkeypatch.setenv("ROCPROF_OUTPUT_PATH", "/tmp/x")
+    assert bench.under_rocprof()
+    monkeypatch.delenv("ROCPROF_OUTPUT_PATH")
+    for k in [k for k in os.environ if k.startswith("ROCPROF_")]:
+        monkeypatch.delenv(k)
+    assert not bench.under_rocprof()
