@@ -3,11 +3,71 @@
 // (tools/tsan_host.cpp, make host-tsan).
 #include "host_copy.hpp"
 
+#include <sched.h>
+
 #include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 
 namespace bfrs {
+
+namespace {
+
+long env_long(const char *name, long dflt) {
+  const char *e = std::getenv(name);
+  return e && *e ? std::strtol(e, nullptr, 10) : dflt;
+}
+
+// CPUs this process may use: the affinity mask, capped by a cgroup-v2 CPU
+// quota (the GPU boxes show 256 CPUs with a quota of 16).
+long cpu_share() {
+  cpu_set_t set;
+  long n = sched_getaffinity(0, sizeof(set), &set) == 0 ? CPU_COUNT(&set) : 8;
+  if (FILE *f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+    char quota[32] = {};
+    long period = 0;
+    if (std::fscanf(f, "%31s %ld", quota, &period) == 2 && std::strcmp(quota, "max") != 0 &&
+        period > 0)
+      n = std::min(n, std::max(1L, (std::strtol(quota, nullptr, 10) + period - 1) / period));
+    std::fclose(f);
+  }
+  return std::max(1L, n);
+}
+
+// BFRS_HOST_COPY_THREADS (1..8, default 8) caps the threads of one call.
+size_t max_parts() {
+  static const size_t v = size_t(std::clamp(env_long("BFRS_HOST_COPY_THREADS", 8), 1L, 8L));
+  return v;
+}
+
+// Helper threads of all concurrent calls together stay within the process's
+// CPU share minus one (BFRS_HOST_COPY_BUDGET overrides): rayon runs one
+// generate_parity per block on every worker (commit.rs:391-466), and 5 blocks
+// x 8 threads on a 16-CPU quota ran 5-15% slower than 5 x 4
+// (tools/rayon_probe.py).  The calling thread always copies
+// its own part, so a call never waits for the budget.
+std::atomic<long> g_helpers{0};
+long helper_budget() {
+  static const long v = std::max(0L, env_long("BFRS_HOST_COPY_BUDGET", cpu_share() - 1));
+  return v;
+}
+
+// Reserve up to `want` helpers; returns how many were granted.
+long reserve_helpers(long want) {
+  const long budget = helper_budget();
+  long cur = g_helpers.load(std::memory_order_relaxed);
+  while (want > 0) {
+    const long take = std::min(want, budget - cur);
+    if (take <= 0) return 0;
+    if (g_helpers.compare_exchange_weak(cur, cur + take, std::memory_order_relaxed)) return take;
+  }
+  return 0;
+}
+
+}  // namespace
 
 // Host copy into pinned memory: up to 8 threads of >= 4 MiB for large shards
 // (one core copies ~10-20 GB/s from pageable memory; the PCIe link takes
@@ -15,12 +75,15 @@ namespace bfrs {
 // this thread; the started ones are always joined, so nothing terminates.
 void host_copy(uint8_t *dst, const uint8_t *src, size_t n) {
   constexpr size_t kPart = 4u << 20, kMaxParts = 8;
-  const size_t parts = std::min<size_t>(kMaxParts, n / kPart);
+  const size_t want = std::min<size_t>(max_parts(), n / kPart);
+  const long helpers = want >= 2 ? reserve_helpers(long(want) - 1) : 0;
+  const size_t parts = size_t(helpers) + 1;
   if (parts < 2) {
     std::memcpy(dst, src, n);
     return;
   }
-  const size_t per = (n / parts + 63) / 64 * 64;
+  // ceil(n / parts) rounded up to 64 B, so that the parts cover all n bytes
+  const size_t per = ((n + parts - 1) / parts + 63) / 64 * 64;
   std::thread th[kMaxParts];
   bool started[kMaxParts] = {};
   for (size_t t = 1; t < parts; ++t) {
@@ -35,6 +98,7 @@ void host_copy(uint8_t *dst, const uint8_t *src, size_t n) {
   std::memcpy(dst, src, std::min(n, per));
   for (size_t t = 1; t < parts; ++t)
     if (started[t]) th[t].join();
+  g_helpers.fetch_sub(helpers, std::memory_order_relaxed);
 }
 
 }  // namespace bfrs

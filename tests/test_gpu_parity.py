@@ -431,6 +431,36 @@ def test_generate_parity_pads_like_reference(ctx, bfrs, oracle):
     assert "No chunks provided" in str(e.value)
 
 
+@pytest.mark.parametrize("staging", ["pinned", "direct"])
+def test_crate_wrappers_at_shard_sizes_with_copy_remainders(bfrs, oracle, monkeypatch, staging):
+    """Shard sizes that host_copy splits into parts with a remainder (12 MiB + 2
+    into 3 parts, 32 MiB + 2 into 8): round 3 found its part size dropped the
+    last bytes there (host_copy.cpp).  Through every wrapper that copies
+    through pinned rows: generate_parity (k = 1: replication; k = 3 against
+    the oracle), recover_segment_rs13 and recover_segment_rs30_3."""
+    monkeypatch.setenv("BFRS_CODEC_STAGING", staging)
+    c = bfrs.Context(0)
+    try:
+        rng = np.random.default_rng(12)
+        for n in ((12 << 20) + 2, (32 << 20) + 2):
+            one = rng.integers(0, 256, n, dtype=np.uint8)
+            par = bfrs.Chunker(c).generate_parity([one], 1, 3)
+            assert par == [one.tobytes()] * 3
+            assert bfrs.recover_segment_rs13(c, par) == one.tobytes()
+            three = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(3)]
+            par3 = bfrs.Chunker(c).generate_parity(three, 3, 3)
+            assert par3 == [r.tobytes() for r in oracle.encode(three, 3)]
+        n = (12 << 20) + 2
+        segs = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(30)]
+        par30 = [np.frombuffer(p, np.uint8) for p in bfrs.Chunker(c).generate_parity(segs, 30, 3)]
+        for target in (0, 17, 29):
+            slots = [None if i in (target, 5, 23) else segs[i] for i in range(30)]
+            got = bfrs.recover_segment_rs30_3(c, slots, par30, target)
+            assert got == segs[target].tobytes()
+    finally:
+        c.close()
+
+
 def test_config1_tier1_8MB_rs13(ctx, bfrs, oracle):
     """BASELINE config 1: single 8 MB file -> RS(1,3) (copies of the 64-padded
     data, generate.rs:26-57) and back through recover_segment_rs13."""

@@ -73,11 +73,15 @@ def test_host_suites_under_asan_ubsan(sanitized_builds, tmp_path):
     assert probe.stdout.split() == ["True", "True"], probe.stdout + probe.stderr
 
 
-@pytest.mark.parametrize("binary", ["blockframe-rs_amd/csrc/build/tsan_host",
-                                    "oracle/_san/tsan_oracle"])
-def test_threaded_host_code_under_tsan(sanitized_builds, binary):
+@pytest.mark.parametrize("binary,budget", [("blockframe-rs_amd/csrc/build/tsan_host", None),
+                                           ("blockframe-rs_amd/csrc/build/tsan_host", "3"),
+                                           ("oracle/_san/tsan_oracle", None)])
+def test_threaded_host_code_under_tsan(sanitized_builds, binary, budget):
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1")
+    if budget is not None:  # host_copy's process-wide helper budget (host_copy.cpp)
+        env["BFRS_HOST_COPY_BUDGET"] = budget
     r = subprocess.run([os.path.join(ROOT, binary)], capture_output=True, text=True, timeout=600,
-                       env=dict(os.environ, TSAN_OPTIONS="halt_on_error=1"))
+                       env=env)
     out = r.stdout + r.stderr[-4000:]
     assert "ThreadSanitizer" not in out, out
     assert r.returncode == 0 and " ok" in r.stdout, out

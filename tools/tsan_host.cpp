@@ -5,8 +5,11 @@
 // 1. bfrs::blake3_hash with 1..16 threads on sizes around the tree's
 //    boundaries (1 KiB chunks, power-of-two subtrees): the subtree threads
 //    must give the single-thread digest;
-// 2. bfrs::host_copy (up to 8 copy threads) called from 4 threads at once, as
-//    codec objects on several rayon workers do (codec_objects.cpp);
+// 2. bfrs::host_copy (up to 8 copy threads, within the process-wide helper
+//    budget) called from 4 threads at once, as codec objects on several rayon
+//    workers do (codec_objects.cpp); sizes whose parts end in a remainder,
+//    canaries past the end (tests/test_sanitize.py also runs it with
+//    BFRS_HOST_COPY_BUDGET=3, so the part counts vary between callers);
 // 3. both at once.
 // Exit 0 = every result equal; TSan reports go to stderr (exit 66).
 #include <cstdio>
@@ -49,7 +52,11 @@ bool hash_checks() {
 }
 
 bool copy_checks() {
-  const size_t sizes[] = {100, (4u << 20) - 1, 8u << 20, (17u << 20) + 17};
+  // (12 MiB + 2) and (32 MiB + 2) split into 3 and 8 parts of a 64-B multiple
+  // plus a remainder: the round-2/3 part size dropped those last bytes
+  const size_t sizes[] = {100, (4u << 20) - 1, 8u << 20, (12u << 20) + 2, (17u << 20) + 17,
+                          (24u << 20) + 6, (32u << 20) + 2};
+  constexpr size_t kCanary = 64;
   bool ok = true;
   std::vector<std::thread> th;
   std::vector<int> good(4, 0);
@@ -58,9 +65,10 @@ bool copy_checks() {
       int g = 1;
       for (size_t n : sizes) {
         const std::vector<uint8_t> src = bytes(n, 77 + w);
-        std::vector<uint8_t> dst(n, 0);
+        std::vector<uint8_t> dst(n + kCanary, 0xA5);
         bfrs::host_copy(dst.data(), src.data(), n);
-        g &= dst == src;
+        g &= std::memcmp(dst.data(), src.data(), n) == 0;
+        for (size_t i = n; i < n + kCanary; ++i) g &= dst[i] == 0xA5;  // nothing past n
       }
       good[w] = g;
     });
