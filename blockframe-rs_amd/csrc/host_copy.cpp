@@ -43,21 +43,24 @@ size_t max_parts() {
   return v;
 }
 
-// Helper threads of all concurrent calls together stay within the process's
-// CPU share minus one (BFRS_HOST_COPY_BUDGET overrides): rayon runs one
-// generate_parity per block on every worker (commit.rs:391-466), and 5 blocks
-// x 8 threads on a 16-CPU quota ran 5-15% slower than 5 x 4
-// (tools/rayon_probe.py).  The calling thread always copies
+// Threads of all concurrent calls together stay within the process's CPU
+// share (BFRS_HOST_COPY_BUDGET overrides the helper count, share - 1), split
+// evenly between the calls in flight: rayon runs one generate_parity per
+// block on every worker (commit.rs:391-466), and 5 blocks x 8 threads on a
+// 16-CPU quota ran 5-15% slower than 5 x 4 (tools/rayon_probe.py, DESIGN.md
+// §7c), while a block alone wants all 8.  The calling thread always copies
 // its own part, so a call never waits for the budget.
-std::atomic<long> g_helpers{0};
+std::atomic<long> g_helpers{0}, g_calls{0};
 long helper_budget() {
   static const long v = std::max(0L, env_long("BFRS_HOST_COPY_BUDGET", cpu_share() - 1));
   return v;
 }
 
-// Reserve up to `want` helpers; returns how many were granted.
-long reserve_helpers(long want) {
+// Reserve up to `want` helpers for a call while `calls` calls are in flight;
+// returns how many were granted.
+long reserve_helpers(long want, long calls) {
   const long budget = helper_budget();
+  want = std::min(want, std::max(0L, (budget + 1) / std::max(1L, calls) - 1));
   long cur = g_helpers.load(std::memory_order_relaxed);
   while (want > 0) {
     const long take = std::min(want, budget - cur);
@@ -76,7 +79,15 @@ long reserve_helpers(long want) {
 void host_copy(uint8_t *dst, const uint8_t *src, size_t n) {
   constexpr size_t kPart = 4u << 20, kMaxParts = 8;
   const size_t want = std::min<size_t>(max_parts(), n / kPart);
-  const long helpers = want >= 2 ? reserve_helpers(long(want) - 1) : 0;
+  if (want < 2) {
+    std::memcpy(dst, src, n);
+    return;
+  }
+  struct InFlight {  // this call counts toward the even split until it returns
+    long calls = g_calls.fetch_add(1, std::memory_order_relaxed) + 1;
+    ~InFlight() { g_calls.fetch_sub(1, std::memory_order_relaxed); }
+  } in_flight;
+  const long helpers = reserve_helpers(long(want) - 1, in_flight.calls);
   const size_t parts = size_t(helpers) + 1;
   if (parts < 2) {
     std::memcpy(dst, src, n);
