@@ -34,12 +34,18 @@
  * its context (it shares the context's slot pool); every other call on it
  * needs the context open.  Free archive handles before bfrs_close.
  *
- * Environment, read by bfrs_open:
+ * Environment, read by bfrs_open (BFRS_HOST_COPY_* on first use, once per
+ * process):
  *   BFRS_CODEC_SLOTS    idle codec slots kept (default 2; 0 = none)
  *   BFRS_CODEC_STAGING  "pinned" (default: add_*_shard copies into a pinned
  *                       row on several threads and queues its H2D) or
  *                       "direct" (one DMA straight from the caller's buffer);
  *                       either way the buffer is free on return
+ *   BFRS_HOST_COPY_THREADS  copy threads per staging call (1..8, default 8);
+ *                       the copy threads of all concurrent calls share the
+ *                       process's CPU share (cgroup quota), split evenly
+ *                       between the calls in flight
+ *   BFRS_HOST_COPY_BUDGET   helper threads in total (default CPU share - 1)
  *   BFRS_KERNEL_VARIANT unset or 76 (default kernel); 75 / 73 force the looped
  *                       subfield / general kernels; anything else fails
  *                       bfrs_open with BFRS_E_INVALID_ARGUMENT (the A/B
@@ -213,7 +219,8 @@ int bfrs_recover_segment_rs13(bfrs_ctx *ctx, const uint8_t *const *parity,
                               const size_t *parity_lens, size_t n_parity, size_t expected_size,
                               uint8_t *out, size_t *out_len);
 /* recover_segment_rs30_3 (recovery.rs:118-173): segments[30] with NULL for
- * None, block_parity[3], target index.  out must hold the shard size. */
+ * None, block_parity[3], target index.  out must hold the shard size (its
+ * contents are unspecified after an error). */
 int bfrs_recover_segment_rs30_3(bfrs_ctx *ctx, const uint8_t *const *segments,
                                 const size_t *seg_lens, size_t n_slots,
                                 const uint8_t *const *block_parity, const size_t *parity_lens,
