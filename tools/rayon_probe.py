@@ -61,13 +61,25 @@ def run_blocks(ctx, blocks):
 
 def main():
     import torch
+    if os.environ.get("PROBE_PINNED_GIB"):  # torch pinned memory allocated and freed first (bench's pcie_inclusive)
+        t = torch.empty(int(float(os.environ["PROBE_PINNED_GIB"]) * 2**30), dtype=torch.uint8,
+                        pin_memory=True)
+        t.fill_(1)
+        del t
     rng = np.random.default_rng(3)
     base = rng.integers(0, 256, S, dtype=np.uint8)
     blocks = [[np.roll(base, 64 * (b * 31 + i)) for i in range(k)] for b, k in enumerate(SHAPES)]
+    if os.environ.get("PROBE_TORCH_SEGS"):  # segments as bench.py makes them: .cpu() of device rows
+        dev = torch.from_numpy(np.stack([x for blk in blocks for x in blk])).cuda()
+        it = iter(range(sum(SHAPES)))
+        blocks = [[dev[next(it)].cpu().numpy() for _ in range(k)] for k in SHAPES]
+        del dev
     gib = sum(SHAPES) * S / 2**30
     res = {"what": f"blocks {SHAPES} x {S >> 20} MiB on {len(SHAPES)} threads, one context; "
                    f"ms (best, median of {REPS})", "host_copy_threads": os.environ.get(
-                       "BFRS_HOST_COPY_THREADS", "default")}
+                       "BFRS_HOST_COPY_THREADS", "default"),
+           "torch_segs": bool(os.environ.get("PROBE_TORCH_SEGS")),
+           "pinned_gib_first": os.environ.get("PROBE_PINNED_GIB")}
     n_in, n_out = sum(SHAPES) * S, 3 * len(SHAPES) * S
     dev = torch.empty(n_in, dtype=torch.uint8, device="cuda")
     pin = torch.empty(n_in, dtype=torch.uint8, pin_memory=True)
