@@ -667,7 +667,44 @@ def crate_api(ctx, sets, reps=7, staging_ab=True):
         tr_reuse = timed(lambda: bfrs.recover_segment_rs30_3_into(c, slots, par, target, got))
         return tg, tr, par, slots, target, tg_reuse, tr_reuse, tg_new_in
 
+    def all_blocks_figure():
+        # rayon's shape (commit.rs:391-466): one generate_parity per block, all of
+        # C2's blocks at once from worker threads sharing the one context (ctypes
+        # drops the GIL for the call)
+        import threading
+        blocks, off = [], 0
+        for kb in sets.shapes:
+            blocks.append([sets.data[off + i].cpu().numpy() for i in range(kb)])
+            off += kb
+        errors = []
+
+        def worker(b):
+            try:
+                bfrs.Chunker(ctx).generate_parity_into(
+                    blocks[b], len(blocks[b]), 3, [np.empty(S, np.uint8) for _ in range(3)])
+            except Exception as e:  # noqa: BLE001 - reported below
+                errors.append(repr(e))
+
+        def all_blocks():
+            ts = [threading.Thread(target=worker, args=(b,)) for b in range(len(blocks))]
+            t0 = time.perf_counter()
+            for t in ts:
+                t.start()
+            for t in ts:
+                t.join()
+            return time.perf_counter() - t0
+
+        # untimed rounds first: the pool grows to one slot per block (a new slot
+        # pins (k+3) x 32 MiB of host memory, ~0.1 s) and the link settles
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < 0.5:
+            all_blocks()
+        t_par = [all_blocks() for _ in range(5)]
+        assert not errors, errors
+        return t_par
+
     cold = settle_link(ctx)
+    t_par = all_blocks_figure()
     tg, tr, par, slots, target, tg_reuse, tr_reuse, tg_new_in = wrappers(ctx)
     tg_py = timed(lambda: ch.generate_parity(segs, k, 3))
     tr_py = timed(lambda: bfrs.recover_segment_rs30_3(ctx, slots, par, target))
@@ -719,39 +756,6 @@ def crate_api(ctx, sets, reps=7, staging_ab=True):
         return {key: round(v * 1e3, 2) for key, v in best.items()}
 
     bd = breakdown()
-    # rayon's shape (commit.rs:391-466): one generate_parity per block, all of
-    # C2's blocks at once from worker threads sharing the one context (ctypes
-    # drops the GIL for the call)
-    import threading
-    blocks, off = [], 0
-    for kb in sets.shapes:
-        blocks.append([sets.data[off + i].cpu().numpy() for i in range(kb)])
-        off += kb
-    errors = []
-
-    def worker(b):
-        try:
-            bfrs.Chunker(ctx).generate_parity_into(
-                blocks[b], len(blocks[b]), 3, [np.empty(S, np.uint8) for _ in range(3)])
-        except Exception as e:  # noqa: BLE001 - reported below
-            errors.append(repr(e))
-
-    def all_blocks():
-        ts = [threading.Thread(target=worker, args=(b,)) for b in range(len(blocks))]
-        t0 = time.perf_counter()
-        for t in ts:
-            t.start()
-        for t in ts:
-            t.join()
-        return time.perf_counter() - t0
-
-    # untimed rounds first: the pool grows to one slot per block (a new slot
-    # pins (k+3) x 32 MiB of host memory, ~0.1 s) and the link settles
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < 0.5:
-        all_blocks()
-    t_par = [all_blocks() for _ in range(5)]
-    assert not errors, errors
     par_gib = sum(sets.shapes) * S / 2**30
     res = {
         "staging": os.environ.get("BFRS_CODEC_STAGING", "pinned"),
@@ -771,7 +775,7 @@ def crate_api(ctx, sets, reps=7, staging_ab=True):
         "generate_parity_all_blocks_threads": {
             "ms": round(min(t_par) * 1e3, 2), "GiBps": round(par_gib / min(t_par), 2),
             "median_ms": round(sorted(t_par)[len(t_par) // 2] * 1e3, 2),
-            "what": f"{len(blocks)} blocks ({'+'.join(map(str, sets.shapes))} x {S >> 20} MiB) "
+            "what": f"{len(sets.shapes)} blocks ({'+'.join(map(str, sets.shapes))} x {S >> 20} MiB) "
                     "on as many threads, one shared context (rayon over blocks), fresh outputs, "
                     "best of 5 after 0.5 s of untimed rounds",
             "codec_slots": int(os.environ.get("BFRS_CODEC_SLOTS", "2"))},
@@ -807,6 +811,36 @@ def crate_api(ctx, sets, reps=7, staging_ab=True):
                               "recover_segment_rs30_3_ms": round(pr * 1e3, 2),
                               "what": f"BFRS_CODEC_STAGING={alt} on a second context, same block"}
     return res
+
+
+def rayon_fresh_process():
+    """BlockFrame's commit_blocked shape (one generate_parity per block on
+    every rayon worker, commit.rs:391-466) in a process of its own, as a
+    BlockFrame commit runs: tools/rayon_probe.py (C2's 5 blocks on 5 threads,
+    one context, fresh outputs, new inputs every round) as a child started
+    before this process touches the GPU.  Inside the bench process, after the
+    device benchmark, the same calls run 20-40% slower (`crate_api.
+    generate_parity_all_blocks_threads`; cause not isolated)."""
+    cmd = ["timeout", "-s", "KILL", "150", sys.executable,
+           os.path.join(ROOT, "tools", "rayon_probe.py")]
+    env = dict(os.environ, PROBE_MODES="pinned", PROBE_REPS="3")
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, env=env, cwd=ROOT)
+    except OSError as e:
+        return {"error": f"{type(e).__name__}: {e}"}
+    if r.returncode != 0:
+        return {"error": f"tools/rayon_probe.py exited {r.returncode}: {r.stderr[-300:]}"}
+    try:
+        res = json.loads(r.stdout.strip().splitlines()[-1])
+    except (ValueError, IndexError):
+        return {"error": "no JSON line from tools/rayon_probe.py"}
+    return {"ms": res["fresh_pinned"][0], "median_ms": res["fresh_pinned"][1],
+            "GiBps": res["fresh_pinned_GiBps"], "inputs_seen_before_ms": res["seen_pinned"][0],
+            "link_floor_ms": res["link_floor_ms"],
+            "what": "5 blocks (30+30+30+30+8 x 32 MiB) on 5 threads in a fresh process "
+                    "(tools/rayon_probe.py): new input buffers and fresh outputs every round, "
+                    "best of 3 (median beside it); link floor = torch H2D of all inputs + D2H "
+                    "of all parity from pinned memory"}
 
 
 def pcie_inclusive(ctx, sets, steps=2, rt=None, job_bytes=None):
@@ -1140,6 +1174,10 @@ def main():
             and int(os.environ.get("WORLD_SIZE", "1")) == 1 and not under_rocprof()):
         # before anything in this process touches the GPU: the passes are child processes
         live_traffic = live_pmc_traffic(args)
+    rayon_child = None
+    if (args.crate == "auto" and args.gpus == 1 and not args.stub and not args.strong
+            and int(os.environ.get("WORLD_SIZE", "1")) == 1 and not under_rocprof()):
+        rayon_child = rayon_fresh_process()  # a child process too, before the GPU is touched
     from bfrs import parallel, synth
 
     rt = Runtime(args)
@@ -1262,6 +1300,8 @@ def main():
         pcie = guarded(pcie_inclusive, ctx, sets)
     if n1 and args.crate == "auto" and not args.strong:
         crate = guarded(crate_api, ctx, sets)
+        if rayon_child is not None and "error" not in crate:
+            crate["generate_parity_all_blocks_fresh_process"] = rayon_child
     if n1 and args.cpu_baseline == "auto" and not args.strong:
         cpu = guarded(cpu_baseline, args, sets, info)
     del sets

@@ -74,12 +74,23 @@ def main():
         it = iter(range(sum(SHAPES)))
         blocks = [[dev[next(it)].cpu().numpy() for _ in range(k)] for k in SHAPES]
         del dev
+    if os.environ.get("PROBE_GPU_WORK"):  # seconds of HBM-bound device copies first, as bench.py's kernel run
+        a = torch.empty(2 << 30, dtype=torch.uint8, device="cuda")
+        b = torch.empty_like(a)
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < float(os.environ["PROBE_GPU_WORK"]):
+            for _ in range(20):
+                b.copy_(a)
+            torch.cuda.synchronize()
+        if os.environ.get("PROBE_KEEP_HBM") is None:
+            del a, b
     gib = sum(SHAPES) * S / 2**30
     res = {"what": f"blocks {SHAPES} x {S >> 20} MiB on {len(SHAPES)} threads, one context; "
                    f"ms (best, median of {REPS})", "host_copy_threads": os.environ.get(
                        "BFRS_HOST_COPY_THREADS", "default"),
            "torch_segs": bool(os.environ.get("PROBE_TORCH_SEGS")),
-           "pinned_gib_first": os.environ.get("PROBE_PINNED_GIB")}
+           "pinned_gib_first": os.environ.get("PROBE_PINNED_GIB"),
+           "gpu_work_s_first": os.environ.get("PROBE_GPU_WORK")}
     n_in, n_out = sum(SHAPES) * S, 3 * len(SHAPES) * S
     dev = torch.empty(n_in, dtype=torch.uint8, device="cuda")
     pin = torch.empty(n_in, dtype=torch.uint8, pin_memory=True)
