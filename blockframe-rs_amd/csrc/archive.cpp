@@ -147,7 +147,6 @@ int Commit::rs13_segments(size_t nseg, bool cv_hash, std::vector<uint8_t> *seg_c
     });
   };
   std::atomic<bool> write_ok{true};
-  std::thread writer[2];
   auto write_round = [&](size_t r) {
     const size_t first = rounds[r].first, cnt = rounds[r].second;
     const Arena &pb = pbuf[r % 2];
@@ -157,7 +156,8 @@ int Commit::rs13_segments(size_t nseg, bool cv_hash, std::vector<uint8_t> *seg_c
     });
   };
   Context &c = ctx->impl;
-  auto gpu_round = [&](size_t r) -> int {
+  // `wait_writer` is the writer of round r - 2, which still owns pbuf[r % 2]
+  auto gpu_round = [&](size_t r, BgTask &wait_writer) -> int {
     const size_t first = rounds[r].first, cnt = rounds[r].second;
     const size_t shard = padded(first);
     Arena &a = arena[r % 2];
@@ -205,7 +205,7 @@ int Commit::rs13_segments(size_t nseg, bool cv_hash, std::vector<uint8_t> *seg_c
       if ((rc = gpu_hash_hex(ctx, sm, sl, &unused, offs.data(), &cvs))) return rc;
       std::memcpy(seg_cvs->data() + first * 32, cvs.data(), cnt * 32);
     }
-    if (writer[r % 2].joinable()) writer[r % 2].join();  // round r-2 still writing pbuf
+    wait_writer.join();
     Arena &pb = pbuf[r % 2];
     for (size_t j = 0; j < cnt; ++j)
       for (size_t p = 0; p < kParity; ++p)
@@ -218,15 +218,15 @@ int Commit::rs13_segments(size_t nseg, bool cv_hash, std::vector<uint8_t> *seg_c
   };
   int rc = BFRS_OK;
   fill(0);
+  BgTask writer[2];  // after the lambdas: joined first on every exit path
   for (size_t r = 0; r < rounds.size() && rc == BFRS_OK; ++r) {
-    std::thread filler;
-    if (r + 1 < rounds.size()) filler = std::thread(fill, r + 1);
-    rc = gpu_round(r);
-    if (filler.joinable()) filler.join();
-    if (rc == BFRS_OK) writer[r % 2] = std::thread(write_round, r);
+    BgTask filler;
+    if (r + 1 < rounds.size()) filler.start([&fill, r] { fill(r + 1); });
+    rc = gpu_round(r, writer[r % 2]);
+    filler.join();
+    if (rc == BFRS_OK) writer[r % 2].start([&write_round, r] { write_round(r); });
   }
-  for (auto &w : writer)
-    if (w.joinable()) w.join();
+  for (auto &w : writer) w.join();
   if (rc) return rc;
   return write_ok ? BFRS_OK : io_error("write RS(1,3) shards");
 }
@@ -366,7 +366,6 @@ int Commit::tier3(std::string *out_dir) {
     if (rc) return rc;
   }
   std::atomic<bool> write_ok{true};
-  std::thread writer[2];
   auto write_block = [&](size_t b) {  // segments from the mmap, parity from pbuf
     size_t s0, k, shard;
     geom(b, &s0, &k, &shard);
@@ -381,7 +380,8 @@ int Commit::tier3(std::string *out_dir) {
     });
   };
   // one block on the GPU: H2D, encode, hashes, D2H parity into pbuf[b % 2]
-  auto gpu_block = [&](size_t b) -> int {
+  // `wait_writer` is the writer of block b - 2, which still owns pbuf[b % 2]
+  auto gpu_block = [&](size_t b, BgTask &wait_writer) -> int {
     size_t s0, k, shard;
     geom(b, &s0, &k, &shard);
     Arena &a = arena[b % 2];
@@ -418,7 +418,7 @@ int Commit::tier3(std::string *out_dir) {
       if ((rc = gpu_hash_hex(ctx, sm, sl, &unused, offs.data(), &cvs))) return rc;
       std::memcpy(seg_cvs.data() + s0 * 32, cvs.data(), k * 32);
     }
-    if (writer[b % 2].joinable()) writer[b % 2].join();  // block b-2 still writing pbuf
+    wait_writer.join();
     Arena &pb = pbuf[b % 2];
     for (size_t p = 0; p < kParity; ++p)
       if (hipMemcpyAsync(pb.hs(p), a.ds(k + p), shard, hipMemcpyDeviceToHost, c.stream) !=
@@ -437,16 +437,16 @@ int Commit::tier3(std::string *out_dir) {
   };
   int rc = BFRS_OK;
   fill(0);
+  BgTask writer[2];  // after the lambdas: joined first on every exit path
   for (size_t b = 0; b < nblocks && rc == BFRS_OK; ++b) {
     // arena[(b+1) % 2] was last used by block b-1's GPU work, which is done
-    std::thread filler;
-    if (b + 1 < nblocks) filler = std::thread(fill, b + 1);
-    rc = gpu_block(b);
-    if (filler.joinable()) filler.join();
-    if (rc == BFRS_OK) writer[b % 2] = std::thread(write_block, b);
+    BgTask filler;
+    if (b + 1 < nblocks) filler.start([&fill, b] { fill(b + 1); });
+    rc = gpu_block(b, writer[b % 2]);
+    filler.join();
+    if (rc == BFRS_OK) writer[b % 2].start([&write_block, b] { write_block(b); });
   }
-  for (auto &w : writer)
-    if (w.joinable()) w.join();
+  for (auto &w : writer) w.join();
   if (rc) return rc;
   if (!write_ok) return io_error("write tier-3 shards");
   mf.root = merkle_root_hex(block_roots);
@@ -1222,9 +1222,14 @@ int bfrs_archive_open(bfrs_ctx *ctx, const char *archive_dir, size_t cache_segme
   if (rc) return rc;
   a->pool = std::make_shared<PinnedPool>(a->g.S);
   a->prefetch = a->g.nseg > 1;
-  if (a->prefetch)
-    for (size_t w = 0; w < bfrs_archive::kPrefetchWorkers; ++w)
-      a->workers.emplace_back(&bfrs_archive::prefetch_loop, a.get());
+  if (a->prefetch) {
+    try {
+      for (size_t w = 0; w < bfrs_archive::kPrefetchWorkers; ++w)
+        a->workers.emplace_back(&bfrs_archive::prefetch_loop, a.get());
+    } catch (const std::system_error &) {  // no thread: fewer prefetch workers, or none
+    }
+    a->prefetch = !a->workers.empty();
+  }
   *out = a.release();
   return BFRS_OK;
   BFRS_API_END

@@ -13,6 +13,8 @@
 #include <sstream>
 #include <thread>
 
+#include <mutex>
+
 #include "runtime.hpp"
 
 namespace bfrs {
@@ -29,14 +31,27 @@ int hw_threads() {
 void parallel_for(size_t n, int threads, const std::function<void(size_t)> &f) {
   if (n == 0) return;
   std::atomic<size_t> next{0};
+  std::mutex err_mu;
+  std::exception_ptr err;
   auto worker = [&] {
-    for (size_t i; (i = next.fetch_add(1)) < n;) f(i);
+    try {
+      for (size_t i; (i = next.fetch_add(1)) < n;) f(i);
+    } catch (...) {
+      next = n;  // the other workers stop after their current item
+      std::lock_guard<std::mutex> g(err_mu);
+      if (!err) err = std::current_exception();
+    }
   };
   std::vector<std::thread> ts;
   const int t = int(std::min<size_t>(n, size_t(std::max(1, threads))));
-  for (int k = 1; k < t; ++k) ts.emplace_back(worker);
+  try {
+    ts.reserve(size_t(t));
+    for (int k = 1; k < t; ++k) ts.emplace_back(worker);
+  } catch (...) {  // no more threads (quota, memory): the started ones and this one do it all
+  }
   worker();
   for (auto &th : ts) th.join();
+  if (err) std::rethrow_exception(err);
 }
 
 bool mkdirs(const std::string &path) {

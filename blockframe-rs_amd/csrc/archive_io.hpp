@@ -10,8 +10,11 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <exception>
 #include <functional>
 #include <string>
+#include <system_error>
+#include <thread>
 #include <vector>
 
 #include "manifest.hpp"
@@ -27,8 +30,53 @@ constexpr uint64_t kMaxSegmentBytes = uint64_t(1) << 36;
 
 int io_error(const std::string &what);  // BFRS_E_WRAPPER + strerror(errno)
 int hw_threads();                        // host worker threads (<= 16)
-// f(i) for i in [0, n) on up to `threads` threads.
+// f(i) for i in [0, n) on up to `threads` threads (fewer if a thread cannot
+// be started).  Every thread is joined before it returns; the first exception
+// thrown by f is rethrown then.
 void parallel_for(size_t n, int threads, const std::function<void(size_t)> &f);
+
+// A task on a thread of its own (the commit pipelines' block filler and shard
+// writers), joined on every exit path, an exception included: declare it
+// after everything the task refers to.  When no thread can be started the
+// task runs inside start().  An exception thrown by the task is kept and
+// rethrown by join().
+class BgTask {
+ public:
+  BgTask() = default;
+  BgTask(const BgTask &) = delete;
+  BgTask &operator=(const BgTask &) = delete;
+  ~BgTask() {
+    if (t_.joinable()) t_.join();
+  }
+  template <class F>
+  void start(F f) {
+    join();
+    auto body = [this, f] {
+      try {
+        f();
+      } catch (...) {
+        err_ = std::current_exception();
+      }
+    };
+    try {
+      t_ = std::thread(body);
+    } catch (const std::system_error &) {
+      body();
+    }
+  }
+  void join() {
+    if (t_.joinable()) t_.join();
+    if (err_) {
+      std::exception_ptr e = err_;
+      err_ = nullptr;
+      std::rethrow_exception(e);
+    }
+  }
+
+ private:
+  std::thread t_;
+  std::exception_ptr err_;
+};
 
 bool mkdirs(const std::string &path);
 bool rmtree(const std::string &path);

@@ -149,10 +149,20 @@ Pending subtree(const uint8_t *data, size_t len, size_t first, size_t n, int thr
   }
   const size_t l = left_len(n);
   Words8 lcv, rcv;
+  std::thread t;
   if (threads > 1 && n >= 64) {
-    std::thread t([&] { lcv = subtree(data, len, first, l, threads / 2).chaining(); });
+    try {
+      t = std::thread([&] { lcv = subtree(data, len, first, l, threads / 2).chaining(); });
+    } catch (...) {  // no thread (quota): this subtree runs on the calling thread
+    }
+  }
+  if (t.joinable()) {
+    // the left half's thread is joined on every path, an exception included
+    struct Join {
+      std::thread &t;
+      ~Join() { t.join(); }
+    } join{t};
     rcv = subtree(data, len, first + l, n - l, threads - threads / 2).chaining();
-    t.join();
   } else {
     lcv = subtree(data, len, first, l, 1).chaining();
     rcv = subtree(data, len, first + l, n - l, 1).chaining();
