@@ -28,6 +28,9 @@ def main():
     ap.add_argument("--threads", type=int, default=4)
     ap.add_argument("--seed", type=int, default=0x50A4)
     ap.add_argument("--large", action="store_true", help="10% of cases with 1-3 MiB shards")
+    ap.add_argument("--huge", type=float, default=0.0,
+                    help="this fraction of cases with 8-40 MiB shards (k <= 6, ragged sizes): "
+                         "the threaded staging copies and their shared budget (host_copy.cpp)")
     a = ap.parse_args()
     os.environ.setdefault("BFRS_PLAN_CACHE", "16")
     import numpy as np
@@ -51,12 +54,16 @@ def main():
         while time.perf_counter() < stop:
             api = str(rng.choice(["host", "host_batch", "dev_batch", "objects", "wrappers"]))
             k, m = one_block(rng)
-            if api == "wrappers" and rng.random() < 0.5:  # recover_segment_rs30_3's shape
+            huge = a.huge > 0 and rng.random() < a.huge
+            if api == "wrappers" and rng.random() < 0.5 and not huge:  # recover_segment_rs30_3's shape
                 k, m = 30, 3
             nblocks = 1 if api in ("host", "objects", "wrappers") else int(rng.integers(1, 5))
             n = int(rng.choice([64, 128, 4096, 65536, int(rng.integers(1, 3000)) * 2]))
             if a.large and rng.random() < 0.1:  # multi-tile grids: 1-3 MiB with a ragged tail
                 n = int(rng.integers(1, 4)) * (1 << 20) + int(rng.integers(0, 64)) * 2
+            if huge:  # 8-40 MiB, any even size: staging copies split into parts with remainders
+                k, m, nblocks = min(k, 6), min(m, 3), 1
+                n = int(rng.integers(4 << 20, 20 << 20)) * 2
             blocks = []
             for _ in range(nblocks):
                 data = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(k)]
@@ -195,6 +202,7 @@ def main():
     stats["codec_staging"] = os.environ.get("BFRS_CODEC_STAGING", "pinned")
     stats["codec_slots"] = os.environ.get("BFRS_CODEC_SLOTS", "2")
     stats["threads"] = a.threads
+    stats["huge_fraction"] = a.huge
     stats["seconds"] = a.seconds
     print(json.dumps(stats))
     return 1 if stats["failures"] else 0
