@@ -27,7 +27,7 @@ def main():
     ap.add_argument("--seconds", type=float, default=60.0)
     ap.add_argument("--threads", type=int, default=4)
     ap.add_argument("--seed", type=int, default=0x50A4)
-    ap.add_argument("--large", action="store_true", help="10% of cases with 1-3 MiB shards")
+    ap.add_argument("--large", action="store_true", help="10%% of cases with 1-3 MiB shards")
     ap.add_argument("--huge", type=float, default=0.0,
                     help="this fraction of cases with 8-40 MiB shards (k <= 6, ragged sizes): "
                          "the threaded staging copies and their shared budget (host_copy.cpp)")
