@@ -59,7 +59,19 @@ def run_blocks(ctx, blocks):
     return el
 
 
+def cpulist(text):
+    cpus = set()
+    for part in text.strip().split(","):
+        if part:
+            a, _, b = part.partition("-")
+            cpus.update(range(int(a), int(b or a) + 1))
+    return cpus
+
+
 def main():
+    node = os.environ.get("PROBE_NODE")
+    if node is not None:  # this process (and every thread it starts) on one NUMA node's CPUs
+        os.sched_setaffinity(0, cpulist(open(f"/sys/devices/system/node/node{node}/cpulist").read()))
     import torch
     if os.environ.get("PROBE_PINNED_GIB"):  # torch pinned memory allocated and freed first (bench's pcie_inclusive)
         t = torch.empty(int(float(os.environ["PROBE_PINNED_GIB"]) * 2**30), dtype=torch.uint8,
@@ -90,7 +102,8 @@ def main():
                        "BFRS_HOST_COPY_THREADS", "default"),
            "torch_segs": bool(os.environ.get("PROBE_TORCH_SEGS")),
            "pinned_gib_first": os.environ.get("PROBE_PINNED_GIB"),
-           "gpu_work_s_first": os.environ.get("PROBE_GPU_WORK")}
+           "gpu_work_s_first": os.environ.get("PROBE_GPU_WORK"),
+           "numa_node_cpus": node}
     n_in, n_out = sum(SHAPES) * S, 3 * len(SHAPES) * S
     dev = torch.empty(n_in, dtype=torch.uint8, device="cuda")
     pin = torch.empty(n_in, dtype=torch.uint8, pin_memory=True)
