@@ -821,7 +821,7 @@ def rayon_fresh_process():
     before this process touches the GPU.  Inside the bench process, after the
     device benchmark, the same calls run 20-40% slower (`crate_api.
     generate_parity_all_blocks_threads`; cause not isolated)."""
-    cmd = ["timeout", "-s", "KILL", "150", sys.executable,
+    cmd = ["timeout", "-s", "KILL", "90", sys.executable,
            os.path.join(ROOT, "tools", "rayon_probe.py")]
     env = dict(os.environ, PROBE_MODES="pinned", PROBE_REPS="3")
     try:
@@ -891,7 +891,7 @@ def pcie_inclusive(ctx, sets, steps=2, rt=None, job_bytes=None):
     }
 
 
-PMC_PASS_TIMEOUT_S = 150
+PMC_PASS_TIMEOUT_S = 60
 
 
 def under_rocprof() -> bool:
