@@ -141,3 +141,32 @@ def test_live_pmc_skipped_under_rocprof(monkeypatch):
     for k in [k for k in os.environ if k.startswith("ROCPROF_")]:
         monkeypatch.delenv(k)
     assert not bench.under_rocprof()
+
+
+def test_rayon_fresh_process_child(monkeypatch):
+    """crate_api.generate_parity_all_blocks_fresh_process: the child's JSON line
+    is mapped to the bench's fields, and a failing child becomes an error
+    entry, never an exception."""
+    import json
+    import subprocess as sp
+
+    class R:
+        def __init__(self, rc, out, err=""):
+            self.returncode, self.stdout, self.stderr = rc, out, err
+    line = {"link_floor_ms": 84.5, "seen_pinned": [90.0, 91.0], "fresh_pinned": [92.0, 95.0],
+            "fresh_pinned_GiBps": 43.5, "seen_pinned_GiBps": 44.4}
+    seen = {}
+
+    def ok_run(cmd, capture_output, text, env, cwd):
+        seen["cmd"], seen["env"] = cmd, env
+        return R(0, "progress\n" + json.dumps(line) + "\n")
+    monkeypatch.setattr(sp, "run", ok_run)
+    r = bench.rayon_fresh_process()
+    assert seen["cmd"][:4] == ["timeout", "-s", "KILL", "90"]
+    assert seen["cmd"][-1].endswith(os.path.join("tools", "rayon_probe.py"))
+    assert seen["env"]["PROBE_MODES"] == "pinned"
+    assert (r["ms"], r["median_ms"], r["inputs_seen_before_ms"], r["link_floor_ms"]) == (92.0, 95.0, 90.0, 84.5)
+    monkeypatch.setattr(sp, "run", lambda *a, **k: R(137, "", "killed"))
+    assert "exited 137" in bench.rayon_fresh_process()["error"]
+    monkeypatch.setattr(sp, "run", lambda *a, **k: R(0, "not json"))
+    assert "error" in bench.rayon_fresh_process()
