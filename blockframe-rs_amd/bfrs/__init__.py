@@ -240,6 +240,8 @@ def _out_nbytes(buf) -> int:
     """Size of a writable output buffer (numpy array or bytearray)."""
     import numpy as np
     if isinstance(buf, np.ndarray):
+        if not buf.flags.writeable:  # e.g. np.frombuffer(bytes): the library would write into it
+            raise ValueError("output buffer is read-only")
         return buf.nbytes
     if isinstance(buf, bytearray):
         return len(buf)
@@ -409,8 +411,35 @@ class Context:
             return t.data_ptr()
         return _host_ptr(t)
 
+    @staticmethod
+    def _check_host_bufs(bufs, shard_bytes, writable, what):
+        """The C-ABI takes bare pointers: every host buffer the binding passes
+        must hold shard_bytes contiguous bytes (and be writable for outputs)."""
+        import numpy as np
+        for t in bufs:
+            if t is None or isinstance(t, int):
+                continue
+            if hasattr(t, "data_ptr"):  # CPU torch tensor
+                if t.device.type != "cpu" or not t.is_contiguous():
+                    raise ValueError(f"{what}: host tensors must be contiguous CPU tensors")
+                n = t.numel() * t.element_size()
+            elif isinstance(t, np.ndarray):
+                if writable and not t.flags.writeable:
+                    raise ValueError(f"{what}: output buffer is read-only")
+                n = t.nbytes
+            elif isinstance(t, (bytes, bytearray)):
+                if writable and isinstance(t, bytes):
+                    raise ValueError(f"{what}: output buffer is read-only (bytes)")
+                n = len(t)
+            else:
+                raise TypeError(f"{what}: unsupported host buffer type {type(t)}")
+            if n < shard_bytes:
+                raise ValueError(f"{what}: buffer of {n} bytes < shard_bytes {shard_bytes}")
+
     def encode_host_batch(self, original_counts, recovery_count, shard_bytes, originals,
                           recovery_out) -> None:
+        self._check_host_bufs(originals, shard_bytes, False, "encode_host_batch")
+        self._check_host_bufs(recovery_out, shard_bytes, True, "encode_host_batch")
         ks = (ctypes.c_uint32 * len(original_counts))(*original_counts)
         po, ko = _ptr_array([self._haddr(t) for t in originals])
         pr, kr = _ptr_array([self._haddr(t) for t in recovery_out])
@@ -419,6 +448,9 @@ class Context:
 
     def decode_host_batch(self, original_counts, recovery_count, shard_bytes, originals,
                           recovery, restored_out) -> None:
+        self._check_host_bufs(list(originals) + list(recovery), shard_bytes, False,
+                              "decode_host_batch")
+        self._check_host_bufs(restored_out, shard_bytes, True, "decode_host_batch")
         ks = (ctypes.c_uint32 * len(original_counts))(*original_counts)
         po, ko = _ptr_array([self._haddr(t) for t in originals])
         pr, kr = _ptr_array([self._haddr(t) for t in recovery])
@@ -791,10 +823,12 @@ class Archive:
     def read_into(self, offset: int, out) -> int:
         import numpy as np
         a = out if isinstance(out, np.ndarray) else np.frombuffer(out, dtype=np.uint8)
-        if a.size and not a.flags.c_contiguous:
+        if a.nbytes and not a.flags.c_contiguous:
             raise ValueError("read_into: destination must be C-contiguous")
-        return self.read_into_ptr(offset, a.__array_interface__["data"][0] if a.size else 0,
-                                  a.size)
+        if not a.flags.writeable:  # bytes, or a read-only view: never write into it
+            raise ValueError("read_into: destination is read-only")
+        return self.read_into_ptr(offset, a.__array_interface__["data"][0] if a.nbytes else 0,
+                                  a.nbytes)
 
     def read_into_ptr(self, offset: int, addr: int, size: int) -> int:
         """bfrs_archive_read into host memory at `addr` (the FUSE reply buffer's

@@ -257,3 +257,25 @@ def test_planner_random_shapes_match_oracle(bfrs, oracle, gf_tables):
                 assert np.array_equal(a, want[i]), (k, m, lost, i)
             checked += 1
     assert checked >= 40
+
+
+def test_binding_rejects_short_or_read_only_host_buffers():
+    """The host-batch calls pass bare pointers: the Python binding refuses
+    buffers shorter than shard_bytes and read-only outputs before any call."""
+    import numpy as np
+    import torch
+    import bfrs
+    chk = bfrs.Context._check_host_bufs
+    ok = np.zeros(128, np.uint8)
+    chk([ok, None, torch.zeros(128, dtype=torch.uint8)], 128, True, "t")
+    with pytest.raises(ValueError, match="< shard_bytes"):
+        chk([np.zeros(64, np.uint8)], 128, False, "t")
+    with pytest.raises(ValueError, match="read-only"):
+        chk([np.frombuffer(bytes(128), np.uint8)], 128, True, "t")
+    with pytest.raises(ValueError, match="read-only"):
+        chk([bytes(128)], 128, True, "t")
+    chk([bytes(128)], 128, False, "t")  # inputs may be read-only
+    with pytest.raises(ValueError, match="contiguous"):
+        chk([torch.zeros(256, dtype=torch.uint8)[::2]], 128, False, "t")
+    with pytest.raises(ValueError, match="read-only"):
+        bfrs._out_nbytes(np.frombuffer(bytes(8), np.uint8))
