@@ -21,11 +21,14 @@ Sub-objects of the same JSON line:
   c4_strong    BASELINE configs[3]: 320 x 32 MiB (10 x RS(30,3) + 1 x RS(20,3)),
                64-B column stripes of every shard over the ranks (strong scaling)
   roofline     gf_apply launch time from HIP events on the launch stream;
-               traffic = PMC bytes of this launch shape (source file named)
+               traffic = HBM bytes per launch from two rocprofv3 --pmc child
+               passes run before the GPU is touched (N=1; the committed
+               profiles/pmc_traffic.json record otherwise, named)
   cpu_baseline the oracle's AVX2 engine (restatement of reed-solomon-simd, not
                the crate) on C2's exact blocks; host CPU model and core counts
   crate_api    the crate-shaped host-memory path BlockFrame calls per block
-               (bfrs_generate_parity / bfrs_recover_segment_rs30_3)
+               (bfrs_generate_parity / bfrs_recover_segment_rs30_3), and
+               rayon's all-blocks shape, also in a fresh child process
   pcie_inclusive  the same batch from pinned host memory (H2D + kernel + D2H)
   c5           BASELINE configs[4]: read of a corrupted 4 GiB tier-3 archive
                through the mount's read core (bfrs_archive_read)
