@@ -314,11 +314,12 @@ def run_c4_strong(rt, ctx, args, stream_handle):
     _, t_dec = timed(rt, lambda: dec(stream_handle), steps)
     rt.sync()
     check = {"decode": check_restored(sets)}
-    if rt.world == 1 and not rt.stub:
+    if rt.stub:
+        check["encode"] = None
+    elif rt.world == 1:
         check["encode"] = check_parity_golden(sets.parity, shapes, sets.S, 0xB10C, "c4_320x32MiB")
     else:
-        check["encode"] = {"match": None, "note": "golden digests cover whole shards; at N > 1 "
-                                                  "the stripes are checked in tests (gloo world 2)"}
+        check["encode"] = check_c4_stripes_golden(rt, sets.parity, shapes, S_full)
     pcie = None
     if args.pcie == "auto" and not rt.stub:
         # device-resident AND incl. pinned H2D/D2H; every
@@ -353,6 +354,31 @@ def run_c4_strong(rt, ctx, args, stream_handle):
 
 # ---------------------------------------------------------------- parity check
 GOLDEN = os.path.join(ROOT, "tests", "golden", "rs_large.json")
+
+
+def check_c4_stripes_golden(rt, parity, shapes, S_full):
+    """N > 1: the golden digests cover whole shards, so after the timed region
+    every rank's parity stripes are all-gathered (one collective, outside
+    any timing), rank 0 reassembles the 33 whole shards and checks them
+    against tests/golden/rs_large.json["c4_320x32MiB"]."""
+    from bfrs import parallel
+    torch = rt.torch
+    ranges = parallel.stripe_ranges(S_full, rt.world)
+    wmax = max(hi - lo for lo, hi in ranges)
+    mine = torch.zeros(parity.shape[0], wmax, dtype=torch.uint8, device=rt.coll_device)
+    mine[:, :parity.shape[1]].copy_(parity)
+    parts = [torch.empty_like(mine) for _ in range(rt.world)]
+    rt.dist.all_gather(parts, mine)
+    if rt.rank != 0:
+        return {"match": None, "note": "checked on rank 0"}
+    whole = torch.empty(parity.shape[0], S_full, dtype=torch.uint8, device=rt.coll_device)
+    for g, (lo, hi) in enumerate(ranges):
+        whole[:, lo:hi].copy_(parts[g][:, :hi - lo])
+    del parts
+    r = check_parity_golden(whole, shapes, S_full, 0xB10C, "c4_320x32MiB")
+    if r is not None:
+        r["assembled_from_ranks"] = rt.world
+    return r
 
 
 def golden_parity(name):
@@ -1387,8 +1413,8 @@ def main():
         "when": "after the timed region, on the buffers the timed launches wrote",
     }
     flags = [all(ranks_ok), (my_check["encode"] or {}).get("match"), (c1 or {}).get("match"),
-             (c4 or {}).get("parity_check", {}).get("encode", {}).get("match"),
-             (c4 or {}).get("parity_check", {}).get("decode", {}).get("match"),
+             ((c4 or {}).get("parity_check", {}).get("encode") or {}).get("match"),
+             ((c4 or {}).get("parity_check", {}).get("decode") or {}).get("match"),
              None if c5 is None else c5.get("blake3_match")]
     line["parity_check"]["all_ok"] = not any(f is False for f in flags)
     print(json.dumps(line), flush=True)

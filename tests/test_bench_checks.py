@@ -170,3 +170,40 @@ def test_rayon_fresh_process_child(monkeypatch):
     assert "exited 137" in bench.rayon_fresh_process()["error"]
     monkeypatch.setattr(sp, "run", lambda *a, **k: R(0, "not json"))
     assert "error" in bench.rayon_fresh_process()
+
+
+def test_c4_stripes_reassembled_for_the_golden_check(monkeypatch):
+    """N > 1: c4_strong's parity stripes are all-gathered after the timed
+    region and rank 0 checks the reassembled whole shards against the golden
+    digests; a wrong byte in another rank's stripe is caught."""
+    from bfrs import parallel
+    shapes, S, world = [3, 2], 384, 3
+    whole = _rows(3 * len(shapes), S, 5)
+    golden = {"blocks": shapes, "segment_size": S, "seed": 0xB10C,
+              "parity_sha256": [[hashlib.sha256(whole[3 * b + j].numpy().tobytes()).hexdigest()
+                                 for j in range(3)] for b in range(len(shapes))]}
+    monkeypatch.setattr(bench, "golden_parity", lambda name: golden)
+    ranges = parallel.stripe_ranges(S, world)
+    assert len({hi - lo for lo, hi in ranges}) >= 1 and ranges[-1][1] == S
+
+    def fake_rt(stripes):
+        class Dist:
+            @staticmethod
+            def all_gather(parts, mine):
+                for g, p in enumerate(parts):
+                    p.zero_()
+                    p[:, :stripes[g].shape[1]].copy_(stripes[g])
+
+        class RT:
+            rank, coll_device = 0, "cpu"
+            dist = Dist()
+        rt = RT()
+        rt.world, rt.torch = world, torch
+        return rt
+
+    stripes = [whole[:, lo:hi].clone() for lo, hi in ranges]
+    r = bench.check_c4_stripes_golden(fake_rt(stripes), stripes[0], shapes, S)
+    assert r["match"] and r["assembled_from_ranks"] == world and r["shards"] == 6
+    stripes[2][4, 3] ^= 0x10  # block 1, parity 1, in the last rank's stripe
+    r = bench.check_c4_stripes_golden(fake_rt(stripes), stripes[0], shapes, S)
+    assert not r["match"] and r["mismatched"] == [[1, 1]]
