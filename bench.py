@@ -842,6 +842,54 @@ def crate_api(ctx, sets, reps=7, staging_ab=True):
     return res
 
 
+B3_GOLDEN = os.path.join(ROOT, "tests", "golden", "blake3_c2.json")
+# VALU ceiling of the device BLAKE3: one lane compresses one
+# 1 KiB chunk block by block; ~780 VALU per 64-B block and lane (round-2 PMC),
+# 256 CUs x 4 SIMDs x 16 lanes per clock at the 2.4 GHz peak clock
+B3_VALU_PER_BLOCK = 780
+B3_VALU_CEILING_GBPS = 256 * 64 * 2.4e9 / B3_VALU_PER_BLOCK * 64 / 1e9
+
+
+def blake3_device(ctx, sets, calls=10):
+    """f2: the device BLAKE3 over C2's 128 HBM-resident data
+    segments in one bfrs_blake3_batch_dev call (descriptor upload, both
+    kernels and the digest download included), best and mean of `calls`,
+    against its VALU ceiling, and every digest against the oracle's golden
+    (tests/golden/blake3_c2.json: the per-segment hashes a tier-3 commit
+    writes, commit.rs:429)."""
+    import torch
+    rows = [sets.data[i] for i in range(sets.data.shape[0])]
+    nbytes = sum(r.numel() for r in rows)
+    for _ in range(3):
+        ctx.blake3_batch_dev(rows)
+    ts = []
+    for _ in range(calls):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        hexes = ctx.blake3_batch_dev(rows)
+        ts.append(time.perf_counter() - t0)
+    check = None
+    try:
+        g = json.load(open(B3_GOLDEN))
+    except (OSError, ValueError):
+        g = None
+    if g and g["segments"] == len(rows) and g["segment_size"] == sets.S and g["seed"] == 0xB10C:
+        bad = [i for i, h in enumerate(hexes) if h != g["blake3"][i]]
+        check = {"golden": "tests/golden/blake3_c2.json", "digests": len(hexes),
+                 "mismatched": bad, "match": not bad}
+    best = min(ts)
+    return {"GBps": round(nbytes / best / 1e9, 1), "ms": round(best * 1e3, 3),
+            "mean_ms": round(sum(ts) / len(ts) * 1e3, 3), "bytes": nbytes,
+            "roofline": {"bound": "valu", "achieved": round(nbytes / best / 1e9, 1),
+                         "peak": round(B3_VALU_CEILING_GBPS, 1), "unit": "GB/s",
+                         "frac": round(nbytes / best / 1e9 / B3_VALU_CEILING_GBPS, 4),
+                         "note": f"~{B3_VALU_PER_BLOCK} VALU per 64-B block and lane; "
+                                 "256 CUs x 64 lane-ops per clock at 2.4 GHz"},
+            "parity_check": check,
+            "what": "bfrs_blake3_batch_dev over C2's 128 x 32 MiB data segments in HBM, one call "
+                    "(upload + kernels + digest download), best of 10 wall-clock calls"}
+
+
 def rayon_fresh_process():
     """BlockFrame's commit_blocked shape (one generate_parity per block on
     every rayon worker, commit.rs:391-466) in a process of its own, as a
@@ -1325,6 +1373,7 @@ def main():
             return {"error": f"{type(e).__name__}: {e}"}
 
     c1 = check_config1(ctx) if not rt.stub else None
+    b3 = guarded(blake3_device, ctx, sets) if n1 and not rt.stub and not args.strong else None
     if n1 and args.pcie == "auto" and not args.strong:
         pcie = guarded(pcie_inclusive, ctx, sets)
     if n1 and args.crate == "auto" and not args.strong:
@@ -1402,6 +1451,7 @@ def main():
         line["crate_api"] = crate
         line["pcie_inclusive"] = pcie
         line["c5"] = c5
+        line["blake3_device"] = b3
     line["c4_strong"] = c4
     line["parity_check"] = {
         "c1_rs13": c1,
@@ -1410,12 +1460,14 @@ def main():
         "c4_encode": (c4 or {}).get("parity_check", {}).get("encode"),
         "c4_decode": (c4 or {}).get("parity_check", {}).get("decode"),
         "c5_blake3": None if c5 is None else c5.get("blake3_match"),
+        "blake3_c2": ((b3 or {}).get("parity_check") or {}).get("match"),
         "when": "after the timed region, on the buffers the timed launches wrote",
     }
     flags = [all(ranks_ok), (my_check["encode"] or {}).get("match"), (c1 or {}).get("match"),
              ((c4 or {}).get("parity_check", {}).get("encode") or {}).get("match"),
              ((c4 or {}).get("parity_check", {}).get("decode") or {}).get("match"),
-             None if c5 is None else c5.get("blake3_match")]
+             None if c5 is None else c5.get("blake3_match"),
+             ((b3 or {}).get("parity_check") or {}).get("match")]
     line["parity_check"]["all_ok"] = not any(f is False for f in flags)
     print(json.dumps(line), flush=True)
     rt.close()

@@ -8,6 +8,7 @@ tests/test_oracle.py before these fixtures are trusted).
   python tests/golden/make_golden.py            # small vectors (seconds)
   python tests/golden/make_golden.py --large    # config-size digests (minutes)
   python tests/golden/make_golden.py --r2       # RS(3,3)/RS(4,3) under both rates
+  python tests/golden/make_golden.py --blake3   # BLAKE3 of C2's 128 segments (bench.py)
 """
 import argparse
 import hashlib
@@ -97,6 +98,21 @@ def large(threads):
                    "synth": "blockframe-rs_amd/bfrs/synth.py splitmix64", **out}, f, indent=1)
 
 
+def blake3_c2():
+    """BLAKE3 of each of C2's 128 data segments (seed 0xB10C), by the oracle's
+    BLAKE3 (pinned to the reference KAT, src/utils.rs:17-18): the golden of
+    bench.py's device-BLAKE3 sub-object (the per-segment hashes a tier-3
+    commit writes into the manifest, commit.rs:429)."""
+    digests = []
+    for i in range(128):
+        digests.append(O.blake3_hex(synth.segment_np(0xB10C, i, synth.SEGMENT_SIZE)))
+    with open(os.path.join(HERE, "blake3_c2.json"), "w") as f:
+        json.dump({"generator": "tests/golden/make_golden.py --blake3",
+                   "synth": "blockframe-rs_amd/bfrs/synth.py splitmix64", "seed": 0xB10C,
+                   "segments": 128, "segment_size": synth.SEGMENT_SIZE,
+                   "blake3": digests}, f, indent=1)
+
+
 def r2():
     """Risk r2 (SURVEY §7, A.4): which rate DefaultRate picks for k in {3, 4}
     at m = 3 decides the parity bytes of a tier-3 file whose last block holds
@@ -138,11 +154,14 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--large", action="store_true")
     ap.add_argument("--r2", action="store_true")
+    ap.add_argument("--blake3", action="store_true")
     ap.add_argument("--threads", type=int, default=8)
     a = ap.parse_args()
     if a.large:
         large(a.threads)
     elif a.r2:
         r2()
+    elif a.blake3:
+        blake3_c2()
     else:
         small()
