@@ -1167,13 +1167,38 @@ def run_c5(args, ctx=None):
             "commit_MBps": round(n / commit_s / 1e6, 1),
             "stats_corrupted": dirty_st, "stats_clean": clean_st, "blake3_match": ok,
         }
-        if args.cpu_baseline == "auto":
+        if args.cpu_baseline == "auto":  # reads the damaged files: before the repair below
             res["cpu_baseline"] = c5_cpu_baseline(adir, m, damaged, n)
+        res["repair"] = c5_repair(ctx, adir, n, len(damaged))
         return res
     finally:
         shutil.rmtree(work, ignore_errors=True)
         if own:
             ctx.close()
+
+
+def c5_repair(ctx, adir, nbytes, n_damaged):
+    """The callers either side of the read path on the same damaged archive
+    (rows a4/f1): FileStore::health_check (health.rs:111-438) and
+    FileStore::repair (health.rs:470-495), intended semantics (every shard
+    hashed on the device, RS(k,3) decode of each damaged block, restored
+    bytes re-verified and written to their own in-block index), then a second
+    health check that must say Healthy.  MB/s = file bytes / wall time."""
+    import bfrs
+    t0 = time.perf_counter()
+    before = bfrs.health_check(ctx, adir)
+    t1 = time.perf_counter()
+    rep = bfrs.repair(ctx, adir)
+    t2 = time.perf_counter()
+    after = bfrs.health_check(ctx, adir)
+    ok = (before.get("status") == "Recoverable" and after.get("status") == "Healthy"
+          and rep.get("segments_repaired") == n_damaged)
+    return {"health_check_MBps": round(nbytes / (t1 - t0) / 1e6, 1),
+            "repair_MBps": round(nbytes / (t2 - t1) / 1e6, 1),
+            "status_before": before.get("status"), "status_after": after.get("status"),
+            "report": rep, "match": ok,
+            "what": "bfrs_health_check, bfrs_repair, bfrs_health_check on the damaged archive "
+                    "(files in the page cache)"}
 
 
 def c5_cpu_baseline(adir, m, damaged, nbytes):
@@ -1460,6 +1485,7 @@ def main():
         "c4_encode": (c4 or {}).get("parity_check", {}).get("encode"),
         "c4_decode": (c4 or {}).get("parity_check", {}).get("decode"),
         "c5_blake3": None if c5 is None else c5.get("blake3_match"),
+        "c5_repair": ((c5 or {}).get("repair") or {}).get("match"),
         "blake3_c2": ((b3 or {}).get("parity_check") or {}).get("match"),
         "when": "after the timed region, on the buffers the timed launches wrote",
     }
@@ -1467,6 +1493,7 @@ def main():
              ((c4 or {}).get("parity_check", {}).get("encode") or {}).get("match"),
              ((c4 or {}).get("parity_check", {}).get("decode") or {}).get("match"),
              None if c5 is None else c5.get("blake3_match"),
+             ((c5 or {}).get("repair") or {}).get("match"),
              ((b3 or {}).get("parity_check") or {}).get("match")]
     line["parity_check"]["all_ok"] = not any(f is False for f in flags)
     print(json.dumps(line), flush=True)
