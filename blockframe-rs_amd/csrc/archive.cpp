@@ -539,8 +539,8 @@ using SegPtr = std::shared_ptr<Seg>;
 // Segments are cached in pinned buffers (LRU); a miss reads the file,
 // verifies it on the GPU and, if it is missing or corrupt, reconstructs it
 // (tier 3: RS(k,3) decode of its block on the GPU, device re-verify).  When
-// reads move to a new segment, the next kPrefetchDepth segments are queued
-// for kPrefetchWorkers threads that load and verify them (reconstructing a
+// reads move to a new segment, the next prefetch_depth segments are queued
+// for prefetch_workers threads that load and verify them (reconstructing a
 // damaged one with its block), so sequential reads
 // overlap file reads, PCIe and hashing with serving (the file read of one
 // segment overlaps the GPU verify of another).
@@ -557,7 +557,9 @@ struct bfrs_archive {
   std::list<size_t> lru;
   std::unordered_map<size_t, std::pair<SegPtr, std::list<size_t>::iterator>> cache;
   bfrs_archive_stats st{};
-  static constexpr size_t kPrefetchDepth = 4, kPrefetchWorkers = 2;
+  // segments queued ahead of the reader and the threads that load them
+  // (BFRS_PREFETCH_DEPTH / BFRS_PREFETCH_WORKERS override at open)
+  size_t prefetch_depth = 16, prefetch_workers = 2;
   std::deque<size_t> wantq;               // queued, not started
   // segments being loaded (by a prefetch worker or a reader); everyone else
   // waits on cv for them instead of loading them again
@@ -1221,10 +1223,14 @@ int bfrs_archive_open(bfrs_ctx *ctx, const char *archive_dir, size_t cache_segme
   int rc = load_geometry(archive_dir, &a->g);
   if (rc) return rc;
   a->pool = std::make_shared<PinnedPool>(a->g.S);
+  if (const char *e = std::getenv("BFRS_PREFETCH_DEPTH"))
+    a->prefetch_depth = size_t(std::clamp(std::strtol(e, nullptr, 10), 1L, 256L));
+  if (const char *e = std::getenv("BFRS_PREFETCH_WORKERS"))
+    a->prefetch_workers = size_t(std::clamp(std::strtol(e, nullptr, 10), 1L, 16L));
   a->prefetch = a->g.nseg > 1;
   if (a->prefetch) {
     try {
-      for (size_t w = 0; w < bfrs_archive::kPrefetchWorkers; ++w)
+      for (size_t w = 0; w < a->prefetch_workers; ++w)
         a->workers.emplace_back(&bfrs_archive::prefetch_loop, a.get());
     } catch (const std::system_error &) {  // no thread: fewer prefetch workers, or none
     }
@@ -1291,7 +1297,7 @@ int bfrs_archive_read(bfrs_archive *a, uint64_t offset, size_t len, uint8_t *out
     if (a->prefetch && (long long)gi != a->last_gi) {  // moved to a new segment
       a->last_gi = (long long)gi;
       // the next segments, at most half the cache so they are not evicted unread
-      const size_t depth = std::min(bfrs_archive::kPrefetchDepth, std::max<size_t>(1, a->cap / 2));
+      const size_t depth = std::min(a->prefetch_depth, std::max<size_t>(1, a->cap / 2));
       bool queued = false;
       for (size_t nx = gi + 1; nx <= gi + depth && nx < a->g.nseg; ++nx)
         if (!a->cache.count(nx) && !a->inflight.count(nx) &&

@@ -46,6 +46,10 @@
  *                       process's CPU share (cgroup quota), split evenly
  *                       between the calls in flight
  *   BFRS_HOST_COPY_BUDGET   helper threads in total (default CPU share - 1)
+ *   BFRS_PREFETCH_DEPTH / BFRS_PREFETCH_WORKERS  archive read handles: segments
+ *                       loaded ahead of the reader (default 16, at most half
+ *                       the cache) and the threads that load them (default 2);
+ *                       read by bfrs_archive_open
  *   BFRS_KERNEL_VARIANT unset or 76 (default kernel); 75 / 73 force the looped
  *                       subfield / general kernels; anything else fails
  *                       bfrs_open with BFRS_E_INVALID_ARGUMENT (the A/B
