@@ -181,12 +181,35 @@ def cross(a):
 
 def summarize(a):
     per = collections.defaultdict(dict)  # dispatch -> {counter: value, "ns": duration}
+    inst = collections.defaultdict(lambda: collections.defaultdict(list))  # dispatch -> counter -> rows
     for r in csv.DictReader(open(a.summarize)):
         if "gf_apply" not in r["Kernel_Name"] or int(r["Grid_Size"]) != C2_GRID:
             continue
         d = per[int(r["Dispatch_Id"])]
         d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
         d["ns"] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        inst[int(r["Dispatch_Id"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    if a.instances:  # spread of a counter over its hardware instances (e.g. TCC channels)
+        ids = sorted(per)[-a.copies * a.launches:]
+        out = []
+        for c in range(a.copies):
+            sel = ids[c * a.launches:(c + 1) * a.launches][3:]
+            if not sel:
+                continue
+            row = {"copy": c, "ms": round(statistics.median(per[i]["ns"] for i in sel) / 1e6, 4)}
+            for k in sorted(inst[sel[0]]):
+                vals = [inst[i][k] for i in sel]
+                n = len(vals[0])
+                mean_inst = [statistics.mean(v[j] for v in vals) for j in range(n)]
+                m = statistics.mean(mean_inst)
+                row[k] = {"instances": n, "sum": round(sum(mean_inst), 1),
+                          "max_over_mean": round(max(mean_inst) / m, 4) if m else None,
+                          "min_over_mean": round(min(mean_inst) / m, 4) if m else None,
+                          "cv": round(statistics.pstdev(mean_inst) / m, 4) if m and n > 1 else None,
+                          "per_instance": [round(x, 1) for x in mean_inst] if n <= 128 else None}
+            out.append(row)
+        print(json.dumps(out, indent=1))
+        return
     ids = sorted(per)[-a.copies * a.launches:]  # after the settle launches
     out = []
     for c in range(a.copies):
@@ -205,6 +228,8 @@ def main():
     ap.add_argument("--launches", type=int, default=20)
     ap.add_argument("--settle", type=int, default=60, help="untimed launches before the copies")
     ap.add_argument("--summarize", default=None)
+    ap.add_argument("--instances", action="store_true",
+                    help="with --summarize: each counter's spread over its hardware instances")
     ap.add_argument("--pitches", default=None,
                     help="comma list of row pitches minus S (bytes): per copy, one buffer of 143 rows at "
                          "the largest pitch, encode timed with each pitch inside the same buffer")
