@@ -166,3 +166,16 @@ def test_manifest_bad_map_key_is_an_error_not_a_crash(bfrs, key):
     with pytest.raises(bfrs.BfrsError) as e:
         bfrs.manifest_check(_canon(m))
     assert e.value.code == bfrs.E_WRAPPER
+
+
+def test_blake3_c2_golden_matches_oracle(oracle):
+    """tests/golden/blake3_c2.json (the golden of bench.py's device-BLAKE3
+    check) holds the oracle's BLAKE3 of C2's segments: re-derived here for
+    the first and the last segment."""
+    import os
+    from bfrs import synth
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "blake3_c2.json")))
+    assert g["segments"] == 128 and g["seed"] == 0xB10C and g["segment_size"] == synth.SEGMENT_SIZE
+    for i in (0, 127):
+        seg = synth.segment_np(0xB10C, i, synth.SEGMENT_SIZE)
+        assert oracle.blake3_hex(seg) == g["blake3"][i]
