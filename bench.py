@@ -92,7 +92,14 @@ def parse(argv=None):
     ap.add_argument("--pmc", choices=["auto", "off"], default="auto",
                     help="N=1: measure roofline.traffic live with two rocprofv3 --pmc child "
                          "passes before the timed run (off: the committed profiles/ record)")
+    ap.add_argument("--trace", choices=["auto", "off"], default="auto",
+                    help="N=1: roofline.trace from a rocprofv3 --kernel-trace --stats child pass "
+                         "over the bench's own device loop, before the timed run")
+    ap.add_argument("--profile-dir", default=None,
+                    help="keep the trace pass's kernel stats and C2 launch summary here")
     ap.add_argument("--traffic-probe", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--trace-probe", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--stub-legs", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--stub", action="store_true",
                     help="CPU-only rehearsal of the launcher/partition/timing path: no GPU, "
                          "the codec calls replaced by a stand-in (tests only, never a bench line)")
@@ -101,8 +108,18 @@ def parse(argv=None):
         a.segments = 320
     if a.stub:
         a.backend = "gloo"
-        a.cpu_baseline = a.pcie = a.crate = a.c5 = "off"
+        a.pmc = a.trace = "off"
+        if not a.stub_legs:  # --stub-legs: tests stand in for the N=1 legs themselves
+            a.cpu_baseline = a.pcie = a.crate = a.c5 = "off"
     return a
+
+
+T_START = time.perf_counter()
+
+
+def progress(msg):
+    """One stderr line per bench phase (a long run shows it is alive)."""
+    print(f"bench.py [{time.perf_counter() - T_START:7.1f} s] {msg}", file=sys.stderr, flush=True)
 
 
 # ---------------------------------------------------------------- launcher
@@ -112,18 +129,52 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def launch_ranks(args) -> int:
+RANK_GRACE_S = 10.0   # SIGTERM -> SIGKILL grace for the siblings of a failed rank
+PG_TIMEOUT_S = 180.0  # process-group timeout (rendezvous and every collective)
+
+
+def launch_ranks(args, argv=None) -> int:
     """--gpus N without torchrun: start N rank processes (this process never
-    touches the GPU), wait, return the first non-zero exit code."""
+    touches the GPU) and reap them in the order they exit (os.wait).  The
+    first rank that exits non-zero ends the job: its siblings get SIGTERM,
+    then SIGKILL after RANK_GRACE_S, and its exit code is returned with the
+    rank named on stderr.  (Waiting on the ranks in rank order would leave the
+    others blocked in a barrier until the process-group timeout.)  0 when
+    every rank exits 0."""
+    import signal
     port = _free_port()
+    argv = sys.argv[1:] if argv is None else argv
     procs = []
     for r in range(args.gpus):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
                    LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
-                                      env=env))
-    rcs = [p.wait() for p in procs]
-    return next((rc for rc in rcs if rc), 0)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    by_pid = {p.pid: (r, p) for r, p in enumerate(procs)}
+    failed = None
+    while by_pid and failed is None:
+        pid, status = os.wait()  # the next rank to exit, in the order they exit
+        if pid not in by_pid:
+            continue
+        r, p = by_pid.pop(pid)
+        p.returncode = os.waitstatus_to_exitcode(status)
+        if p.returncode != 0:
+            failed = (r, p.returncode)
+    if failed is None:
+        return 0
+    rank, rc = failed
+    print(f"bench.py: rank {rank} exited {rc}; terminating the other ranks", file=sys.stderr,
+          flush=True)
+    live = [p for _, p in by_pid.values()]
+    for p in live:
+        p.send_signal(signal.SIGTERM)
+    t_end = time.time() + RANK_GRACE_S
+    for p in live:
+        try:
+            p.wait(timeout=max(0.0, t_end - time.time()))
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
+    return rc if rc > 0 else 128 - rc  # a signal (-N) becomes 128 + N, as a shell reports it
 
 
 class Runtime:
@@ -145,14 +196,36 @@ class Runtime:
             torch.cuda.set_device(self.device)
         self.dist = None
         if self.world > 1 or "TORCHELASTIC_RUN_ID" in os.environ:  # under torchrun: RCCL even at N=1
+            import datetime
             import torch.distributed as dist
-            kw = {}
+            kw = {"timeout": datetime.timedelta(seconds=PG_TIMEOUT_S)}
             if args.backend == "nccl":
                 kw["device_id"] = self.device
             dist.init_process_group(args.backend, **kw)
             assert dist.get_world_size() == self.world == args.gpus
             self.dist = dist
         self.coll_device = "cpu" if args.backend == "gloo" else self.device
+        if os.environ.get("BENCH_FAIL_RANK") == str(self.rank):
+            # test hook (tests/test_parallel.py): this rank dies right after
+            # joining the process group, as a rank that faults early would
+            raise SystemExit(3)
+
+    def device_info(self) -> dict:
+        """This rank's device as the process sees it: the HIP ordinal and the
+        PCI bus id (distinct ids per rank prove one GPU per rank)."""
+        if self.stub:
+            return {"rank": self.rank, "device": "cpu", "pci_bus_id": None}
+        p = self.torch.cuda.get_device_properties(self.device)
+        bus = getattr(p, "pci_bus_id", None)
+        return {"rank": self.rank, "device": self.torch.cuda.current_device(),
+                "pci_bus_id": bus, "name": p.name}
+
+    def gather_objects(self, obj) -> list:
+        if not self.dist:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
 
     def sync(self):
         if not self.stub:
@@ -190,6 +263,38 @@ def timed(rt, step, steps):
     el = time.perf_counter() - t0
     rt.barrier()
     return el, rt.max_over_ranks(el)
+
+
+def device_loop(rt, step, stream, args):
+    """Settle, W warmup steps, then the timed region: K steps between a
+    barrier + synchronize on both sides.  HIP events on the launch stream
+    bracket the same region: every launch in it is gf_apply (2 per step), so
+    their mean duration = span / 2K.  Returns (settle steps, this rank's
+    seconds, launch ms).  The bench and its kernel-trace child run this same
+    loop, so the trace's last 2K dispatches are the child's timed region."""
+    settle_steps = settle(rt, step, args.settle_ms)
+    for _ in range(args.warmup):
+        step()
+    rt.sync()
+    # (the correctness guard runs after the timed region: host work here would
+    # idle the GPU and the timed region would start on ramping clocks again)
+    torch = rt.torch
+    if stream is not None:
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    rt.barrier()
+    rt.sync()
+    t0 = time.perf_counter()
+    if stream is not None:
+        ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    if stream is not None:
+        ev1.record(stream)
+    rt.sync()
+    elapsed = time.perf_counter() - t0  # this rank's K steps; the job time is the max over ranks
+    rt.barrier()
+    launch_ms = ev0.elapsed_time(ev1) / (2 * args.steps) if stream is not None else None
+    return settle_steps, elapsed, launch_ms
 
 
 def settle(rt, step, ms):
@@ -406,6 +511,103 @@ def check_parity_golden(parity_rows, shapes, S, seed, name):
             "mismatched": bad, "match": not bad}
 
 
+def golden_covers(name, shapes, S, seed) -> bool:
+    """True when tests/golden/rs_large.json[name] is the digest set of exactly
+    this batch, so its check must run and must match."""
+    g = golden_parity(name)
+    return bool(g) and g["blocks"] == list(shapes) and g["segment_size"] == S and g["seed"] == seed
+
+
+class Legs:
+    """The side legs of a bench line (config 1, device BLAKE3, PCIe, crate
+    API, CPU baseline, config 5).  Every exception becomes the leg's
+    {"error": ...} entry, which parity_summary counts as a FAILED check: the
+    line still prints, with all_ok false, and the process exits non-zero.
+    OSError / MemoryError (disk space for c5's archive, host memory for
+    pinned buffers) let the later legs run; anything else (a BfrsError from
+    the library, a HIP fault, a wrong result) skips them, since the device
+    may be unusable, and names the leg in parity_check.aborted."""
+
+    def __init__(self):
+        self.aborted = None
+
+    def run(self, name, fn, *a):
+        if self.aborted:
+            return {"error": f"skipped: {self.aborted}"}
+        progress(f"leg {name}")
+        try:
+            return fn(*a)
+        except (OSError, MemoryError) as e:
+            return {"error": f"{type(e).__name__}: {e}"}
+        except Exception as e:  # noqa: BLE001 - recorded as this leg's failure
+            self.aborted = f"{name} raised {type(e).__name__}"
+            return {"error": f"{type(e).__name__}: {e}"}
+
+
+def leg_flag(res, *path):
+    """The check value at `path` inside an enabled leg's result; a missing
+    result or an {"error": ...} entry is a failed check (False), never None."""
+    if not isinstance(res, dict) or "error" in res:
+        return False
+    v = res
+    for k in path:
+        v = v.get(k) if isinstance(v, dict) else None
+    return v
+
+
+def parity_summary(enabled, detail):
+    """parity_check of the line: `enabled` maps each check to (expected?,
+    value).  An expected check passes only with value True: False, None (the
+    check did not run) and an error entry all fail, so all_ok cannot be true
+    while an enabled check was skipped.  Checks that do not apply (no golden
+    covers a non-default batch size, a leg switched off) are listed apart."""
+    failed = [k for k, (exp, v) in enabled.items() if exp and v is not True]
+    out = dict(detail)
+    out["expected"] = sorted(k for k, (exp, _) in enabled.items() if exp)
+    out["not_applicable"] = sorted(k for k, (exp, _) in enabled.items() if not exp)
+    out["failed"] = failed
+    out["all_ok"] = not failed
+    return out
+
+
+def host_budget(args, world):
+    """Pinned host memory the run asks for, per rank and for the node, beside
+    what the host offers (MemTotal / MemAvailable, the cgroup's memory.max).
+    At N > 1 the only pinned buffers are c4_strong.pcie_inclusive's: each
+    rank's stripes of config 4's data, parity and restored shards."""
+    from bfrs import parallel, synth
+    shapes = synth.block_shapes(args.c4_segments)
+    stripe = max(hi - lo for lo, hi in parallel.stripe_ranges(args.segment_bytes, world))
+    c4_pinned = ((sum(shapes) + 6 * len(shapes)) * stripe
+                 if args.c4 == "auto" and args.pcie == "auto" and not args.strong else 0)
+    per_rank = c4_pinned
+    if world == 1 and args.pcie == "auto" and not args.strong:  # + pcie_inclusive's C2 buffers
+        c2 = synth.block_shapes(args.segments)
+        per_rank = max(per_rank, (sum(c2) + 6 * len(c2)) * args.segment_bytes)
+    mem = {}
+    try:
+        for line in open("/proc/meminfo"):
+            k, v = line.split(":", 1)
+            if k in ("MemTotal", "MemAvailable"):
+                mem[k] = int(v.split()[0]) * 1024
+    except (OSError, ValueError):
+        pass
+    cg = None
+    try:
+        t = open("/sys/fs/cgroup/memory.max").read().strip()
+        cg = None if t == "max" else int(t)
+    except (OSError, ValueError):
+        pass
+    node = per_rank * world
+    avail = min(x for x in (mem.get("MemAvailable"), cg) if x) if (mem.get("MemAvailable") or cg) else None
+    return {"pinned_bytes_per_rank": per_rank, "ranks": world, "pinned_bytes_node": node,
+            "c4_pcie_pinned_bytes_per_rank": c4_pinned,
+            "mem_total": mem.get("MemTotal"), "mem_available": mem.get("MemAvailable"),
+            "cgroup_memory_max": cg, "fits": None if avail is None else node < avail,
+            "what": "largest pinned host buffer set of one rank (c4_strong.pcie_inclusive at N>1; "
+                    "at N=1 also pcie_inclusive's C2 batch) x ranks, against this host"}
+
+
 def check_config1(ctx):
     """BASELINE configs[0]: a single 8 MB file's RS(1,3) through the product
     (Chunker::generate_parity_segmented, generate.rs:26-57, then
@@ -509,6 +711,7 @@ def cpu_baseline(args, sets, info):
         return time.perf_counter() - t0
 
     res = {}
+    self_ok = True  # the engine's own results: last block's parity, every restored shard
     # rayon over blocks (codec only, then + wrapper copies)
     for name, copies in (("rayon_blocks", False), ("rayon_blocks_wrapper_copies", True)):
         t_e = run(min(threads, nb), shapes, blocks, [[None] * 3] * nb, par, False, copies)
@@ -519,9 +722,9 @@ def cpu_baseline(args, sets, info):
     for b, k in enumerate(shapes):
         want = oracle.encode(blocks[b][:k], 3, eng) if b == nb - 1 else None
         if want is not None:
-            assert all(np.array_equal(par[b][j], want[j]) for j in range(3)), "cpu parity check"
+            self_ok &= all(np.array_equal(par[b][j], want[j]) for j in range(3))
         for i in sets.erased[b]:
-            assert np.array_equal(rest[b][i], blocks[b][i]), "cpu decode check"
+            self_ok &= bool(np.array_equal(rest[b][i], blocks[b][i]))
     # column stripes over all cores (64-B aligned)
     def striped(nthreads, nst):
         sw = S // nst
@@ -561,6 +764,7 @@ def cpu_baseline(args, sets, info):
     st = res["striped"]
     return {
         "value": st["value"], "unit": "GiB/s", "cores": threads, "kind": "port",
+        "self_check": bool(self_ok),
         "engine": "avx2" if eng == oracle.ENGINE_AVX2 else "scalar",
         "encode_GiBps": st["encode_GiBps"], "decode_GiBps": st["decode_GiBps"],
         "sample": f"C2's exact blocks ({'+'.join(map(str, shapes))} x 32 MiB), encode + the bench's "
@@ -626,6 +830,7 @@ def crate_api(ctx, sets, reps=7, staging_ab=True):
     ch = bfrs.Chunker(ctx)
 
     medians = {}
+    recover_ok = []  # every wrappers() round checks its restored segment against the original
 
     def timed(f, n=reps, key=None):
         """Best of n wall-clock calls; the median is kept under `key`: the host
@@ -691,8 +896,8 @@ def crate_api(ctx, sets, reps=7, staging_ab=True):
                                                             np.empty(S, np.uint8)),
                    key=f"recover_{id(c)}")
         got = np.empty(S, np.uint8)
-        assert bfrs.recover_segment_rs30_3_into(c, slots, par, target, got) == S
-        assert np.array_equal(got, segs[target]), "crate_api recover mismatch"
+        ok = bfrs.recover_segment_rs30_3_into(c, slots, par, target, got) == S
+        recover_ok.append(ok and np.array_equal(got, segs[target]))
         tr_reuse = timed(lambda: bfrs.recover_segment_rs30_3_into(c, slots, par, target, got))
         return tg, tr, par, slots, target, tg_reuse, tr_reuse, tg_new_in
 
@@ -801,6 +1006,7 @@ def crate_api(ctx, sets, reps=7, staging_ab=True):
                                    "python_wrapper_ms": round(tr_py * 1e3, 2),
                                    "what": "one erased segment of that block, pageable host in/out"},
         "breakdown": bd,
+        "recover_match": bool(recover_ok) and all(recover_ok),
         "generate_parity_all_blocks_threads": {
             "ms": round(min(t_par) * 1e3, 2), "GiBps": round(par_gib / min(t_par), 2),
             "median_ms": round(sorted(t_par)[len(t_par) // 2] * 1e3, 2),
@@ -834,6 +1040,7 @@ def crate_api(ctx, sets, reps=7, staging_ab=True):
             pg, pr, _, _, _, pg_reuse, pr_reuse, pg_new_in = wrappers(c2)
         finally:
             c2.close()
+        res["recover_match"] = all(recover_ok)
         res["alt_staging"] = {"staging": alt, "generate_parity_ms": round(pg * 1e3, 2),
                               "generate_parity_touched_outputs_ms": round(pg_reuse * 1e3, 2),
                               "generate_parity_new_inputs_ms": round(pg_new_in * 1e3, 2),
@@ -954,13 +1161,15 @@ def pcie_inclusive(ctx, sets, steps=2, rt=None, job_bytes=None):
 
     t_enc = clock(lambda: ctx.encode_host_batch(shapes, 3, S, enc_in, enc_out))
     t_dec = clock(lambda: ctx.decode_host_batch(shapes, 3, S, dec_in_h, enc_out, dec_out_h))
-    seg = 0
+    seg, bad = 0, []
     for b, k in enumerate(shapes):
         for t, i in enumerate(sets.erased[b]):
-            assert torch.equal(h_rest[3 * b + t], h_data[seg + i]), "host-path decode mismatch"
+            if not torch.equal(h_rest[3 * b + t], h_data[seg + i]):
+                bad.append([b, i])
         seg += k
     gib = (job_bytes or nseg * S) / 2**30
     return {
+        "decode_match": not bad, "decode_mismatched": bad,
         "encode_GiBps": round(gib / t_enc, 2), "decode_GiBps": round(gib / t_dec, 2),
         "encode_ms": round(t_enc * 1e3, 2), "decode_ms": round(t_dec * 1e3, 2),
         "h2d_bytes_encode": nseg * S, "d2h_bytes_encode": 3 * nb * S,
@@ -1057,6 +1266,125 @@ def live_pmc_traffic(args):
         "dispatches": [len(fetch), len(write)],
         "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
         "seconds": round(time.perf_counter() - t0, 1)}
+
+
+TRACE_PASS_TIMEOUT_S = 150
+
+
+def trace_probe(args):
+    """--trace-probe: the child of the live kernel-trace pass.  The bench's
+    own device part, unchanged: the same C2 batch (shapes, pitch, layout,
+    seed, allocation order), the same settle / warmup / timed loop
+    (device_loop), so rocprofv3 times the same kind of launches the line's
+    HIP events time.  Prints its own event launch_ms as a JSON line."""
+    from bfrs import synth
+    import bfrs
+    rt = Runtime(args)
+    sets = ShardSets(rt, synth.block_shapes(args.segments), args.segment_bytes, args.layout,
+                     args.pitch)
+    fill(rt, sets, 0xB10C)
+    ctx = bfrs.Context(rt.device.index)
+    enc, dec = codec_calls(rt, ctx, sets)
+    stream = rt.torch.cuda.current_stream()
+    sh = stream.cuda_stream
+
+    def step():
+        enc(sh)
+        dec(sh)
+    _, elapsed, launch_ms = device_loop(rt, step, stream, args)
+    print(json.dumps({"launch_ms": launch_ms, "steps": args.steps,
+                      "ms_per_step": elapsed / args.steps * 1e3}), flush=True)
+    return 0
+
+
+def summarize_kernel_trace(csv_path, steps):
+    """The C2 launches of a kernel_trace.csv: gf_apply dispatches at the
+    largest grid (the C2 batch; encode and decode share the grid), in start
+    order; the last 2K of them are the probe's timed region."""
+    import csv
+    import statistics
+    rows = [r for r in csv.DictReader(open(csv_path)) if "gf_apply" in r["Kernel_Name"]]
+    if not rows:
+        raise RuntimeError("no gf_apply dispatches in the kernel trace")
+    grid = max(int(r["Grid_Size_X"]) for r in rows)
+    c2 = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"])
+                for r in rows if int(r["Grid_Size_X"]) == grid)
+    timed = c2[-2 * steps:]
+    if len(timed) < 2 * steps:
+        raise RuntimeError(f"kernel trace holds {len(timed)} C2 launches, expected {2 * steps}")
+    d = [(e - s) / 1e6 for s, e, _ in timed]
+    return {"kernel": timed[-1][2].split("(")[0].replace("void ", ""), "grid": grid,
+            "launches": len(d), "launches_in_trace": len(c2),
+            "mean_ms": round(statistics.mean(d), 4), "median_ms": round(statistics.median(d), 4),
+            "min_ms": round(min(d), 4), "max_ms": round(max(d), 4),
+            "span_ms_per_launch": round((timed[-1][1] - timed[0][0]) / 1e6 / len(d), 4)}
+
+
+def live_kernel_trace(args, profile_dir=None):
+    """roofline.trace measured in this run: one `rocprofv3 --kernel-trace
+    --stats` child pass (the program right after `--`, no shell hop) over the
+    bench's own device loop (trace_probe), started before this process touches
+    the GPU.  Returns the C2 launch summary of the child's timed region, the
+    child's own HIP-event launch time and the --stats top kernels, or
+    {"error": ...}.  With profile_dir, the stats CSV and the summary are kept
+    there (the committed profiles/ evidence of a bench line)."""
+    import csv
+    import glob
+    import shutil
+    import tempfile
+    if shutil.which("rocprofv3") is None or shutil.which("timeout") is None:
+        return {"error": "rocprofv3 not on PATH"}
+    t0 = time.perf_counter()
+    workdir = tempfile.mkdtemp(prefix="bfrs_trace_")
+    out = os.path.join(workdir, "trace")
+    cmd = ["timeout", "-s", "KILL", str(TRACE_PASS_TIMEOUT_S), "rocprofv3", "--kernel-trace",
+           "--stats", "--output-format", "csv", "-d", out, "-o", "run", "--",
+           sys.executable, os.path.abspath(__file__), "--trace-probe",
+           "--segments", str(args.segments), "--segment-bytes", str(args.segment_bytes),
+           "--pitch", str(args.pitch), "--layout", args.layout, "--steps", str(args.steps),
+           "--warmup", str(args.warmup), "--settle-ms", str(args.settle_ms)]
+    env = dict(os.environ, TMPDIR=workdir, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    env.pop("TORCHELASTIC_RUN_ID", None)
+    try:
+        log_path = os.path.join(workdir, "trace.log")
+        with open(log_path, "w") as log:
+            rc = subprocess.call(cmd, stdout=log, stderr=subprocess.STDOUT, env=env, cwd=workdir)
+        if rc != 0:
+            raise RuntimeError(f"rocprofv3 --kernel-trace exited {rc}: "
+                               f"{open(log_path).read()[-300:]}")
+        child = None
+        for line in open(log_path):
+            if line.startswith("{") and '"launch_ms"' in line:
+                child = json.loads(line)
+        traces = glob.glob(os.path.join(out, "**", "*kernel_trace.csv"), recursive=True)
+        stats = glob.glob(os.path.join(out, "**", "*kernel_stats.csv"), recursive=True)
+        if not traces:
+            raise RuntimeError("no kernel_trace.csv in the rocprofv3 output")
+        summ = summarize_kernel_trace(traces[0], args.steps)
+        top = []
+        if stats:
+            for r in list(csv.DictReader(open(stats[0])))[:4]:
+                top.append({"name": r["Name"][:90], "calls": int(r["Calls"]),
+                            "average_ms": round(float(r["AverageNs"]) / 1e6, 4),
+                            "percentage": float(r["Percentage"])})
+        summ.update({
+            "how": "measured in this run: rocprofv3 --kernel-trace --stats child pass (before this "
+                   "process touched the GPU) over the bench's own C2 batch and device loop "
+                   f"(settle, {args.warmup} warmup, {args.steps} timed steps); the last "
+                   f"{2 * args.steps} C2 dispatches = the child's timed region",
+            "child_event_launch_ms": round(child["launch_ms"], 4) if child else None,
+            "stats_top": top, "seconds": round(time.perf_counter() - t0, 1)})
+        if profile_dir:
+            os.makedirs(profile_dir, exist_ok=True)
+            if stats:
+                shutil.copy(stats[0], os.path.join(profile_dir, "trace_kernel_stats.csv"))
+            with open(os.path.join(profile_dir, "trace_c2_launch_summary.json"), "w") as f:
+                json.dump(summ, f, indent=1)
+        return summ
+    except (OSError, RuntimeError, ValueError, KeyError) as e:
+        return {"error": f"{type(e).__name__}: {e}", "seconds": round(time.perf_counter() - t0, 1)}
+    finally:
+        shutil.rmtree(workdir, ignore_errors=True)
 
 
 def pmc_traffic(alg_bytes):
@@ -1259,8 +1587,8 @@ def c5_cpu_baseline(adir, m, damaged, nbytes):
 
 
 # ---------------------------------------------------------------- main
-def main():
-    args = parse()
+def main(argv=None):
+    args = parse(argv)
     if args.workload == "c5":
         line = run_c5(args)
         line.update({"n_gpus": 1, "higher_is_better": True, "vs_baseline": None, "dtype": "u8",
@@ -1268,18 +1596,25 @@ def main():
         print(json.dumps(line), flush=True)
         return 0 if line["blake3_match"] else 1
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        return launch_ranks(args)
+        return launch_ranks(args, argv)
     if args.traffic_probe:
         return traffic_probe(args)
-    live_traffic = None
-    if (args.pmc == "auto" and args.gpus == 1 and not args.stub and not args.strong
-            and int(os.environ.get("WORLD_SIZE", "1")) == 1 and not under_rocprof()):
+    if args.trace_probe:
+        return trace_probe(args)
+    solo = (args.gpus == 1 and not args.stub and not args.strong
+            and int(os.environ.get("WORLD_SIZE", "1")) == 1 and not under_rocprof())
+    live_traffic = live_trace = None
+    if args.pmc == "auto" and solo:
         # before anything in this process touches the GPU: the passes are child processes
         live_traffic = live_pmc_traffic(args)
+        progress("live PMC passes done")
+    if args.trace == "auto" and solo:
+        live_trace = live_kernel_trace(args, args.profile_dir)
+        progress("live kernel-trace pass done")
     rayon_child = None
-    if (args.crate == "auto" and args.gpus == 1 and not args.stub and not args.strong
-            and int(os.environ.get("WORLD_SIZE", "1")) == 1 and not under_rocprof()):
+    if args.crate == "auto" and solo:
         rayon_child = rayon_fresh_process()  # a child process too, before the GPU is touched
+        progress("rayon child done")
     from bfrs import parallel, synth
 
     rt = Runtime(args)
@@ -1315,31 +1650,9 @@ def main():
         encode(sh)
         decode(sh)
 
-    settle_steps = settle(rt, step, args.settle_ms)
-    for _ in range(args.warmup):
-        step()
-    rt.sync()
-    # (the correctness guard runs after the timed region: host work here would
-    # idle the GPU and the timed region would start on ramping clocks again)
-
-    # Timed region: K steps between a barrier + synchronize on both sides.
-    # HIP events on the launch stream bracket the same region: every launch
-    # in it is gf_apply (2 per step), so their mean duration = span / 2K.
-    if not rt.stub:
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    rt.barrier()
-    rt.sync()
-    t0 = time.perf_counter()
-    if not rt.stub:
-        ev0.record(stream)
-    for _ in range(args.steps):
-        step()
-    if not rt.stub:
-        ev1.record(stream)
-    rt.sync()
-    elapsed = time.perf_counter() - t0  # this rank's K steps; the job time is the max over ranks
-    rt.barrier()
-    launch_ms = ev0.elapsed_time(ev1) / (2 * args.steps) if not rt.stub else None
+    settle_steps, elapsed, launch_ms = device_loop(rt, step, stream if not rt.stub else None, args)
+    if rt.rank == 0:
+        progress("timed region done")
     rank_ms = [round(x / args.steps * 1e3, 4) for x in rt.gather_over_ranks(elapsed)]
     elapsed = rt.max_over_ranks(elapsed)
 
@@ -1380,36 +1693,30 @@ def main():
     if args.c4 == "auto" and not args.strong:
         c4 = run_c4_strong(rt, ctx, args, sh)  # collective inside: every rank runs it, no guard
 
+    devices = rt.gather_objects(rt.device_info())  # collective: every rank, before rank 0 goes on
     if rt.rank != 0:
         rt.close()
         return 0 if ok_here else 3
 
     n1 = rt.world == 1
     info = host_info()
+    legs = Legs()
+    real = not rt.stub or args.stub_legs  # --stub-legs: the CPU tests' stand-ins run the legs
+    solo_legs = n1 and real and not args.strong
+    c1 = legs.run("c1_rs13", check_config1, ctx) if real else None
+    b3 = legs.run("blake3_device", blake3_device, ctx, sets) if solo_legs else None
     pcie = crate = cpu = c5 = None
-
-    def guarded(fn, *a):
-        """A side measurement that fails for an environmental reason (disk
-        space for c5's archive, host memory for the pinned buffers) is recorded
-        as its error; the headline line above it still prints."""
-        try:
-            return fn(*a)
-        except (OSError, MemoryError, RuntimeError) as e:  # not AssertionError: a wrong result fails the run
-            return {"error": f"{type(e).__name__}: {e}"}
-
-    c1 = check_config1(ctx) if not rt.stub else None
-    b3 = guarded(blake3_device, ctx, sets) if n1 and not rt.stub and not args.strong else None
-    if n1 and args.pcie == "auto" and not args.strong:
-        pcie = guarded(pcie_inclusive, ctx, sets)
-    if n1 and args.crate == "auto" and not args.strong:
-        crate = guarded(crate_api, ctx, sets)
+    if solo_legs and args.pcie == "auto":
+        pcie = legs.run("pcie_inclusive", pcie_inclusive, ctx, sets)
+    if solo_legs and args.crate == "auto":
+        crate = legs.run("crate_api", crate_api, ctx, sets)
         if rayon_child is not None and "error" not in crate:
             crate["generate_parity_all_blocks_fresh_process"] = rayon_child
-    if n1 and args.cpu_baseline == "auto" and not args.strong:
-        cpu = guarded(cpu_baseline, args, sets, info)
+    if solo_legs and args.cpu_baseline == "auto":
+        cpu = legs.run("cpu_baseline", cpu_baseline, args, sets, info)
     del sets
-    if n1 and args.c5 == "auto" and not args.strong:
-        c5 = guarded(run_c5, args, ctx)
+    if solo_legs and args.c5 == "auto":
+        c5 = legs.run("c5", run_c5, args, ctx)
 
     line = {
         "metric": METRIC,
@@ -1472,30 +1779,57 @@ def main():
                 "ms": round(copy_ms, 4),
                 "what": "torch copy_ of alg_bytes/2 bytes (same read + write bytes as one launch), same box"},
         }
+        trace = live_trace
+        if trace and "error" not in trace:
+            trace["ratio_mean_to_launch_ms"] = round(trace["mean_ms"] / launch_ms, 4)
+            trace["frac_at_trace_mean"] = round(
+                alg_bytes / (trace["mean_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
+        elif trace is None:
+            trace = {"live_pass": "skipped under rocprofv3" if under_rocprof() else "off"}
+        line["roofline"]["trace"] = trace
         line["cpu_baseline"] = cpu
         line["crate_api"] = crate
         line["pcie_inclusive"] = pcie
         line["c5"] = c5
         line["blake3_device"] = b3
+    elif args.stub_legs:
+        line.update({"cpu_baseline": cpu, "crate_api": crate, "pcie_inclusive": pcie, "c5": c5,
+                     "blake3_device": b3})
     line["c4_strong"] = c4
-    line["parity_check"] = {
-        "c1_rs13": c1,
-        "c2_encode": my_check["encode"], "c3_decode": my_check["decode"],
+    line["rank_devices"] = devices
+    line["host_budget"] = host_budget(args, rt.world)
+    golden_c2 = golden_covers("c2_128x32MiB", shapes, S, seed) and not rt.stub
+    golden_c4 = (golden_covers("c4_320x32MiB", synth.block_shapes(args.c4_segments), S_full, 0xB10C)
+                 and not rt.stub)
+    c4_pc = (c4 or {}).get("parity_check") or {}
+    legs_enabled = {
+        "ranks_ok": (True, all(ranks_ok)),
+        "c2_encode": (golden_c2, leg_flag(my_check["encode"], "match")),
+        "c3_decode": (True, leg_flag(my_check["decode"], "match")),
+        "c1_rs13": (real, leg_flag(c1, "match")),
+        "c4_encode": (args.c4 == "auto" and not args.strong and golden_c4,
+                      leg_flag(c4_pc.get("encode"), "match")),
+        "c4_decode": (args.c4 == "auto" and not args.strong, leg_flag(c4_pc.get("decode"), "match")),
+        "c5_blake3": (solo_legs and args.c5 == "auto", leg_flag(c5, "blake3_match")),
+        "c5_repair": (solo_legs and args.c5 == "auto", leg_flag(c5, "repair", "match")),
+        "blake3_c2": (solo_legs and (golden_c2 or args.stub_legs),
+                      leg_flag(b3, "parity_check", "match")),
+        "blake3_device_ran": (solo_legs, isinstance(b3, dict) and "error" not in b3),
+        "pcie_decode": (solo_legs and args.pcie == "auto", leg_flag(pcie, "decode_match")),
+        "crate_recover": (solo_legs and args.crate == "auto", leg_flag(crate, "recover_match")),
+        "cpu_baseline_self_check": (solo_legs and args.cpu_baseline == "auto",
+                                    leg_flag(cpu, "self_check")),
+    }
+    line["parity_check"] = parity_summary(legs_enabled, {
+        "c1_rs13": c1, "c2_encode": my_check["encode"], "c3_decode": my_check["decode"],
         "ranks_ok": [bool(x) for x in ranks_ok],
-        "c4_encode": (c4 or {}).get("parity_check", {}).get("encode"),
-        "c4_decode": (c4 or {}).get("parity_check", {}).get("decode"),
+        "c4_encode": c4_pc.get("encode"), "c4_decode": c4_pc.get("decode"),
         "c5_blake3": None if c5 is None else c5.get("blake3_match"),
         "c5_repair": ((c5 or {}).get("repair") or {}).get("match"),
         "blake3_c2": ((b3 or {}).get("parity_check") or {}).get("match"),
-        "when": "after the timed region, on the buffers the timed launches wrote",
-    }
-    flags = [all(ranks_ok), (my_check["encode"] or {}).get("match"), (c1 or {}).get("match"),
-             ((c4 or {}).get("parity_check", {}).get("encode") or {}).get("match"),
-             ((c4 or {}).get("parity_check", {}).get("decode") or {}).get("match"),
-             None if c5 is None else c5.get("blake3_match"),
-             ((c5 or {}).get("repair") or {}).get("match"),
-             ((b3 or {}).get("parity_check") or {}).get("match")]
-    line["parity_check"]["all_ok"] = not any(f is False for f in flags)
+        "when": "after the timed region, on the buffers the timed launches wrote"})
+    if legs.aborted:
+        line["parity_check"]["aborted"] = legs.aborted
     print(json.dumps(line), flush=True)
     rt.close()
     return 0 if line["parity_check"]["all_ok"] else 1

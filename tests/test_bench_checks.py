@@ -207,3 +207,147 @@ def test_c4_stripes_reassembled_for_the_golden_check(monkeypatch):
     stripes[2][4, 3] ^= 0x10  # block 1, parity 1, in the last rank's stripe
     r = bench.check_c4_stripes_golden(fake_rt(stripes), stripes[0], shapes, S)
     assert not r["match"] and r["mismatched"] == [[1, 1]]
+
+
+# ---------------------------------------------------------------- all_ok
+def _stub_legs(monkeypatch, **override):
+    """Stand-ins for the N=1 legs, each reporting a passing check; `override`
+    replaces some of them."""
+    legs = {
+        "check_config1": lambda ctx: {"match": True},
+        "blake3_device": lambda ctx, sets: {"GBps": 1.0, "parity_check": {"match": True}},
+        "pcie_inclusive": lambda ctx, sets: {"decode_match": True},
+        "crate_api": lambda ctx, sets: {"recover_match": True},
+        "cpu_baseline": lambda args, sets, info: {"self_check": True, "value": 1.0},
+        "run_c5": lambda args, ctx: {"blake3_match": True, "repair": {"match": True}},
+    }
+    legs.update(override)
+    for k, v in legs.items():
+        monkeypatch.setattr(bench, k, v)
+
+
+def _run_stub_main(capsys):
+    import json
+    rc = bench.main(["--stub", "--stub-legs", "--segments", "4", "--segment-bytes", "4096",
+                     "--steps", "2", "--warmup", "1", "--settle-ms", "0", "--c4", "off"])
+    line = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+    return rc, line
+
+
+def test_all_legs_passing_gives_all_ok(monkeypatch, capsys):
+    _stub_legs(monkeypatch)
+    rc, line = _run_stub_main(capsys)
+    pc = line["parity_check"]
+    assert rc == 0 and pc["all_ok"] and pc["failed"] == []
+    for k in ("c1_rs13", "c3_decode", "c5_blake3", "c5_repair", "blake3_c2", "pcie_decode",
+              "crate_recover", "cpu_baseline_self_check"):
+        assert k in pc["expected"], k
+    assert "c2_encode" in pc["not_applicable"]  # no golden covers a 4 x 4 KiB batch
+
+
+def test_c5_error_entry_fails_the_line(monkeypatch, capsys):
+    _stub_legs(monkeypatch, run_c5=lambda args, ctx: {"error": "OSError: [Errno 28] No space"})
+    rc, line = _run_stub_main(capsys)
+    pc = line["parity_check"]
+    assert rc != 0 and not pc["all_ok"]
+    assert set(pc["failed"]) == {"c5_blake3", "c5_repair"}
+
+
+def test_blake3_bfrs_error_fails_the_line_and_skips_later_legs(monkeypatch, capsys):
+    import bfrs
+    ran = []
+
+    def b3(ctx, sets):
+        raise bfrs.BfrsError(-11, "hip: an illegal memory access was encountered")
+
+    def crate(ctx, sets):
+        ran.append("crate")
+        return {"recover_match": True}
+    _stub_legs(monkeypatch, blake3_device=b3, crate_api=crate)
+    rc, line = _run_stub_main(capsys)
+    pc = line["parity_check"]
+    assert rc != 0 and not pc["all_ok"]
+    assert "blake3_c2" in pc["failed"] and "blake3_device_ran" in pc["failed"]
+    assert "BfrsError" in line["blake3_device"]["error"]
+    assert pc["aborted"].startswith("blake3_device raised BfrsError")
+    assert ran == [] and "skipped" in line["crate_api"]["error"]
+
+
+def test_a_check_that_did_not_run_fails(monkeypatch, capsys):
+    # a leg that returns without its check value (None) must not pass
+    _stub_legs(monkeypatch, pcie_inclusive=lambda ctx, sets: {"encode_GiBps": 50.0})
+    rc, line = _run_stub_main(capsys)
+    assert rc != 0 and line["parity_check"]["failed"] == ["pcie_decode"]
+
+
+def test_parity_summary_rules():
+    s = bench.parity_summary({"a": (True, True), "b": (True, None), "c": (False, None),
+                              "d": (True, False)}, {})
+    assert s["failed"] == ["b", "d"] and s["not_applicable"] == ["c"] and not s["all_ok"]
+    assert bench.leg_flag({"error": "x"}, "match") is False
+    assert bench.leg_flag(None, "match") is False
+    assert bench.leg_flag({"r": {"match": True}}, "r", "match") is True
+
+
+# ---------------------------------------------------------------- roofline.trace (VERDICT r3 item 1)
+def _write_trace(path, launches, grid=5242880):
+    import csv
+    with open(path, "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["Kind", "Dispatch_Id", "Kernel_Name", "Start_Timestamp", "End_Timestamp",
+                    "Grid_Size_X"])
+        t = 1000
+        w.writerow(["KERNEL_DISPATCH", 0, "fill_kernel", t, t + 50, 4096])
+        for i, dur_ns in enumerate(launches):
+            t += 10_000
+            w.writerow(["KERNEL_DISPATCH", i + 1,
+                        "void bfrs::gf_apply_unrolled_kernel<true, 6, 4>(bfrs::KernArgs)",
+                        t, t + dur_ns, grid])
+            t += dur_ns
+        w.writerow(["KERNEL_DISPATCH", 999,
+                    "void bfrs::gf_apply_unrolled_kernel<true, 6, 4>(bfrs::KernArgs)", t, t + 7, 256])
+
+
+def test_kernel_trace_summary_takes_the_timed_region(tmp_path):
+    p = str(tmp_path / "run_kernel_trace.csv")
+    # 6 settle/warmup launches at 1.2 ms, then 2K = 4 timed launches at 0.8 ms
+    _write_trace(p, [1_200_000] * 6 + [800_000, 800_000, 790_000, 810_000])
+    s = bench.summarize_kernel_trace(p, steps=2)
+    assert s["launches"] == 4 and s["launches_in_trace"] == 10
+    assert s["mean_ms"] == 0.8 and s["median_ms"] == 0.8 and s["grid"] == 5242880
+    assert "gf_apply_unrolled_kernel" in s["kernel"]
+    with pytest.raises(RuntimeError):
+        bench.summarize_kernel_trace(p, steps=6)
+
+
+def test_live_kernel_trace_child_pass(monkeypatch, tmp_path):
+    import shutil
+    import subprocess as sp
+    seen = {}
+
+    def fake_call(cmd, stdout=None, stderr=None, env=None, cwd=None):
+        seen["cmd"] = cmd
+        assert cmd[:4] == ["timeout", "-s", "KILL", str(bench.TRACE_PASS_TIMEOUT_S)]
+        i = cmd.index("--")
+        assert cmd[i + 1] == sys.executable and "--trace-probe" in cmd  # no shell hop
+        assert "--kernel-trace" in cmd[:i] and "--stats" in cmd[:i] and "--pmc" not in cmd
+        out = os.path.join(cmd[cmd.index("-d") + 1], "host", "1")
+        os.makedirs(out)
+        _write_trace(os.path.join(out, "run_kernel_trace.csv"), [900_000] * 4 + [820_000] * 6)
+        with open(os.path.join(out, "run_kernel_stats.csv"), "w") as f:
+            f.write('"Name","Calls","TotalDurationNs","AverageNs","Percentage","MinNs","MaxNs","StdDev"\n'
+                    '"void bfrs::gf_apply_unrolled_kernel<true, 6, 4>(bfrs::KernArgs)",10,8,820000.0,90.0,1,2,3\n')
+        stdout.write('{"launch_ms": 0.8213, "steps": 3, "ms_per_step": 1.7}\n')
+        return 0
+    monkeypatch.setattr(sp, "call", fake_call)
+    monkeypatch.setattr(shutil, "which", lambda name: "/usr/bin/" + name)
+    args = bench.parse(["--steps", "3", "--warmup", "2"])
+    prof = str(tmp_path / "prof")
+    s = bench.live_kernel_trace(args, prof)
+    assert "error" not in s, s
+    assert s["launches"] == 6 and s["mean_ms"] == 0.82 and s["child_event_launch_ms"] == 0.8213
+    assert s["stats_top"][0]["average_ms"] == 0.82
+    assert os.path.exists(os.path.join(prof, "trace_kernel_stats.csv"))
+    assert os.path.exists(os.path.join(prof, "trace_c2_launch_summary.json"))
+    monkeypatch.setattr(sp, "call", lambda cmd, **kw: 124)
+    assert "exited 124" in bench.live_kernel_trace(args)["error"]

@@ -110,3 +110,56 @@ def test_bench_refuses_mismatched_world(monkeypatch):
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--stub"],
                        capture_output=True, text=True, timeout=120, env=env, cwd=root)
     assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr
+
+
+def test_launcher_fails_fast_when_a_rank_dies():
+    """rank 1 exits 3 right after joining the process
+    group; the launcher must notice, terminate rank 0 (which would otherwise
+    sit in a barrier until the process-group timeout) and return 3 within
+    seconds, naming the rank."""
+    import subprocess
+    import sys
+    import time
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--stub",
+           "--segments", "8", "--segment-bytes", "65536", "--steps", "3", "--warmup", "1",
+           "--settle-ms", "5", "--c4", "off"]
+    env = dict(os.environ, BENCH_FAIL_RANK="1")
+    env.pop("WORLD_SIZE", None)
+    t0 = time.time()
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=150, env=env, cwd=root)
+    took = time.time() - t0
+    assert r.returncode == 3, (r.returncode, r.stderr[-2000:])
+    assert "rank 1 exited 3" in r.stderr
+    assert took < 90, took  # imports dominate; the process-group timeout is 180 s
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+
+
+def test_stub_line_reports_rank_devices_and_host_budget():
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--stub",
+           "--segments", "8", "--segment-bytes", "65536", "--steps", "2", "--warmup", "1",
+           "--settle-ms", "5", "--c4-segments", "40"]
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert [d["rank"] for d in line["rank_devices"]] == [0, 1]
+    hb = line["host_budget"]
+    assert hb["ranks"] == 2 and hb["pinned_bytes_per_rank"] == 0  # the stub pins nothing
+
+
+def test_host_budget_at_eight_ranks():
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    hb = bench.host_budget(bench.parse(["--gpus", "8"]), 8)
+    # c4_strong.pcie_inclusive pins each rank's 4 MiB stripes of config 4's
+    # 320 data + 33 parity + 33 restored shards
+    assert hb["c4_pcie_pinned_bytes_per_rank"] == (320 + 66) * 4 * 2**20
+    assert hb["pinned_bytes_node"] == 8 * hb["pinned_bytes_per_rank"]
+    assert hb["mem_total"] and hb["fits"] in (True, False)
