@@ -506,11 +506,18 @@ def _live_codec(obj):
     return obj.handle
 
 
-def _view(fn, handle, index):
+def _view(fn, owner, index):
+    """A read-only numpy view of a codec object's pinned row.  The view keeps
+    `owner` (the encoder / decoder) alive: the row belongs to the object's
+    codec slot, which goes back to the pool (or is freed) when the object is
+    freed, so a view that outlived its object would read another object's
+    bytes or freed memory."""
     import numpy as np
     p, n = ctypes.c_void_p(), _sz()
-    _check(fn(handle, index, ctypes.byref(p), ctypes.byref(n)))
-    a = np.ctypeslib.as_array((ctypes.c_uint8 * n.value).from_address(p.value))
+    _check(fn(owner._h(), index, ctypes.byref(p), ctypes.byref(n)))
+    buf = (ctypes.c_uint8 * n.value).from_address(p.value)
+    buf._bfrs_owner = owner  # the array's base is buf, buf holds the object
+    a = np.frombuffer(buf, dtype=np.uint8)
     a.flags.writeable = False
     return a
 
@@ -543,7 +550,7 @@ class ReedSolomonEncoder:
     def recovery_view(self, index: int):
         """Recovery shard `index` as a read-only numpy view of the encoder's
         pinned row (valid until the next call on this encoder), no copy."""
-        return _view(lib().bfrs_encoder_recovery, self._h(), index)
+        return _view(lib().bfrs_encoder_recovery, self, index)
 
     def recovery_iter(self):
         for j in range(self.recovery_count):
@@ -585,7 +592,7 @@ class ReedSolomonDecoder:
         """Restored original `index` as a read-only numpy view (valid until the
         next add/decode call), or None if it was not restored."""
         try:
-            return _view(lib().bfrs_decoder_restored_original, self._h(), index)
+            return _view(lib().bfrs_decoder_restored_original, self, index)
         except BfrsError as e:
             if e.code == E_NOT_RESTORED:
                 return None

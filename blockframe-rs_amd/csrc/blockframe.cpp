@@ -54,6 +54,13 @@ class Prefault {
   std::thread th_;
 };
 
+// [a, a + na) and [b, b + nb) share a byte.
+bool overlaps(const uint8_t *a, size_t na, const uint8_t *b, size_t nb) {
+  if (!a || !b || !na || !nb) return false;
+  const auto x = reinterpret_cast<uintptr_t>(a), y = reinterpret_cast<uintptr_t>(b);
+  return x < y + nb && y < x + na;
+}
+
 // RAII holders for the streaming objects.
 struct Enc {
   bfrs_encoder *p = nullptr;
@@ -196,6 +203,16 @@ int bfrs_recover_segment_rs30_3(bfrs_ctx *ctx, const uint8_t *const *segments,
   int rc = bfrs_decoder_new(ctx, 30, 3, shard_size, &dec.p);
   if (rc) return rc;
   if (!out) return set_error(BFRS_E_INVALID_ARGUMENT, "out is NULL");
+  // out is first-touched (zeroed) by a helper thread while the inputs are
+  // still being staged, so it must not share bytes with any of them (the
+  // reference's output is a fresh Vec; include/bfrs.h states the rule)
+  for (size_t i = 0; i < 30; ++i)
+    if (overlaps(out, shard_size, segments[i], segments[i] ? seg_lens[i] : 0))
+      return set_error(BFRS_E_INVALID_ARGUMENT, "recover_segment_rs30_3: out overlaps a segment");
+  for (size_t j = 0; j < 3; ++j)
+    if (overlaps(out, shard_size, block_parity[j], parity_lens[j]))
+      return set_error(BFRS_E_INVALID_ARGUMENT,
+                       "recover_segment_rs30_3: out overlaps a parity shard");
   uint8_t *const outs[1] = {out};
   Prefault pf(outs, 1, shard_size);
   for (size_t i = 0; i < 30; ++i)

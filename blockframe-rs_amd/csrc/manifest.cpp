@@ -136,7 +136,7 @@ struct Parser {
     }
     return true;
   }
-  bool string(std::string *out) {
+  bool string(std::string *out, bool *escaped = nullptr) {
     if (p >= t.size() || t[p] != '"') return fail("expected string");
     ++p;
     while (p < t.size() && t[p] != '"') {
@@ -150,6 +150,7 @@ struct Parser {
         continue;
       }
       if (++p >= t.size()) return fail("bad escape");
+      if (escaped) *escaped = true;
       switch (t[p++]) {
         case '"': out->push_back('"'); break;
         case '\\': out->push_back('\\'); break;
@@ -258,7 +259,9 @@ struct Parser {
       for (;;) {
         ws();
         std::string k;
-        if (!string(&k)) return false;
+        bool esc = false;
+        if (!string(&k, &esc)) return false;
+        if (esc) v->escaped_keys.insert(k);
         ws();
         if (p >= t.size() || t[p] != ':') return fail("expected ':'");
         ++p;
@@ -452,11 +455,16 @@ struct Reader {
     }
     return true;
   }
-  // map key: decimal integer in [lo, hi] (serde_json parses map keys of
-  // integer type from their string form: optional '-', digits)
-  bool key(const std::string &k, int64_t lo, int64_t hi, int64_t *out) {
+  // map key: decimal integer in [lo, hi].  serde_json 1.0.148 (MapKey::
+  // deserialize_number) runs the JSON number grammar over the key's raw bytes
+  // between the quotes, so it refuses a leading zero ("01"), a key written
+  // with an escaped digit, and "-0" (which that grammar yields as the float -0.0, no
+  // integer) -- each of which would otherwise alias another key
+  bool key(const Json &map, const std::string &k, int64_t lo, int64_t hi, int64_t *out) {
     size_t i = !k.empty() && k[0] == '-' ? 1 : 0;
-    bool ok = i < k.size() && k.size() - i <= 19;
+    bool ok = i < k.size() && k.size() - i <= 19 && !map.escaped_keys.count(k);
+    if (ok && k[i] == '0' && k.size() - i > 1) ok = false;  // leading zero
+    if (ok && i == 1 && k == "-0") ok = false;
     uint64_t mag = 0;
     for (; ok && i < k.size(); ++i) {
       if (k[i] < '0' || k[i] > '9') ok = false;
@@ -499,7 +507,7 @@ bool Manifest::from_json(const std::string &text, Manifest *m, std::string *err)
   if (const Json *lv = mt->get("leaves")) {  // HashMap<i32, String>, #[serde(default)]
     if (!r.object(lv, "leaves", false)) return false;
     for (const auto &kv : lv->o) {
-      if (!r.key(kv.first, INT32_MIN, INT32_MAX, &id)) return false;
+      if (!r.key(*lv, kv.first, INT32_MIN, INT32_MAX, &id)) return false;
       if (kv.second.kind != Json::kString) return r.fail("invalid type in 'leaves'");
       m->leaves[id] = kv.second.s;
     }
@@ -507,7 +515,7 @@ bool Manifest::from_json(const std::string &text, Manifest *m, std::string *err)
   if (const Json *sg = mt->get("segments")) {  // HashMap<usize, SegmentHashes>
     if (!r.object(sg, "segments", false)) return false;
     for (const auto &kv : sg->o) {
-      if (!r.key(kv.first, 0, INT64_MAX, &id)) return false;
+      if (!r.key(*sg, kv.first, 0, INT64_MAX, &id)) return false;
       SegmentHashes sh;
       if (!r.object(&kv.second, "segments entry") || !r.str(kv.second, "data", &sh.data) ||
           !r.str_array(kv.second.get("parity"), "parity", &sh.parity))
@@ -518,7 +526,7 @@ bool Manifest::from_json(const std::string &text, Manifest *m, std::string *err)
   if (const Json *bl = mt->get("blocks")) {  // HashMap<usize, BlockHashes>
     if (!r.object(bl, "blocks", false)) return false;
     for (const auto &kv : bl->o) {
-      if (!r.key(kv.first, 0, INT64_MAX, &id)) return false;
+      if (!r.key(*bl, kv.first, 0, INT64_MAX, &id)) return false;
       BlockHashes bh;
       if (!r.object(&kv.second, "blocks entry") ||
           !r.str_array(kv.second.get("segments"), "segments", &bh.segments) ||

@@ -10,6 +10,7 @@
 
 #include <cstdint>
 #include <map>
+#include <set>
 #include <memory>
 #include <string>
 #include <vector>
@@ -26,6 +27,9 @@ struct Json {
   enum Kind { kNull, kBool, kInt, kUInt, kFloat, kString, kArray, kObject } kind = kNull;
   bool b = false;
   bool dup = false;
+  // keys whose raw text held a backslash escape: serde_json reads an integer
+  // map key with the number grammar on the raw bytes, so an escaped digit is no key
+  std::set<std::string> escaped_keys;
   int64_t i = 0;
   uint64_t u = 0;
   std::string s;

@@ -131,8 +131,27 @@ int CodecPool::acquire(size_t nshards, size_t shard_bytes, std::unique_ptr<Codec
   return BFRS_OK;
 }
 
+namespace {
+// Makes `dev` current for a scope and restores the caller's device after it:
+// the last codec object of a pool may be freed on any thread (a GC running
+// in a worker bound to another GPU), which must not be left switched to this
+// pool's device.
+struct DeviceScope {
+  int prev = -1;
+  explicit DeviceScope(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (dev >= 0 && dev != prev) (void)hipSetDevice(dev);
+  }
+  ~DeviceScope() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+}  // namespace
+
 void CodecPool::release(std::unique_ptr<CodecSlot> slot) {
   if (!slot) return;
+  DeviceScope scope(device);  // a slot dropped below is freed on its own device
   (void)hipStreamSynchronize(slot->stream);
   std::unique_ptr<CodecSlot> drop;  // freed after the lock is released
   {
@@ -154,12 +173,12 @@ void CodecPool::release(std::unique_ptr<CodecSlot> slot) {
 }
 
 CodecPool::~CodecPool() {
-  (void)hipSetDevice(device);
+  DeviceScope scope(device);
   free.clear();
 }
 
 Context::~Context() {
-  if (device >= 0) (void)hipSetDevice(device);
+  DeviceScope scope(device);
   if (stream) (void)hipStreamSynchronize(stream);
   codec_pool.reset();  // idle slots go now; live codec objects keep the pool
   staging.reset();  // archive staging arenas (pinned + device)

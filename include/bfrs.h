@@ -224,7 +224,9 @@ int bfrs_recover_segment_rs13(bfrs_ctx *ctx, const uint8_t *const *parity,
                               uint8_t *out, size_t *out_len);
 /* recover_segment_rs30_3 (recovery.rs:118-173): segments[30] with NULL for
  * None, block_parity[3], target index.  out must hold the shard size (its
- * contents are unspecified after an error). */
+ * contents are unspecified after an error) and must not overlap any segment
+ * or parity buffer (BFRS_E_INVALID_ARGUMENT): it is first-touched while they
+ * are staged. */
 int bfrs_recover_segment_rs30_3(bfrs_ctx *ctx, const uint8_t *const *segments,
                                 const size_t *seg_lens, size_t n_slots,
                                 const uint8_t *const *block_parity, const size_t *parity_lens,

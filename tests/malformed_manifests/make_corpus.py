@@ -163,6 +163,14 @@ def corpus():
         "block_keys_shifted": dump(t3).replace('"blocks":{"0":', '"blocks":{"7":'),
         "duplicate_block_key": dump(t3).replace('"blocks":{"0":', '"blocks":{"1":'),
         "duplicate_size_key": v3[:-1] + ',"size":5}',
+        # integer map keys serde_json 1.0.148 refuses: it runs the JSON number
+        # grammar over the raw key bytes; each would alias key 0/1
+        "block_key_leading_zero": dump(t3).replace('"blocks":{"0":', '"blocks":{"01":'),
+        "block_key_minus_zero": dump(t3).replace('"blocks":{"0":', '"blocks":{"-0":'),
+        "block_key_escaped_digit": dump(t3).replace('"blocks":{"0":', '"blocks":{"\\u0030":'),
+        "leaves_key_leading_zero": edit(t3, ["merkle_tree", "leaves"], {"00": H}),
+        "leaves_key_minus_zero": edit(t3, ["merkle_tree", "leaves"], {"-0": H}),
+        "t2_segment_key_leading_zero": dump(t2).replace('"segments":{"0":', '"segments":{"00":'),
         "leaves_gap": edit(t3, ["merkle_tree", "leaves"], {"0": H, "5": H}),
         "leaves_key_text": edit(t3, ["merkle_tree", "leaves"], {"a": H}),
         "t2_segment_count_short": edit(t2, ["size"], 9 * S),

@@ -6,6 +6,7 @@ with committed SHA-256 digests (tests/golden/rs_large.json) and use
 size-independent properties (encode -> erase -> decode round trip, BLAKE3 of
 restored segments against the manifest-style hash of the original).
 """
+import gc
 import hashlib
 import json
 import os
@@ -381,6 +382,23 @@ def test_codec_staging_slots_and_lifetimes(bfrs, oracle, monkeypatch, staging, s
     assert dec.restored_view(17).tobytes() == data[17].tobytes()
     assert dec.restored_original(2) == data[2].tobytes()
     assert dec.restored_view(0) is None
+    # a view outlives the Python name of its object: the encoder
+    # stays alive through the view, so its slot is neither reused by the next
+    # encoder nor freed (BFRS_CODEC_SLOTS=0), and the bytes stay the parity
+    enc = bfrs.ReedSolomonEncoder(c, 30, 3, n)
+    for d in data:
+        enc.add_original_shard(d)
+    view = enc.encode().recovery_view(1)
+    rview = dec.restored_view(29)
+    del enc
+    gc.collect()
+    other = bfrs.ReedSolomonEncoder(c, 30, 3, n)
+    for d in data:
+        other.add_original_shard(255 - d)
+    other.encode()
+    assert view.tobytes() == want[1] and rview.tobytes() == data[29].tobytes()
+    del other, view, rview
+    gc.collect()
     keep = bfrs.ReedSolomonEncoder(c, 8, 3, n)
     c.close()  # objects still alive: freeing them later is safe
     with pytest.raises(bfrs.BfrsError):
@@ -527,6 +545,19 @@ def test_into_forms_match_wrappers(ctx, bfrs, oracle):
     assert bytes(got) == data[11].tobytes()
     with pytest.raises(ValueError):
         bfrs.recover_segment_rs30_3_into(ctx, slots, par, 11, np.empty(n - 64, np.uint8))
+    # an output that shares bytes with an input is refused before anything is
+    # touched (out is first-touched while the inputs are staged)
+    big = np.concatenate([data[0], data[1]])
+    alias_slots = [big[:n], big[n:]] + slots[2:]
+    par_w = [np.array(p) for p in par]
+    for src, out in ((alias_slots, big[n // 2:n // 2 + n]), (slots, par_w[2])):
+        keep = np.array(out)
+        with pytest.raises(bfrs.BfrsError) as e:
+            bfrs.recover_segment_rs30_3_into(ctx, src, par_w, 11, out)
+        assert e.value.code == bfrs.E_INVALID_ARGUMENT and "overlaps" in str(e.value)
+        assert np.array_equal(out, keep)
+    assert bfrs.recover_segment_rs30_3_into(ctx, alias_slots, par_w, 11, got) == n
+    assert bytes(got) == data[11].tobytes()
 
 
 # ---------------------------------------------------------------- BASELINE config sizes

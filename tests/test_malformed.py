@@ -49,6 +49,8 @@ PARSE_ERRORS = {
     "size_overflow_digits", "segment_size_negative", "tier_2_pow_40", "tier_negative",
     "block_key_negative", "missing_time_of_creation", "nul_bytes", "raw_control_chars",
     "lone_high_surrogate", "surrogate_bad_low",
+    "block_key_leading_zero", "block_key_minus_zero", "block_key_escaped_digit",
+    "leaves_key_leading_zero", "leaves_key_minus_zero", "t2_segment_key_leading_zero",
 }
 
 
