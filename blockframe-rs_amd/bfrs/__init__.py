@@ -53,9 +53,10 @@ EXPORTS = (
     "bfrs_decoder_add_original_shard", "bfrs_decoder_add_recovery_shard", "bfrs_decoder_decode",
     "bfrs_decoder_restored_original", "bfrs_decoder_free", "bfrs_encode", "bfrs_decode",
     "bfrs_encode_batch_dev", "bfrs_decode_batch_dev", "bfrs_encode_host_batch",
-    "bfrs_decode_host_batch", "bfrs_generate_parity",
+    "bfrs_decode_host_batch", "bfrs_encode_host_batch_multi", "bfrs_decode_host_batch_multi",
+    "bfrs_generate_parity",
     "bfrs_generate_parity_segmented", "bfrs_recover_segment_rs13", "bfrs_recover_segment_rs30_3",
-    "bfrs_blake3_hex", "bfrs_blake3_batch_dev", "bfrs_blake3_combine", "bfrs_merkle_root_hex", "bfrs_manifest_check", "bfrs_commit", "bfrs_repair", "bfrs_health_check",
+    "bfrs_blake3_hex", "bfrs_blake3_batch_dev", "bfrs_blake3_combine", "bfrs_merkle_root_hex", "bfrs_manifest_check", "bfrs_commit", "bfrs_commit_multi", "bfrs_repair", "bfrs_health_check",
     "bfrs_store_list", "bfrs_store_find", "bfrs_batch_health_check", "bfrs_archive_open",
     "bfrs_archive_size", "bfrs_archive_stat", "bfrs_archive_read", "bfrs_archive_stats_get", "bfrs_archive_close",
 )
@@ -164,6 +165,12 @@ def lib() -> ctypes.CDLL:
                                         _pp], ctypes.c_int),
             "bfrs_decode_host_batch": ([_vp, _sz, ctypes.POINTER(ctypes.c_uint32), _sz, _sz, _pp,
                                         _pp, _pp], ctypes.c_int),
+            "bfrs_encode_host_batch_multi": ([_pp, _sz, _sz, ctypes.POINTER(ctypes.c_uint32), _sz,
+                                              _sz, _pp, _pp], ctypes.c_int),
+            "bfrs_decode_host_batch_multi": ([_pp, _sz, _sz, ctypes.POINTER(ctypes.c_uint32), _sz,
+                                              _sz, _pp, _pp, _pp], ctypes.c_int),
+            "bfrs_commit_multi": ([_pp, _sz, ctypes.c_char_p, ctypes.c_char_p, _sz, ctypes.c_int,
+                                   ctypes.c_char_p, _sz], ctypes.c_int),
             "bfrs_generate_parity": ([_vp, _pp, ctypes.POINTER(_sz), _sz, _sz, _sz, _pp,
                                       ctypes.POINTER(_sz)], ctypes.c_int),
             "bfrs_generate_parity_segmented": ([_vp, _vp, _sz, _pp, ctypes.POINTER(_sz)],
@@ -746,14 +753,60 @@ def manifest_check(text) -> tuple:
     return bool(valid.value), out.value.decode()
 
 
-def commit(ctx: Context, file_path: str, archive_root: str, segment_size: int = 0,
+def commit(ctx, file_path: str, archive_root: str, segment_size: int = 0,
            tier: int = 0) -> str:
     """Chunker::commit (src/chunker/commit.rs:593-613); tier 1/2/3 forces
-    commit_tiny/commit_segmented/commit_blocked.  Returns the archive directory."""
+    commit_tiny/commit_segmented/commit_blocked.  Returns the archive directory.
+    `ctx` may be a list of contexts (one per device): bfrs_commit_multi deals a
+    tier-3 file's blocks over them from this one process (commit.rs:391-393)."""
     out = ctypes.create_string_buffer(4096)
-    _check(lib().bfrs_commit(ctx.handle, os.fsencode(file_path), os.fsencode(archive_root),
-                             segment_size, tier, out, len(out)))
+    if isinstance(ctx, (list, tuple)):
+        pc, kc = _ctx_array(ctx)
+        _check(lib().bfrs_commit_multi(pc, len(ctx), os.fsencode(file_path),
+                                       os.fsencode(archive_root), segment_size, tier, out,
+                                       len(out)))
+    else:
+        _check(lib().bfrs_commit(ctx.handle, os.fsencode(file_path), os.fsencode(archive_root),
+                                 segment_size, tier, out, len(out)))
     return out.value.decode()
+
+
+def _ctx_array(ctxs):
+    for c in ctxs:
+        if not isinstance(c, Context) or not c.handle:
+            raise BfrsError(E_INVALID_ARGUMENT, "a context of the list is closed or not a Context")
+    return _ptr_array([c.handle.value if isinstance(c.handle, ctypes.c_void_p) else c.handle
+                       for c in ctxs])
+
+
+def encode_host_batch_multi(ctxs, original_counts, recovery_count, shard_bytes, originals,
+                            recovery_out) -> None:
+    """bfrs_encode_host_batch_multi: one host-memory batch over several contexts
+    (normally one per device) from this process, context d taking the 64-B
+    column stripe d of every shard (include/bfrs.h)."""
+    Context._check_host_bufs(originals, shard_bytes, False, "encode_host_batch_multi")
+    Context._check_host_bufs(recovery_out, shard_bytes, True, "encode_host_batch_multi")
+    pc, kc = _ctx_array(ctxs)
+    ks = (ctypes.c_uint32 * len(original_counts))(*original_counts)
+    po, ko = _ptr_array([Context._haddr(t) for t in originals])
+    pr, kr = _ptr_array([Context._haddr(t) for t in recovery_out])
+    _check(lib().bfrs_encode_host_batch_multi(pc, len(ctxs), len(original_counts), ks,
+                                              recovery_count, shard_bytes, po, pr))
+
+
+def decode_host_batch_multi(ctxs, original_counts, recovery_count, shard_bytes, originals,
+                            recovery, restored_out) -> None:
+    """bfrs_decode_host_batch_multi (see encode_host_batch_multi)."""
+    Context._check_host_bufs(list(originals) + list(recovery), shard_bytes, False,
+                             "decode_host_batch_multi")
+    Context._check_host_bufs(restored_out, shard_bytes, True, "decode_host_batch_multi")
+    pc, kc = _ctx_array(ctxs)
+    ks = (ctypes.c_uint32 * len(original_counts))(*original_counts)
+    po, ko = _ptr_array([Context._haddr(t) for t in originals])
+    pr, kr = _ptr_array([Context._haddr(t) for t in recovery])
+    pd, kd = _ptr_array([Context._haddr(t) for t in restored_out])
+    _check(lib().bfrs_decode_host_batch_multi(pc, len(ctxs), len(original_counts), ks,
+                                              recovery_count, shard_bytes, po, pr, pd))
 
 
 def repair(ctx: Context, archive_dir: str) -> dict:

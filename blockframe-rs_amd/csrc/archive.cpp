@@ -65,6 +65,7 @@ struct Commit {
   bfrs_ctx *ctx;
   std::string root, name;
   size_t S;
+  std::vector<bfrs_ctx *> ctxs;  // tier 3: blocks dealt over these (ctxs[0] == ctx)
   Mapped m;
   int threads = hw_threads();
 
@@ -339,116 +340,148 @@ int Commit::tier3(std::string *out_dir) {
   const bool cv_hash = pow2_kib(S) && nseg >= 2;
   std::vector<uint8_t> seg_cvs(cv_hash ? nseg * 32 : 0);
   std::vector<std::string> block_roots(nblocks);
-  StagingCache &sc = staging(ctx);
-  std::lock_guard<std::mutex> staging_lock(sc.mu);
-  Arena *arena = sc.a, *pbuf = sc.a + 2;  // pbuf: pinned parity of the block being written
-  for (int i = 0; i < 2; ++i) {
-    int rc = arena[i].reserve(S, kBlockSegments + kParity);
-    if (rc) return rc;
-  }
+  std::vector<BlockHashes> block_hashes(nblocks);
   auto geom = [&](size_t b, size_t *s0, size_t *k, size_t *shard) {
     *s0 = b * kBlockSegments;
     *k = std::min(kBlockSegments, nseg - *s0);
     *shard = std::min(S, m.n - *s0 * S);  // the block's first segment is its longest
   };
-  auto fill = [&](size_t b) {
-    size_t s0, k, shard;
-    geom(b, &s0, &k, &shard);
-    Arena &a = arena[b % 2];
-    parallel_for(k, threads, [&](size_t s) {
-      const size_t len = std::min(S, m.n - (s0 + s) * S);
-      std::memcpy(a.hs(s), m.p + (s0 + s) * S, len);
-      if (len < shard) std::memset(a.hs(s) + len, 0, shard - len);
-    });
-  };
-  for (int i = 0; i < 2; ++i) {
-    int rc = pbuf[i].reserve(S, kParity);
-    if (rc) return rc;
-  }
   std::atomic<bool> write_ok{true};
-  auto write_block = [&](size_t b) {  // segments from the mmap, parity from pbuf
-    size_t s0, k, shard;
-    geom(b, &s0, &k, &shard);
-    const Arena &pb = pbuf[b % 2];
-    parallel_for(k + kParity, threads, [&](size_t i) {
-      bool ok;
-      if (i < k)
-        ok = write_file(t3_seg(dir, b, i), m.p + (s0 + i) * S, std::min(S, m.n - (s0 + i) * S));
-      else
-        ok = write_file(t3_par(dir, b, i - k), pb.hs(i - k), shard);
-      if (!ok) write_ok = false;
-    });
+  // The pipeline of one context over its blocks `mine` (in file order): its
+  // own staging arenas, stream, filler and writers; `thr` host threads for
+  // the copies.  Every result lands in a per-block slot (seg_cvs ranges,
+  // block_roots, block_hashes), so several pipelines run side by side.
+  auto pipeline = [&](bfrs_ctx *cx, const std::vector<size_t> &mine, int thr) -> int {
+    Context &c = cx->impl;
+    if (hipSetDevice(c.device) != hipSuccess) return set_error(BFRS_E_HIP, "commit: hipSetDevice");
+    StagingCache &sc = staging(cx);
+    std::lock_guard<std::mutex> staging_lock(sc.mu);
+    Arena *arena = sc.a, *pbuf = sc.a + 2;  // pbuf: pinned parity of the block being written
+    for (int i = 0; i < 2; ++i) {
+      int rc = arena[i].reserve(S, kBlockSegments + kParity);
+      if (rc) return rc;
+      if ((rc = pbuf[i].reserve(S, kParity))) return rc;
+    }
+    auto fill = [&](size_t i) {
+      size_t s0, k, shard;
+      geom(mine[i], &s0, &k, &shard);
+      Arena &a = arena[i % 2];
+      parallel_for(k, thr, [&](size_t s) {
+        const size_t len = std::min(S, m.n - (s0 + s) * S);
+        std::memcpy(a.hs(s), m.p + (s0 + s) * S, len);
+        if (len < shard) std::memset(a.hs(s) + len, 0, shard - len);
+      });
+    };
+    auto write_block = [&](size_t i) {  // segments from the mmap, parity from pbuf
+      const size_t b = mine[i];
+      size_t s0, k, shard;
+      geom(b, &s0, &k, &shard);
+      const Arena &pb = pbuf[i % 2];
+      parallel_for(k + kParity, thr, [&](size_t j) {
+        bool ok;
+        if (j < k)
+          ok = write_file(t3_seg(dir, b, j), m.p + (s0 + j) * S, std::min(S, m.n - (s0 + j) * S));
+        else
+          ok = write_file(t3_par(dir, b, j - k), pb.hs(j - k), shard);
+        if (!ok) write_ok = false;
+      });
+    };
+    // one block on the GPU: H2D, encode, hashes, D2H parity into pbuf[i % 2].
+    // `wait_writer` is the writer of block i - 2, which still owns pbuf[i % 2]
+    auto gpu_block = [&](size_t i, BgTask &wait_writer) -> int {
+      const size_t b = mine[i];
+      size_t s0, k, shard;
+      geom(b, &s0, &k, &shard);
+      Arena &a = arena[i % 2];
+      if (hipMemcpyAsync(a.d, a.h, a.slot * k, hipMemcpyHostToDevice, c.stream) != hipSuccess)
+        return set_error(BFRS_E_HIP, "commit: H2D copy failed");
+      std::vector<const uint8_t *> orig(k);
+      std::vector<uint8_t *> rec(kParity);
+      for (size_t s = 0; s < k; ++s) orig[s] = a.ds(s);
+      for (size_t p = 0; p < kParity; ++p) rec[p] = a.ds(k + p);
+      const uint32_t kk = uint32_t(k);
+      int rc = encode_batch_on(cx, 1, &kk, kParity, shard, orig.data(), rec.data(), c.stream);
+      if (rc) return rc;
+      std::vector<const uint8_t *> msgs;
+      std::vector<size_t> lens;
+      for (size_t s = 0; s < k; ++s) {
+        msgs.push_back(a.ds(s));
+        lens.push_back(std::min(S, m.n - (s0 + s) * S));
+      }
+      for (size_t p = 0; p < kParity; ++p) {
+        msgs.push_back(a.ds(k + p));
+        lens.push_back(shard);
+      }
+      std::vector<std::string> hex;
+      if ((rc = gpu_hash_hex(cx, msgs, lens, &hex))) return rc;
+      if (cv_hash) {  // the segments as nodes of the file's BLAKE3 tree
+        std::vector<const uint8_t *> sm(msgs.begin(), msgs.begin() + k);
+        std::vector<size_t> sl(lens.begin(), lens.begin() + k);
+        std::vector<uint64_t> offs(k);
+        for (size_t s = 0; s < k; ++s) offs[s] = uint64_t(s0 + s) * (S / 1024);
+        std::vector<std::string> unused;
+        std::vector<uint8_t> cvs;
+        if ((rc = gpu_hash_hex(cx, sm, sl, &unused, offs.data(), &cvs))) return rc;
+        std::memcpy(seg_cvs.data() + s0 * 32, cvs.data(), k * 32);
+      }
+      wait_writer.join();
+      Arena &pb = pbuf[i % 2];
+      for (size_t p = 0; p < kParity; ++p)
+        if (hipMemcpyAsync(pb.hs(p), a.ds(k + p), shard, hipMemcpyDeviceToHost, c.stream) !=
+            hipSuccess)
+          return set_error(BFRS_E_HIP, "commit: D2H copy failed");
+      if (hipStreamSynchronize(c.stream) != hipSuccess)
+        return set_error(BFRS_E_HIP, "commit: stream synchronize failed");
+      BlockHashes &bh = block_hashes[b];
+      bh.segments.assign(hex.begin(), hex.begin() + k);
+      bh.parity.assign(hex.begin() + k, hex.end());
+      std::vector<std::string> leaves = bh.segments;
+      leaves.insert(leaves.end(), bh.parity.begin(), bh.parity.end());
+      block_roots[b] = merkle_root_hex(leaves);
+      return BFRS_OK;
+    };
+    int rc = BFRS_OK;
+    if (mine.empty()) return rc;
+    fill(0);
+    BgTask writer[2];  // after the lambdas: joined first on every exit path
+    for (size_t i = 0; i < mine.size() && rc == BFRS_OK; ++i) {
+      // arena[(i+1) % 2] was last used by block i-1's GPU work, which is done
+      BgTask filler;
+      if (i + 1 < mine.size()) filler.start([&fill, i] { fill(i + 1); });
+      rc = gpu_block(i, writer[i % 2]);
+      filler.join();
+      if (rc == BFRS_OK) writer[i % 2].start([&write_block, i] { write_block(i); });
+    }
+    for (auto &w : writer) w.join();
+    return rc;
   };
-  // one block on the GPU: H2D, encode, hashes, D2H parity into pbuf[b % 2]
-  // `wait_writer` is the writer of block b - 2, which still owns pbuf[b % 2]
-  auto gpu_block = [&](size_t b, BgTask &wait_writer) -> int {
-    size_t s0, k, shard;
-    geom(b, &s0, &k, &shard);
-    Arena &a = arena[b % 2];
-    Context &c = ctx->impl;
-    if (hipSetDevice(c.device) != hipSuccess ||
-        hipMemcpyAsync(a.d, a.h, a.slot * k, hipMemcpyHostToDevice, c.stream) != hipSuccess)
-      return set_error(BFRS_E_HIP, "commit: H2D copy failed");
-    std::vector<const uint8_t *> orig(k);
-    std::vector<uint8_t *> rec(kParity);
-    for (size_t s = 0; s < k; ++s) orig[s] = a.ds(s);
-    for (size_t p = 0; p < kParity; ++p) rec[p] = a.ds(k + p);
-    const uint32_t kk = uint32_t(k);
-    int rc = encode_batch_on(ctx, 1, &kk, kParity, shard, orig.data(), rec.data(), c.stream);
-    if (rc) return rc;
-    std::vector<const uint8_t *> msgs;
-    std::vector<size_t> lens;
-    for (size_t s = 0; s < k; ++s) {
-      msgs.push_back(a.ds(s));
-      lens.push_back(std::min(S, m.n - (s0 + s) * S));
+  // blocks dealt round-robin over the contexts (block b to context b % n)
+  const size_t n = std::max<size_t>(1, std::min(ctxs.size(), nblocks));
+  std::vector<std::vector<size_t>> mine(n);
+  for (size_t b = 0; b < nblocks; ++b) mine[b % n].push_back(b);
+  const int thr = std::max(2, threads / int(n));
+  std::vector<int> rcs(n, BFRS_OK);
+  std::vector<std::string> errs(n);
+  auto run = [&](size_t d) {
+    try {
+      rcs[d] = pipeline(ctxs[d], mine[d], n == 1 ? threads : thr);
+    } catch (const std::bad_alloc &) {
+      rcs[d] = set_error(BFRS_E_NOMEM, "host memory allocation failed");
+    } catch (const std::exception &e) {
+      rcs[d] = set_error(BFRS_E_WRAPPER, std::string("internal error: ") + e.what());
     }
-    for (size_t p = 0; p < kParity; ++p) {
-      msgs.push_back(a.ds(k + p));
-      lens.push_back(shard);
-    }
-    std::vector<std::string> hex;
-    if ((rc = gpu_hash_hex(ctx, msgs, lens, &hex))) return rc;
-    if (cv_hash) {  // the segments as nodes of the file's BLAKE3 tree
-      std::vector<const uint8_t *> sm(msgs.begin(), msgs.begin() + k);
-      std::vector<size_t> sl(lens.begin(), lens.begin() + k);
-      std::vector<uint64_t> offs(k);
-      for (size_t s = 0; s < k; ++s) offs[s] = uint64_t(s0 + s) * (S / 1024);
-      std::vector<std::string> unused;
-      std::vector<uint8_t> cvs;
-      if ((rc = gpu_hash_hex(ctx, sm, sl, &unused, offs.data(), &cvs))) return rc;
-      std::memcpy(seg_cvs.data() + s0 * 32, cvs.data(), k * 32);
-    }
-    wait_writer.join();
-    Arena &pb = pbuf[b % 2];
-    for (size_t p = 0; p < kParity; ++p)
-      if (hipMemcpyAsync(pb.hs(p), a.ds(k + p), shard, hipMemcpyDeviceToHost, c.stream) !=
-          hipSuccess)
-        return set_error(BFRS_E_HIP, "commit: D2H copy failed");
-    if (hipStreamSynchronize(c.stream) != hipSuccess)
-      return set_error(BFRS_E_HIP, "commit: stream synchronize failed");
-    BlockHashes bh;
-    bh.segments.assign(hex.begin(), hex.begin() + k);
-    bh.parity.assign(hex.begin() + k, hex.end());
-    std::vector<std::string> leaves = bh.segments;
-    leaves.insert(leaves.end(), bh.parity.begin(), bh.parity.end());
-    block_roots[b] = merkle_root_hex(leaves);
-    mf.blocks[int64_t(b)] = bh;
-    return BFRS_OK;
+    if (rcs[d]) errs[d] = bfrs_last_error();  // thread-local: carried back below
   };
-  int rc = BFRS_OK;
-  fill(0);
-  BgTask writer[2];  // after the lambdas: joined first on every exit path
-  for (size_t b = 0; b < nblocks && rc == BFRS_OK; ++b) {
-    // arena[(b+1) % 2] was last used by block b-1's GPU work, which is done
-    BgTask filler;
-    if (b + 1 < nblocks) filler.start([&fill, b] { fill(b + 1); });
-    rc = gpu_block(b, writer[b % 2]);
-    filler.join();
-    if (rc == BFRS_OK) writer[b % 2].start([&write_block, b] { write_block(b); });
+  {
+    std::vector<BgTask> others(n - 1);  // joined on every exit path
+    for (size_t d = 1; d < n; ++d) others[d - 1].start([&run, d] { run(d); });
+    run(0);
+    for (auto &t : others) t.join();
   }
-  for (auto &w : writer) w.join();
-  if (rc) return rc;
+  for (size_t d = 0; d < n; ++d)
+    if (rcs[d]) return set_error(rcs[d], n == 1 ? errs[d] : "context " + std::to_string(d) + ": " + errs[d]);
   if (!write_ok) return io_error("write tier-3 shards");
+  for (size_t b = 0; b < nblocks; ++b) mf.blocks[int64_t(b)] = std::move(block_hashes[b]);
   mf.root = merkle_root_hex(block_roots);
   const std::string file_hash = cv_hash ? blake3_combine_cvs_hex(seg_cvs.data(), nseg)
                                         : nseg == 1 ? mf.blocks[0].segments[0]
@@ -829,12 +862,18 @@ int bfrs_manifest_check(const char *text, size_t len, int *valid, char *canonica
   BFRS_API_END
 }
 
-int bfrs_commit(bfrs_ctx *ctx, const char *file_path, const char *archive_root,
-                size_t segment_size, int tier, char *out_dir, size_t out_cap) {
-  BFRS_API_BEGIN
-  if (!ctx || !file_path || !archive_root)
+}  // extern "C"
+
+namespace {
+int commit_impl(const std::vector<bfrs_ctx *> &ctxs, const char *file_path,
+                const char *archive_root, size_t segment_size, int tier, char *out_dir,
+                size_t out_cap) {
+  if (ctxs.empty() || !file_path || !archive_root)
     return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_commit: NULL argument");
-  Commit c{ctx, archive_root, basename_of(file_path), segment_size ? segment_size : kDefaultSegment};
+  for (bfrs_ctx *c : ctxs)
+    if (!c) return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_commit: NULL context");
+  Commit c{ctxs[0], archive_root, basename_of(file_path),
+           segment_size ? segment_size : kDefaultSegment, ctxs};
   c.m.fd = open(file_path, O_RDONLY);
   if (c.m.fd < 0) return io_error(std::string("open ") + file_path);
   struct stat st;
@@ -860,6 +899,25 @@ int bfrs_commit(bfrs_ctx *ctx, const char *file_path, const char *archive_root,
     out_dir[out_cap - 1] = 0;
   }
   return BFRS_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int bfrs_commit(bfrs_ctx *ctx, const char *file_path, const char *archive_root,
+                size_t segment_size, int tier, char *out_dir, size_t out_cap) {
+  BFRS_API_BEGIN
+  return commit_impl({ctx}, file_path, archive_root, segment_size, tier, out_dir, out_cap);
+  BFRS_API_END
+}
+
+int bfrs_commit_multi(bfrs_ctx *const *ctxs, size_t n_ctx, const char *file_path,
+                      const char *archive_root, size_t segment_size, int tier, char *out_dir,
+                      size_t out_cap) {
+  BFRS_API_BEGIN
+  if (!ctxs || n_ctx == 0) return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_commit_multi: no contexts");
+  return commit_impl(std::vector<bfrs_ctx *>(ctxs, ctxs + n_ctx), file_path, archive_root,
+                     segment_size, tier, out_dir, out_cap);
   BFRS_API_END
 }
 

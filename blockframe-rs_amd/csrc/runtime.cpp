@@ -681,12 +681,10 @@ int decode_batch_on(bfrs_ctx *ctx, size_t nblocks, const uint32_t *ks, size_t m,
 
 }  // namespace bfrs
 
-extern "C" {
-
 // ---- host-memory API: pipelined through HBM ----------------------------------
-static int check_host_batch(bfrs_ctx *ctx, size_t nblocks, const uint32_t *ks, size_t m,
-                            size_t shard_bytes, bool decode, const uint8_t *const *orig,
-                            const uint8_t *const *rec, uint8_t *const *out) {
+int bfrs::check_host_batch(bfrs_ctx *ctx, size_t nblocks, const uint32_t *ks, size_t m,
+                           size_t shard_bytes, bool decode, const uint8_t *const *orig,
+                           const uint8_t *const *rec, uint8_t *const *out) {
   if (!ctx || (nblocks && (!ks || !orig || !out || (decode && !rec))))
     return set_error(BFRS_E_INVALID_ARGUMENT, "host batch: NULL argument");
   size_t oi = 0;
@@ -716,6 +714,8 @@ static int check_host_batch(bfrs_ctx *ctx, size_t nblocks, const uint32_t *ks, s
   }
   return BFRS_OK;
 }
+
+extern "C" {
 
 int bfrs_encode_host_batch(bfrs_ctx *ctx, size_t nblocks, const uint32_t *ks, size_t m,
                            size_t shard_bytes, const uint8_t *const *orig,

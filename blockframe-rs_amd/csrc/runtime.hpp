@@ -209,6 +209,10 @@ struct bfrs_ctx {
 };
 
 namespace bfrs {
+// Pointer and shape checks of the host-memory batch API (one block list).
+int check_host_batch(bfrs_ctx *ctx, size_t nblocks, const uint32_t *ks, size_t m,
+                     size_t shard_bytes, bool decode, const uint8_t *const *orig,
+                     const uint8_t *const *rec, uint8_t *const *out);
 // Wrapper fast paths (blockframe.cpp): the owned Vec outputs of
 // generate_parity / recover_segment_rs30_3 (generate.rs:95-96,
 // recovery.rs:166-170) are filled by D2H straight into the caller's buffers.

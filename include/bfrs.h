@@ -187,6 +187,24 @@ int bfrs_decode_host_batch(bfrs_ctx *ctx, size_t nblocks, const uint32_t *origin
                            const uint8_t *const *originals, const uint8_t *const *recovery,
                            uint8_t *const *restored_out);
 
+/* The same host-memory batch spread over several contexts from ONE process
+ * (BlockFrame is one process: rayon over blocks, src/chunker/commit.rs:391-393;
+ * BASELINE configs[3], a 10 GiB archive over 1/2/4/8 GPUs).  ctxs[d] is
+ * normally one context per device; context d streams the 64-byte-aligned
+ * column stripe d of every shard (the tail chunk in the last stripe) through
+ * its own device on a host thread of its own, so any block list balances
+ * exactly and no bytes move between devices (the code acts per 64-byte
+ * chunk).  Same arguments and results as bfrs_encode_host_batch /
+ * bfrs_decode_host_batch; an error names the stripe and device. */
+int bfrs_encode_host_batch_multi(bfrs_ctx *const *ctxs, size_t n_ctx, size_t nblocks,
+                                 const uint32_t *original_counts, size_t recovery_count,
+                                 size_t shard_bytes, const uint8_t *const *originals,
+                                 uint8_t *const *recovery_out);
+int bfrs_decode_host_batch_multi(bfrs_ctx *const *ctxs, size_t n_ctx, size_t nblocks,
+                                 const uint32_t *original_counts, size_t recovery_count,
+                                 size_t shard_bytes, const uint8_t *const *originals,
+                                 const uint8_t *const *recovery, uint8_t *const *restored_out);
+
 /* ---- device-resident batch API (pointers are device memory) ----------- */
 /* Encodes nblocks independent RS blocks in one launch.  Block b has
  * original_counts[b] originals, all blocks share recovery_count and
@@ -274,6 +292,16 @@ int bfrs_manifest_check(const char *text, size_t len, int *valid, char *canonica
  * directory is written to out_dir (NUL-terminated, truncated to out_cap). */
 int bfrs_commit(bfrs_ctx *ctx, const char *file_path, const char *archive_root,
                 size_t segment_size, int tier, char *out_dir, size_t out_cap);
+/* bfrs_commit over several contexts (normally one per device) from one
+ * process: a tier-3 file's blocks are dealt round-robin (block b to context
+ * b % n_ctx, rayon's independent blocks, commit.rs:391-393), each context
+ * runs the commit pipeline of its blocks on a host thread of its own (fill,
+ * H2D, encode, device BLAKE3, D2H, file writes).  The archive -- every file
+ * and the manifest except time_of_creation -- is byte-identical to
+ * bfrs_commit's.  Tiers 1/2 (one RS(1,3) stream, <= 1 GB) run on ctxs[0]. */
+int bfrs_commit_multi(bfrs_ctx *const *ctxs, size_t n_ctx, const char *file_path,
+                      const char *archive_root, size_t segment_size, int tier, char *out_dir,
+                      size_t out_cap);
 
 typedef struct {
   uint64_t blocks_checked;      /* tier 3: blocks; tiers 1/2: segments */
