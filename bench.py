@@ -1177,6 +1177,73 @@ def pcie_inclusive(ctx, sets, steps=2, rt=None, job_bytes=None):
     }
 
 
+def c4_one_process(args, ctx, world, one_device=False, steps=2):
+    """c4_strong.pcie_inclusive_one_process: BASELINE configs[3] (320 x 32 MiB)
+    from pinned host memory through bfrs_encode_host_batch_multi /
+    bfrs_decode_host_batch_multi, ONE process driving one context per GPU
+    (BlockFrame is one process, commit.rs:391-393), beside the one-process-
+    per-GPU figure (c4_strong.pcie_inclusive).  Rank 0 runs it after the
+    other ranks have left their devices.  Parity checked against the golden
+    digests, restored shards against the originals."""
+    import torch
+    import bfrs
+    from bfrs import synth
+    S = args.segment_bytes
+    shapes = synth.block_shapes(args.c4_segments)
+    nseg, nb = sum(shapes), len(shapes)
+    host = torch.empty(nseg, S, dtype=torch.uint8, pin_memory=True)
+    row = torch.empty(S + 8, dtype=torch.uint8, device=f"cuda:{ctx.device}")
+    n8 = (S + 7) // 8 * 8
+    for s in range(nseg):
+        synth.fill_segment_torch(row[:n8], 0xB10C, s)
+        host[s].copy_(row[:S])
+    del row
+    par = torch.empty(3 * nb, S, dtype=torch.uint8, pin_memory=True)
+    rest = torch.empty(3 * nb, S, dtype=torch.uint8, pin_memory=True)
+    import numpy as np
+    enc_in = [host[s] for s in range(nseg)]
+    enc_out = [par[i] for i in range(3 * nb)]
+    dec_in, dec_out, want, seg = [], [], [], 0
+    for b, k in enumerate(shapes):
+        er = sorted(np.random.default_rng(0xDEC0DE + b).choice(k, min(3, k), replace=False).tolist())
+        for i in range(k):
+            dec_in.append(None if i in er else host[seg + i])
+            dec_out.append(rest[3 * b + er.index(i)] if i in er else None)
+            if i in er:
+                want.append((3 * b + er.index(i), seg + i))
+        seg += k
+    extra = [bfrs.Context(0 if one_device else d) for d in range(1, world)]
+    ctxs = [ctx] + extra
+    try:
+        def clock(call):
+            call()  # warm: pins nothing new, grows each context's slab buffers
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                call()
+            return (time.perf_counter() - t0) / steps
+        t_enc = clock(lambda: bfrs.encode_host_batch_multi(ctxs, shapes, 3, S, enc_in, enc_out))
+        t_dec = clock(lambda: bfrs.decode_host_batch_multi(ctxs, shapes, 3, S, dec_in, enc_out,
+                                                           dec_out))
+    finally:
+        for c in extra:
+            c.close()
+    golden = check_parity_golden(par, shapes, S, 0xB10C, "c4_320x32MiB")
+    restored_ok = all(torch.equal(rest[r], host[s]) for r, s in want)
+    gib = nseg * S / 2**30
+    del host, par, rest
+    return {
+        "devices": len(ctxs), "contexts_on_device_0": one_device or world == 1,
+        "encode_GiBps": round(gib / t_enc, 2), "decode_GiBps": round(gib / t_dec, 2),
+        "encode_ms": round(t_enc * 1e3, 2), "decode_ms": round(t_dec * 1e3, 2),
+        "parity_golden": golden, "restored_match": restored_ok,
+        "match": bool(restored_ok and (golden or {}).get("match") is not False
+                      and (golden is not None or S != 32 << 20 or args.c4_segments != 320)),
+        "what": "one process, one context per GPU: bfrs_*_host_batch_multi over pinned host "
+                "buffers (context d = column stripe d of every shard); whole-job GiB/s, mean "
+                f"of {steps} timed calls after a warm call",
+    }
+
+
 PMC_PASS_TIMEOUT_S = 60
 
 
@@ -1271,6 +1338,52 @@ def live_pmc_traffic(args):
 TRACE_PASS_TIMEOUT_S = 150
 
 
+def same_process_trace(rt, step, stream, steps, profile_dir=None):
+    """A kernel trace of THIS process: K more steps on the timed region's own
+    buffers (same process, same HBM placement, right after the timed region),
+    recorded by the profiler built into torch (kineto over the ROCm tracer:
+    GPU start/end timestamps of every dispatch, ours included, since libbfrs
+    runs on torch's HIP runtime).  Returns the gf_apply C2 launches' mean /
+    median and the same loop's own HIP-event launch time, or {"error": ...}.
+    The rocprofv3 child pass (live_kernel_trace) runs in another process,
+    whose buffers may land in the other HBM placement mode."""
+    import statistics
+    torch = rt.torch
+    try:
+        from torch.autograd import DeviceType
+        from torch.profiler import ProfilerActivity, profile
+        if ProfilerActivity.CUDA not in torch.profiler.supported_activities():
+            return {"error": "torch profiler has no GPU activity on this build"}
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        rt.sync()
+        with profile(activities=[ProfilerActivity.CUDA]) as prof:
+            ev0.record(stream)
+            for _ in range(steps):
+                step()
+            ev1.record(stream)
+            rt.sync()
+        kern = [(e.start_ns(), e.duration_ns(), e.name())
+                for e in prof.profiler.kineto_results.events()
+                if e.device_type() == DeviceType.CUDA and "gf_apply" in e.name()]
+        if len(kern) < 2 * steps:
+            return {"error": f"trace holds {len(kern)} gf_apply dispatches, expected {2 * steps}"}
+        d = [x[1] / 1e6 for x in sorted(kern)[-2 * steps:]]
+        out = {"how": "torch.profiler (kineto, ROCm tracer) over K more steps on the timed "
+                      "region's own buffers, right after it, in the bench process itself",
+               "kernel": kern[-1][2].rsplit("(", 1)[0].replace("void ", ""),
+               "launches": len(d), "mean_ms": round(statistics.mean(d), 4),
+               "median_ms": round(statistics.median(d), 4), "min_ms": round(min(d), 4),
+               "max_ms": round(max(d), 4),
+               "loop_event_launch_ms": round(ev0.elapsed_time(ev1) / (2 * steps), 4)}
+        if profile_dir:
+            os.makedirs(profile_dir, exist_ok=True)
+            with open(os.path.join(profile_dir, "same_process_trace.json"), "w") as f:
+                json.dump(dict(out, durations_ms=[round(x, 5) for x in d]), f, indent=1)
+        return out
+    except Exception as e:  # noqa: BLE001 - a missing tracer is reported, never fatal
+        return {"error": f"{type(e).__name__}: {e}"}
+
+
 def trace_probe(args):
     """--trace-probe: the child of the live kernel-trace pass.  The bench's
     own device part, unchanged: the same C2 batch (shapes, pitch, layout,
@@ -1313,7 +1426,7 @@ def summarize_kernel_trace(csv_path, steps):
     if len(timed) < 2 * steps:
         raise RuntimeError(f"kernel trace holds {len(timed)} C2 launches, expected {2 * steps}")
     d = [(e - s) / 1e6 for s, e, _ in timed]
-    return {"kernel": timed[-1][2].split("(")[0].replace("void ", ""), "grid": grid,
+    return {"kernel": timed[-1][2].rsplit("(", 1)[0].replace("void ", ""), "grid": grid,
             "launches": len(d), "launches_in_trace": len(c2),
             "mean_ms": round(statistics.mean(d), 4), "median_ms": round(statistics.median(d), 4),
             "min_ms": round(min(d), 4), "max_ms": round(max(d), 4),
@@ -1657,6 +1770,9 @@ def main(argv=None):
     elapsed = rt.max_over_ranks(elapsed)
 
     enc_ms = dec_ms = copy_ms = None
+    sp_trace = None
+    if not rt.stub and args.trace == "auto" and not under_rocprof():
+        sp_trace = same_process_trace(rt, step, stream, args.steps, args.profile_dir)
     if not rt.stub:
         # Per-direction rates: short back-to-back loops after the timed region.
         def per_launch(fn, n=max(3, args.steps // 2)):
@@ -1715,6 +1831,11 @@ def main(argv=None):
     if solo_legs and args.cpu_baseline == "auto":
         cpu = legs.run("cpu_baseline", cpu_baseline, args, sets, info)
     del sets
+    c4_1p = None
+    if real and args.c4 == "auto" and args.pcie == "auto" and not args.strong:
+        c4_1p = legs.run("c4_one_process", c4_one_process, args, ctx, rt.world, args.one_device)
+        if c4 is not None:
+            c4["pcie_inclusive_one_process"] = c4_1p
     if solo_legs and args.c5 == "auto":
         c5 = legs.run("c5", run_c5, args, ctx)
 
@@ -1787,6 +1908,11 @@ def main(argv=None):
         elif trace is None:
             trace = {"live_pass": "skipped under rocprofv3" if under_rocprof() else "off"}
         line["roofline"]["trace"] = trace
+        if sp_trace and "error" not in sp_trace:
+            sp_trace["ratio_mean_to_launch_ms"] = round(sp_trace["mean_ms"] / launch_ms, 4)
+            sp_trace["frac_at_trace_mean"] = round(
+                alg_bytes / (sp_trace["mean_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
+        line["roofline"]["trace_same_process"] = sp_trace
         line["cpu_baseline"] = cpu
         line["crate_api"] = crate
         line["pcie_inclusive"] = pcie
@@ -1810,6 +1936,8 @@ def main(argv=None):
         "c4_encode": (args.c4 == "auto" and not args.strong and golden_c4,
                       leg_flag(c4_pc.get("encode"), "match")),
         "c4_decode": (args.c4 == "auto" and not args.strong, leg_flag(c4_pc.get("decode"), "match")),
+        "c4_one_process": (real and args.c4 == "auto" and args.pcie == "auto" and not args.strong,
+                           leg_flag(c4_1p, "match")),
         "c5_blake3": (solo_legs and args.c5 == "auto", leg_flag(c5, "blake3_match")),
         "c5_repair": (solo_legs and args.c5 == "auto", leg_flag(c5, "repair", "match")),
         "blake3_c2": (solo_legs and (golden_c2 or args.stub_legs),

@@ -220,6 +220,7 @@ def _stub_legs(monkeypatch, **override):
         "crate_api": lambda ctx, sets: {"recover_match": True},
         "cpu_baseline": lambda args, sets, info: {"self_check": True, "value": 1.0},
         "run_c5": lambda args, ctx: {"blake3_match": True, "repair": {"match": True}},
+        "c4_one_process": lambda args, ctx, world, one: {"match": True},
     }
     legs.update(override)
     for k, v in legs.items():
@@ -229,7 +230,7 @@ def _stub_legs(monkeypatch, **override):
 def _run_stub_main(capsys):
     import json
     rc = bench.main(["--stub", "--stub-legs", "--segments", "4", "--segment-bytes", "4096",
-                     "--steps", "2", "--warmup", "1", "--settle-ms", "0", "--c4", "off"])
+                     "--steps", "2", "--warmup", "1", "--settle-ms", "0", "--c4-segments", "40"])
     line = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
     return rc, line
 
@@ -240,7 +241,7 @@ def test_all_legs_passing_gives_all_ok(monkeypatch, capsys):
     pc = line["parity_check"]
     assert rc == 0 and pc["all_ok"] and pc["failed"] == []
     for k in ("c1_rs13", "c3_decode", "c5_blake3", "c5_repair", "blake3_c2", "pcie_decode",
-              "crate_recover", "cpu_baseline_self_check"):
+              "crate_recover", "cpu_baseline_self_check", "c4_decode", "c4_one_process"):
         assert k in pc["expected"], k
     assert "c2_encode" in pc["not_applicable"]  # no golden covers a 4 x 4 KiB batch
 
