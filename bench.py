@@ -1050,11 +1050,20 @@ def crate_api(ctx, sets, reps=7, staging_ab=True):
 
 
 B3_GOLDEN = os.path.join(ROOT, "tests", "golden", "blake3_c2.json")
-# VALU ceiling of the device BLAKE3: one lane compresses one
-# 1 KiB chunk block by block; ~780 VALU per 64-B block and lane (round-2 PMC),
-# 256 CUs x 4 SIMDs x 16 lanes per clock at the 2.4 GHz peak clock
-B3_VALU_PER_BLOCK = 780
-B3_VALU_CEILING_GBPS = 256 * 64 * 2.4e9 / B3_VALU_PER_BLOCK * 64 / 1e9
+# VALU ceilings of the device BLAKE3, 256 CUs x 4 SIMDs x 16
+# lanes per clock at the 2.4 GHz peak clock.  The compression function needs
+# ~690 VALU per 64-B block and lane (7 rounds x 8 G x 12 ops + the output
+# XORs); the algorithm runs 16 block compressions per 1 KiB chunk plus one
+# parent per chunk (n - 1 parents for n chunks), so 690 x 17/16 = 733 VALU per
+# 64 B of input is the algorithmic need (`peak`).  `peak_compression_only`
+# (690 per 64 B, no parents) and round 3's issued count (780) are reported too.
+B3_VALU_PER_BLOCK = 690
+B3_VALU_PER_64B_ALG = B3_VALU_PER_BLOCK * 17 / 16
+B3_LANE_OPS_PER_S = 256 * 64 * 2.4e9
+
+
+def b3_ceiling_gbps(valu_per_64b):
+    return B3_LANE_OPS_PER_S / valu_per_64b * 64 / 1e9
 
 
 def blake3_device(ctx, sets, calls=10):
@@ -1088,13 +1097,32 @@ def blake3_device(ctx, sets, calls=10):
     return {"GBps": round(nbytes / best / 1e9, 1), "ms": round(best * 1e3, 3),
             "mean_ms": round(sum(ts) / len(ts) * 1e3, 3), "bytes": nbytes,
             "roofline": {"bound": "valu", "achieved": round(nbytes / best / 1e9, 1),
-                         "peak": round(B3_VALU_CEILING_GBPS, 1), "unit": "GB/s",
-                         "frac": round(nbytes / best / 1e9 / B3_VALU_CEILING_GBPS, 4),
-                         "note": f"~{B3_VALU_PER_BLOCK} VALU per 64-B block and lane; "
-                                 "256 CUs x 64 lane-ops per clock at 2.4 GHz"},
+                         "peak": round(b3_ceiling_gbps(B3_VALU_PER_64B_ALG), 1), "unit": "GB/s",
+                         "frac": round(nbytes / best / 1e9 / b3_ceiling_gbps(B3_VALU_PER_64B_ALG), 4),
+                         "peak_compression_only": round(b3_ceiling_gbps(B3_VALU_PER_BLOCK), 1),
+                         "frac_compression_only": round(
+                             nbytes / best / 1e9 / b3_ceiling_gbps(B3_VALU_PER_BLOCK), 4),
+                         "peak_r3_issued_780": round(b3_ceiling_gbps(780), 1),
+                         "note": f"peak: {B3_VALU_PER_BLOCK} VALU per 64-B compression x 17/16 "
+                                 "(one parent per 1 KiB chunk) = the algorithm's VALU per 64 B of "
+                                 "input; 256 CUs x 64 lane-ops per clock at 2.4 GHz"},
             "parity_check": check,
             "what": "bfrs_blake3_batch_dev over C2's 128 x 32 MiB data segments in HBM, one call "
                     "(upload + kernels + digest download), best of 10 wall-clock calls"}
+
+
+def pinned_host_state(rt):
+    """Pinned host memory this process holds at the time (torch's caching host
+    allocator: pinned buffers it keeps after they are freed)."""
+    if rt.stub:
+        return None
+    try:
+        st = rt.torch.cuda.host_memory_stats()
+        return {k: st.get(k) for k in ("allocated_bytes.current", "reserved_bytes.current",
+                                      "num_host_alloc", "num_host_free") if k in st} or dict(
+            list(st.items())[:8])
+    except Exception as e:  # noqa: BLE001 - informative only
+        return {"error": f"{type(e).__name__}: {e}"}
 
 
 def rayon_fresh_process():
@@ -1338,7 +1366,7 @@ def live_pmc_traffic(args):
 TRACE_PASS_TIMEOUT_S = 150
 
 
-def same_process_trace(rt, step, stream, steps, profile_dir=None):
+def same_process_trace(rt, step, stream, steps, profile_dir=None, settle_ms=300.0):
     """A kernel trace of THIS process: K more steps on the timed region's own
     buffers (same process, same HBM placement, right after the timed region),
     recorded by the profiler built into torch (kineto over the ROCm tracer:
@@ -1357,6 +1385,10 @@ def same_process_trace(rt, step, stream, steps, profile_dir=None):
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         rt.sync()
         with profile(activities=[ProfilerActivity.CUDA]) as prof:
+            # the profiler's start idles the GPU, and the clock ramps after
+            # any idle gap: settle again inside the trace, then
+            # the K traced steps, whose 2K launches are the last in the trace
+            settle(rt, step, settle_ms)
             ev0.record(stream)
             for _ in range(steps):
                 step()
@@ -1368,8 +1400,10 @@ def same_process_trace(rt, step, stream, steps, profile_dir=None):
         if len(kern) < 2 * steps:
             return {"error": f"trace holds {len(kern)} gf_apply dispatches, expected {2 * steps}"}
         d = [x[1] / 1e6 for x in sorted(kern)[-2 * steps:]]
-        out = {"how": "torch.profiler (kineto, ROCm tracer) over K more steps on the timed "
-                      "region's own buffers, right after it, in the bench process itself",
+        out = {"how": "torch.profiler (kineto over the ROCm tracer: GPU timestamps of every "
+                      "dispatch) in the bench process itself, on the timed region's own "
+                      f"buffers right after it: {settle_ms:.0f} ms of settle steps, then K "
+                      "traced steps; the last 2K gf_apply dispatches",
                "kernel": kern[-1][2].rsplit("(", 1)[0].replace("void ", ""),
                "launches": len(d), "mean_ms": round(statistics.mean(d), 4),
                "median_ms": round(statistics.median(d), 4), "min_ms": round(min(d), 4),
@@ -1825,7 +1859,13 @@ def main(argv=None):
     if solo_legs and args.pcie == "auto":
         pcie = legs.run("pcie_inclusive", pcie_inclusive, ctx, sets)
     if solo_legs and args.crate == "auto":
+        host_pinned = pinned_host_state(rt)
+        if os.environ.get("BENCH_HOST_EMPTY_CACHE") == "1" and not rt.stub:
+            rt.torch._C._host_emptyCache()  # A/B: give torch's cached pinned blocks back first
+            host_pinned["after_empty_cache"] = pinned_host_state(rt)
         crate = legs.run("crate_api", crate_api, ctx, sets)
+        if isinstance(crate, dict) and "error" not in crate:
+            crate["pinned_host_before"] = host_pinned
         if rayon_child is not None and "error" not in crate:
             crate["generate_parity_all_blocks_fresh_process"] = rayon_child
     if solo_legs and args.cpu_baseline == "auto":
@@ -1907,12 +1947,19 @@ def main(argv=None):
                 alg_bytes / (trace["mean_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
         elif trace is None:
             trace = {"live_pass": "skipped under rocprofv3" if under_rocprof() else "off"}
-        line["roofline"]["trace"] = trace
+        if trace and "error" not in trace:
+            trace["note"] = ("another process: its shard buffers land wherever the driver places "
+                             "them, in either HBM placement mode (DESIGN.md §9b), so its launch "
+                             "time can differ from this process's by the mode gap (~8%)")
         if sp_trace and "error" not in sp_trace:
             sp_trace["ratio_mean_to_launch_ms"] = round(sp_trace["mean_ms"] / launch_ms, 4)
+            sp_trace["ratio_median_to_launch_ms"] = round(sp_trace["median_ms"] / launch_ms, 4)
             sp_trace["frac_at_trace_mean"] = round(
                 alg_bytes / (sp_trace["mean_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
-        line["roofline"]["trace_same_process"] = sp_trace
+        # roofline.trace: a kernel trace of this very process (same buffers,
+        # same placement); the rocprofv3 child pass beside it
+        line["roofline"]["trace"] = sp_trace
+        line["roofline"]["trace_rocprofv3_child"] = trace
         line["cpu_baseline"] = cpu
         line["crate_api"] = crate
         line["pcie_inclusive"] = pcie

@@ -249,8 +249,37 @@ __global__ __launch_bounds__(256) void blake3_group_kernel(const HashGroup *__re
 #pragma unroll
   for (int w = 0; w < 8; ++w) lds[0][t * kRow + w] = cv[w];
   __syncthreads();
-  pair_down<1>(lds[0], lds[1], nchunks, g.single != 0, g.single ? nullptr : group_cvs + 8 * blockIdx.x,
-               msg_cvs + 8 * g.msg, digests + 8 * g.msg);
+  if (g.single) {  // the whole message: pair down to the root here
+    pair_down<1>(lds[0], lds[1], nchunks, true, nullptr, msg_cvs + 8 * g.msg, digests + 8 * g.msg);
+    return;
+  }
+  // kGroupLevels levels (256 -> 64 nodes); an odd last node is carried up
+  uint32_t n = nchunks, *src = lds[0], *dst = lds[1];
+#pragma unroll
+  for (uint32_t lv = 0; lv < kGroupLevels; ++lv) {
+    const uint32_t half = (n + 1) / 2;
+    if (t < half) {
+      uint32_t r[8];
+      if (2 * t + 1 < n) {
+        parent_cv(src + 2 * t * kRow, src + (2 * t + 1) * kRow, r);
+      } else {
+#pragma unroll
+        for (int w = 0; w < 8; ++w) r[w] = src[2 * t * kRow + w];
+      }
+#pragma unroll
+      for (int w = 0; w < 8; ++w) dst[t * kRow + w] = r[w];
+    }
+    __syncthreads();
+    uint32_t *tmp = src;
+    src = dst;
+    dst = tmp;
+    n = half;
+  }
+  if (t < n) {
+    uint32_t *o = group_cvs + 8 * (size_t(blockIdx.x) * kGroupOut + t);
+#pragma unroll
+    for (int w = 0; w < 8; ++w) o[w] = src[t * kRow + w];
+  }
 }
 
 __global__ __launch_bounds__(256) void blake3_reduce_kernel(const HashReduce *__restrict__ jobs,

@@ -48,9 +48,22 @@ int Context::blake3_dev(size_t n, const uint8_t *const *d_msgs, const size_t *le
       groups.push_back(h);
     }
   }
-  // reduction levels: level L's nodes of message i are cur[off[i], off[i]+cnt[i])
+  // reduction levels: level L's nodes of message i are cur[off[i], off[i]+cnt[i]).
+  // Kernel 1 leaves a multi-group message's level-2 nodes (kGroupOut per full
+  // group, ceil(chunks / 4) for its last one) at group index * kGroupOut.
   std::vector<std::vector<HashReduce>> levels;
-  std::vector<uint32_t> cnt(g_count), off(g_first);
+  std::vector<uint32_t> cnt(n), off(n);
+  for (size_t i = 0; i < n; ++i) {
+    if (g_count[i] == 1) {  // finalised by kernel 1
+      cnt[i] = 1;
+      continue;
+    }
+    const size_t last = lens[i] - size_t(g_count[i] - 1) * kGroupBytes;
+    const uint32_t last_nodes =
+        uint32_t(((last + kChunkBytes - 1) / kChunkBytes + (1u << kGroupLevels) - 1) >> kGroupLevels);
+    off[i] = g_first[i] * kGroupOut;
+    cnt[i] = (g_count[i] - 1) * kGroupOut + last_nodes;
+  }
   for (;;) {
     std::vector<HashReduce> jobs;
     uint32_t next = 0;
@@ -83,9 +96,12 @@ int Context::blake3_dev(size_t n, const uint8_t *const *d_msgs, const size_t *le
   for (auto &l : levels) njobs += l.size();
   const size_t b_groups = align_up(groups.size() * sizeof(HashGroup), 256);
   const size_t b_jobs = align_up(njobs * sizeof(HashReduce) + 16, 256);
-  const size_t b_cv = align_up(groups.size() * 32, 256);
+  // cvA holds kernel 1's level-2 nodes (and later levels in place); cvB the
+  // first reduce level's outputs, <= one per kReduceFanIn nodes per message
+  const size_t b_cv = align_up(groups.size() * kGroupOut * 32, 256);
+  const size_t b_cv1 = align_up((groups.size() * kGroupOut / kReduceFanIn + n + 1) * 32, 256);
   const size_t b_out = align_up(n * 32, 256);
-  const size_t need = b_groups + b_jobs + 2 * b_cv + 2 * b_out;
+  const size_t need = b_groups + b_jobs + b_cv + b_cv1 + 2 * b_out;
   const size_t h_need = b_groups + b_jobs + 2 * b_out;
   if (need > d_hash_cap) {
     if (d_hash) {
@@ -113,8 +129,8 @@ int Context::blake3_dev(size_t n, const uint8_t *const *d_msgs, const size_t *le
   auto *d_jobs = reinterpret_cast<HashReduce *>(d + b_groups);
   auto *d_cv0 = reinterpret_cast<uint32_t *>(d + b_groups + b_jobs);
   auto *d_cv1 = reinterpret_cast<uint32_t *>(d + b_groups + b_jobs + b_cv);
-  auto *d_msg_cvs = reinterpret_cast<uint32_t *>(d + b_groups + b_jobs + 2 * b_cv);
-  auto *d_digests = reinterpret_cast<uint32_t *>(d + b_groups + b_jobs + 2 * b_cv + b_out);
+  auto *d_msg_cvs = reinterpret_cast<uint32_t *>(d + b_groups + b_jobs + b_cv + b_cv1);
+  auto *d_digests = reinterpret_cast<uint32_t *>(d + b_groups + b_jobs + b_cv + b_cv1 + b_out);
   // descriptors through pinned memory (one async copy)
   std::memcpy(h, groups.data(), groups.size() * sizeof(HashGroup));
   size_t jo = 0;
