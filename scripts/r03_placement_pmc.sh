@@ -14,6 +14,9 @@ SETS=("TCC_EA0_RDREQ_GMI_32B_sum TCC_EA0_RDREQ_DRAM_sum TCC_EA0_RDREQ_GMI_CREDIT
       "TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum TCC_EA0_WRREQ_DRAM_CREDIT_STALL_sum TCC_EA0_RDREQ_LEVEL_sum TCC_EA0_RDREQ_sum GRBM_GUI_ACTIVE")
 for i in ${PASSES:-1 2 3}; do
   set=${SETS[$((i - 1))]}
+  # a set over one pass's per-block limits makes rocprofv3 hang at start
+  # (round 3's per-channel TCC pass): refuse it before the GPU is touched
+  python3 tools/pmc_fit.py $set || exit 2
   timeout -s KILL 240 rocprofv3 --pmc $set --output-format csv -d "$PWD/$OUT/ppmc_${TAG}_$i" -o pmc \
       -- python3 tools/placement_pmc.py --copies ${COPIES:-6} --launches 20 > "$OUT/ppmc_${TAG}_$i.log" 2>&1
   rc=$?; echo "pass $i rc=$rc"; [ $rc -eq 0 ] || exit $rc
