@@ -56,7 +56,7 @@ EXPORTS = (
     "bfrs_decode_host_batch", "bfrs_encode_host_batch_multi", "bfrs_decode_host_batch_multi",
     "bfrs_generate_parity",
     "bfrs_generate_parity_segmented", "bfrs_recover_segment_rs13", "bfrs_recover_segment_rs30_3",
-    "bfrs_blake3_hex", "bfrs_blake3_batch_dev", "bfrs_blake3_combine", "bfrs_merkle_root_hex", "bfrs_manifest_check", "bfrs_commit", "bfrs_commit_multi", "bfrs_repair", "bfrs_health_check",
+    "bfrs_blake3_hex", "bfrs_blake3_batch_dev", "bfrs_blake3_combine", "bfrs_merkle_root_hex", "bfrs_manifest_check", "bfrs_commit", "bfrs_commit_multi", "bfrs_repair", "bfrs_repair_multi", "bfrs_health_check",
     "bfrs_store_list", "bfrs_store_find", "bfrs_batch_health_check", "bfrs_archive_open",
     "bfrs_archive_size", "bfrs_archive_stat", "bfrs_archive_read", "bfrs_archive_stats_get", "bfrs_archive_close",
 )
@@ -193,6 +193,8 @@ def lib() -> ctypes.CDLL:
             "bfrs_health_check": ([_vp, ctypes.c_char_p, ctypes.c_char_p, _sz, ctypes.POINTER(_sz)],
                                   ctypes.c_int),
             "bfrs_repair": ([_vp, ctypes.c_char_p, ctypes.POINTER(RepairReport)], ctypes.c_int),
+            "bfrs_repair_multi": ([_pp, _sz, ctypes.c_char_p, ctypes.POINTER(RepairReport)],
+                                  ctypes.c_int),
             "bfrs_store_list": ([ctypes.c_char_p, ctypes.c_char_p, _sz, ctypes.POINTER(_sz)],
                                 ctypes.c_int),
             "bfrs_store_find": ([ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, _sz,
@@ -809,10 +811,16 @@ def decode_host_batch_multi(ctxs, original_counts, recovery_count, shard_bytes, 
                                               recovery_count, shard_bytes, po, pr, pd))
 
 
-def repair(ctx: Context, archive_dir: str) -> dict:
-    """FileStore::repair (src/filestore/health.rs:470-495), intended semantics."""
+def repair(ctx, archive_dir: str) -> dict:
+    """FileStore::repair (src/filestore/health.rs:470-495), intended semantics.
+    `ctx` may be a list of contexts: bfrs_repair_multi deals a tier-3 archive's
+    blocks over them from this one process."""
     rep = RepairReport()
-    _check(lib().bfrs_repair(ctx.handle, os.fsencode(archive_dir), ctypes.byref(rep)))
+    if isinstance(ctx, (list, tuple)):
+        pc, kc = _ctx_array(ctx)
+        _check(lib().bfrs_repair_multi(pc, len(ctx), os.fsencode(archive_dir), ctypes.byref(rep)))
+    else:
+        _check(lib().bfrs_repair(ctx.handle, os.fsencode(archive_dir), ctypes.byref(rep)))
     return rep.as_dict()
 
 

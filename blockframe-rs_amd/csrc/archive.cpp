@@ -921,49 +921,101 @@ int bfrs_commit_multi(bfrs_ctx *const *ctxs, size_t n_ctx, const char *file_path
   BFRS_API_END
 }
 
-int bfrs_repair(bfrs_ctx *ctx, const char *archive_dir, bfrs_repair_report *report) {
-  BFRS_API_BEGIN
-  if (!ctx || !archive_dir || !report)
+}  // extern "C"
+
+namespace {
+// repair_blocked (health.rs:642-765), intended semantics, over the blocks
+// `mine` of a tier-3 archive on one context; counts land in *rep.
+int repair_blocks(bfrs_ctx *ctx, const Geometry &g, const std::vector<size_t> &mine,
+                  bfrs_repair_report *rep) {
+  if (hipSetDevice(ctx->impl.device) != hipSuccess)
+    return set_error(BFRS_E_HIP, "repair: hipSetDevice failed");
+  StagingCache &sc = staging(ctx);
+  std::lock_guard<std::mutex> staging_lock(sc.mu);
+  Arena &a = sc.a[0];
+  int rc;
+  for (const size_t b : mine) {
+    BlockState bs;
+    if ((rc = load_block(ctx, g, b, a, &bs))) return rc;
+    ++rep->blocks_checked;
+    rep->segments_checked += bs.k;
+    const std::vector<uint8_t> was_ok = bs.seg_ok;
+    const size_t parity_bad = kParity - bs.valid_parity();
+    const int restored = restore_block(ctx, g, a, bs);
+    if (restored == BFRS_E_NOT_ENOUGH_SHARDS) {
+      ++rep->unrecoverable_blocks;
+      continue;
+    }
+    if (restored < 0) return restored;
+    for (size_t s = 0; s < bs.k; ++s)
+      if (!was_ok[s]) {
+        if (!write_file(t3_seg(g.dir, b, s), a.hs(s), bs.lens[s]))
+          return io_error("write restored segment");
+        ++rep->segments_repaired;
+      }
+    if (parity_bad) {
+      const std::vector<uint8_t> par_was = bs.par_ok;
+      if ((rc = reencode_parity(ctx, g, a, bs))) return rc;
+      for (size_t p = 0; p < kParity; ++p)
+        if (!par_was[p] && !write_file(t3_par(g.dir, b, p), a.hs(bs.k + p), bs.shard))
+          return io_error("write parity");
+      rep->parity_repaired += parity_bad;
+    }
+  }
+  return BFRS_OK;
+}
+
+// Tier-3 blocks dealt round-robin over the contexts (block b to context
+// b % n), each context on a host thread of its own; reports summed.
+int repair_tier3(const std::vector<bfrs_ctx *> &ctxs, const Geometry &g, bfrs_repair_report *report) {
+  std::vector<size_t> blocks;
+  for (const auto &kv : g.mf.blocks) blocks.push_back(size_t(kv.first));
+  const size_t n = std::max<size_t>(1, std::min(ctxs.size(), blocks.size()));
+  std::vector<std::vector<size_t>> mine(n);
+  for (size_t i = 0; i < blocks.size(); ++i) mine[i % n].push_back(blocks[i]);
+  std::vector<bfrs_repair_report> reps(n, bfrs_repair_report{});
+  std::vector<int> rcs(n, BFRS_OK);
+  std::vector<std::string> errs(n);
+  auto run = [&](size_t d) {
+    try {
+      rcs[d] = repair_blocks(ctxs[d], g, mine[d], &reps[d]);
+    } catch (const std::bad_alloc &) {
+      rcs[d] = set_error(BFRS_E_NOMEM, "host memory allocation failed");
+    } catch (const std::exception &e) {
+      rcs[d] = set_error(BFRS_E_WRAPPER, std::string("internal error: ") + e.what());
+    }
+    if (rcs[d]) errs[d] = bfrs_last_error();
+  };
+  {
+    std::vector<BgTask> others(n - 1);  // joined on every exit path
+    for (size_t d = 1; d < n; ++d) others[d - 1].start([&run, d] { run(d); });
+    run(0);
+    for (auto &t : others) t.join();
+  }
+  for (const auto &r : reps) {
+    report->blocks_checked += r.blocks_checked;
+    report->segments_checked += r.segments_checked;
+    report->segments_repaired += r.segments_repaired;
+    report->parity_repaired += r.parity_repaired;
+    report->unrecoverable_blocks += r.unrecoverable_blocks;
+  }
+  for (size_t d = 0; d < n; ++d)
+    if (rcs[d]) return set_error(rcs[d], n == 1 ? errs[d] : "context " + std::to_string(d) + ": " + errs[d]);
+  return BFRS_OK;
+}
+
+int repair_impl(const std::vector<bfrs_ctx *> &ctxs, const char *archive_dir,
+                bfrs_repair_report *report) {
+  if (ctxs.empty() || !archive_dir || !report)
     return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_repair: NULL argument");
+  for (bfrs_ctx *c : ctxs)
+    if (!c) return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_repair: NULL context");
+  bfrs_ctx *ctx = ctxs[0];
   *report = bfrs_repair_report{};
   Geometry g;
   int rc = load_geometry(archive_dir, &g);
   if (rc) return rc;
-  if (g.mf.tier == 3) {  // repair_blocked (health.rs:642-765), intended semantics
-    StagingCache &sc = staging(ctx);
-    std::lock_guard<std::mutex> staging_lock(sc.mu);
-    Arena &a = sc.a[0];
-    for (const auto &kv : g.mf.blocks) {
-      const size_t b = size_t(kv.first);
-      BlockState bs;
-      if ((rc = load_block(ctx, g, b, a, &bs))) return rc;
-      ++report->blocks_checked;
-      report->segments_checked += bs.k;
-      const std::vector<uint8_t> was_ok = bs.seg_ok;
-      const size_t parity_bad = kParity - bs.valid_parity();
-      const int restored = restore_block(ctx, g, a, bs);
-      if (restored == BFRS_E_NOT_ENOUGH_SHARDS) {
-        ++report->unrecoverable_blocks;
-        continue;
-      }
-      if (restored < 0) return restored;
-      for (size_t s = 0; s < bs.k; ++s)
-        if (!was_ok[s]) {
-          if (!write_file(t3_seg(g.dir, b, s), a.hs(s), bs.lens[s]))
-            return io_error("write restored segment");
-          ++report->segments_repaired;
-        }
-      if (parity_bad) {
-        const std::vector<uint8_t> par_was = bs.par_ok;
-        if ((rc = reencode_parity(ctx, g, a, bs))) return rc;
-        for (size_t p = 0; p < kParity; ++p)
-          if (!par_was[p] && !write_file(t3_par(g.dir, b, p), a.hs(bs.k + p), bs.shard))
-            return io_error("write parity");
-        report->parity_repaired += parity_bad;
-      }
-    }
-    return BFRS_OK;
-  }
+  if (g.mf.tier == 3) return repair_tier3(ctxs, g, report);
   // tiers 1/2 (repair_tiny :497, repair_segment :542): per-segment RS(1,3).
   // The reference restores only the data; with the intended semantics, as
   // for tier 3, a damaged parity copy is re-encoded from the verified data
@@ -1017,6 +1069,22 @@ int bfrs_repair(bfrs_ctx *ctx, const char *archive_dir, bfrs_repair_report *repo
     }
   }
   return BFRS_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int bfrs_repair(bfrs_ctx *ctx, const char *archive_dir, bfrs_repair_report *report) {
+  BFRS_API_BEGIN
+  return repair_impl({ctx}, archive_dir, report);
+  BFRS_API_END
+}
+
+int bfrs_repair_multi(bfrs_ctx *const *ctxs, size_t n_ctx, const char *archive_dir,
+                      bfrs_repair_report *report) {
+  BFRS_API_BEGIN
+  if (!ctxs || n_ctx == 0) return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_repair_multi: no contexts");
+  return repair_impl(std::vector<bfrs_ctx *>(ctxs, ctxs + n_ctx), archive_dir, report);
   BFRS_API_END
 }
 

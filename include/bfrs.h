@@ -317,6 +317,13 @@ typedef struct {
  * re-encoded.  Blocks with more damage than valid parity are counted, not
  * errors. */
 int bfrs_repair(bfrs_ctx *ctx, const char *archive_dir, bfrs_repair_report *report);
+/* bfrs_repair over several contexts (normally one per device) from one
+ * process: a tier-3 archive's blocks are dealt round-robin (block b to context
+ * b % n_ctx, repair_blocked's independent blocks, health.rs:642-765), each
+ * context verifying, decoding and writing its blocks on a host thread of its
+ * own; the report is the sum.  Tiers 1/2 run on ctxs[0]. */
+int bfrs_repair_multi(bfrs_ctx *const *ctxs, size_t n_ctx, const char *archive_dir,
+                      bfrs_repair_report *report);
 
 /* FileStore::health_check (src/filestore/health.rs:111-438), intended
  * semantics: every shard is hashed against the manifest (tier 3: device

@@ -156,7 +156,21 @@ def test_commit_multi_equals_commit(bfrs, tmp_path, n_ctx, seg, size):
             else:
                 assert ta[f] == tb[f], f
         assert bfrs.health_check(one, b)["status"] == "Healthy"
+        # damage in two blocks, repaired through bfrs_repair_multi (blocks dealt
+        # over the contexts, report summed), then through bfrs_repair
         seg0 = os.path.join(b, "blocks", "block_0", "segments", "segment_1.dat")
+        par1 = os.path.join(b, "blocks", "block_1", "parity", "block_parity_2.dat")
+        os.unlink(seg0)
+        with open(par1, "r+b") as f:
+            c = f.read(1)
+            f.seek(0)
+            f.write(bytes([c[0] ^ 0xFF]))
+        rep = bfrs.repair(ctxs, b)
+        assert rep["segments_repaired"] == 1 and rep["parity_repaired"] == 1, rep
+        assert rep["blocks_checked"] == len([k for k in ta if k.endswith("block_parity_0.dat")])
+        assert bfrs.health_check(one, b)["status"] == "Healthy"
+        for f in (seg0, par1):
+            assert open(f, "rb").read() == ta[os.path.relpath(f, b)]
         os.unlink(seg0)
         rep = bfrs.repair(one, b)
         assert rep["segments_repaired"] == 1 and bfrs.health_check(one, b)["status"] == "Healthy"
