@@ -214,7 +214,7 @@ __device__ __forceinline__ void pair_down(uint32_t *buf0, uint32_t *buf1, uint32
   }
 }
 
-__global__ __launch_bounds__(256) void blake3_group_kernel(const HashGroup *__restrict__ groups,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void blake3_group_kernel(const HashGroup *__restrict__ groups,
                                                            uint32_t *__restrict__ group_cvs,
                                                            uint32_t *__restrict__ msg_cvs,
                                                            uint32_t *__restrict__ digests) {

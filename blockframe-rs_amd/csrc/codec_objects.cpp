@@ -63,7 +63,8 @@ struct CodecObject {
       HIP_TRY(hipMemcpyAsync(d_row(i), h_row(i), len, hipMemcpyHostToDevice, slot->stream));
     } else {
       HIP_TRY(hipMemcpyAsync(d_row(i), src, len, hipMemcpyHostToDevice, slot->stream));
-      HIP_TRY(hipStreamSynchronize(slot->stream));
+      int rc = slot->sync();
+      if (rc) return rc;
     }
     return BFRS_OK;
   }
@@ -201,7 +202,7 @@ int bfrs_encoder_encode(bfrs_encoder *e) {
   for (size_t j = 0; j < e->m; ++j)
     HIP_TRY(hipMemcpyAsync(e->h_row(e->k + j), e->d_row(e->k + j), e->shard_bytes,
                            hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipStreamSynchronize(st));
+  if ((rc = e->slot->sync())) return rc;
   e->encoded = true;
   e->fetched_to_pinned = true;
   return BFRS_OK;
@@ -316,8 +317,7 @@ int bfrs_decoder_decode(bfrs_decoder *d) {
   d->decoded = true;
   hipStream_t st = d->slot->stream;
   if (orig_recv == d->k) {  // nothing to restore; the staged copies still have to land
-    HIP_TRY(hipStreamSynchronize(st));
-    return BFRS_OK;
+    return d->slot->sync();
   }
   // Restored shards are written over the erased originals' own rows.
   std::vector<const uint8_t *> dorig(d->k), drec(d->m);
@@ -334,7 +334,7 @@ int bfrs_decoder_decode(bfrs_decoder *d) {
   int rc = decode_batch_on(d->ctx, 1, &kk, d->m, d->shard_bytes, dorig.data(), drec.data(),
                            drest.data(), st);
   if (rc) return rc;
-  HIP_TRY(hipStreamSynchronize(st));
+  if ((rc = d->slot->sync())) return rc;
   for (size_t i = 0; i < d->k; ++i) d->restored[i] = !d->orig_present[i];
   return BFRS_OK;
   BFRS_API_END
@@ -353,7 +353,8 @@ int bfrs_decoder_restored_original(bfrs_decoder *d, size_t index, const uint8_t 
     HIP_TRY(hipSetDevice(d->pool->device));
     HIP_TRY(hipMemcpyAsync(d->h_row(index), d->d_row(index), d->shard_bytes, hipMemcpyDeviceToHost,
                            d->slot->stream));
-    HIP_TRY(hipStreamSynchronize(d->slot->stream));
+    int rc = d->slot->sync();
+    if (rc) return rc;
     d->fetched[index] = 1;
   }
   *data = d->h_row(index);
@@ -380,6 +381,5 @@ int bfrs::decoder_restored_to_host(bfrs_decoder *d, size_t index, uint8_t *out) 
   HIP_TRY(hipSetDevice(d->pool->device));
   HIP_TRY(hipMemcpyAsync(out, d->d_row(index), d->shard_bytes, hipMemcpyDeviceToHost,
                          d->slot->stream));
-  HIP_TRY(hipStreamSynchronize(d->slot->stream));
-  return BFRS_OK;
+  return d->slot->sync();
 }

@@ -99,8 +99,18 @@ static int upload_plan(Plan *p) {
   return BFRS_OK;
 }
 
+int CodecSlot::sync() {
+  HIP_TRY(hipEventRecord(done, stream));
+  HIP_TRY(hipEventSynchronize(done));
+  return BFRS_OK;
+}
+
 CodecSlot::~CodecSlot() {
-  if (stream) {
+  if (done) {
+    if (stream) (void)sync();
+    (void)hipEventDestroy(done);
+  }
+  if (stream && own_stream) {
     (void)hipStreamSynchronize(stream);
     (void)hipStreamDestroy(stream);
   }
@@ -108,25 +118,51 @@ CodecSlot::~CodecSlot() {
   if (h) (void)hipHostFree(h);
 }
 
+int CodecPool::init_streams(size_t n) {
+  for (size_t i = 0; i < n; ++i) {
+    hipStream_t st;
+    HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    streams.push_back(st);
+    users.push_back(0);
+  }
+  return BFRS_OK;
+}
+
 int CodecPool::acquire(size_t nshards, size_t shard_bytes, std::unique_ptr<CodecSlot> *out) {
   const size_t stride = (shard_bytes + 255) / 256 * 256;
+  std::unique_ptr<CodecSlot> s;
   {
     std::lock_guard<std::mutex> g(mu);
     for (size_t i = 0; i < free.size(); ++i)
       if (free[i]->stride >= stride && free[i]->nshards >= nshards &&
           free[i]->stride * free[i]->nshards <= 2 * stride * nshards) {
-        *out = std::move(free[i]);
+        s = std::move(free[i]);
         free.erase(free.begin() + long(i));
-        return BFRS_OK;
+        break;
       }
   }
-  auto s = std::make_unique<CodecSlot>();
-  s->stride = stride;
-  s->nshards = nshards;
-  HIP_TRY(hipSetDevice(device));
-  HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
-  HIP_TRY(hipMalloc(&s->d, stride * nshards));
-  HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&s->h), stride * nshards, hipHostMallocDefault));
+  if (!s) {
+    s = std::make_unique<CodecSlot>();
+    s->stride = stride;
+    s->nshards = nshards;
+    HIP_TRY(hipSetDevice(device));
+    HIP_TRY(hipEventCreateWithFlags(&s->done, hipEventDisableTiming));
+    if (streams.empty()) {
+      HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+      s->own_stream = true;
+    }
+    HIP_TRY(hipMalloc(&s->d, stride * nshards));
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&s->h), stride * nshards, hipHostMallocDefault));
+  }
+  if (!streams.empty()) {  // the shared stream with the fewest live slots
+    std::lock_guard<std::mutex> g(mu);
+    size_t best = 0;
+    for (size_t i = 1; i < streams.size(); ++i)
+      if (users[i] < users[best]) best = i;
+    ++users[best];
+    s->stream = streams[best];
+    s->stream_idx = int(best);
+  }
   *out = std::move(s);
   return BFRS_OK;
 }
@@ -152,10 +188,14 @@ struct DeviceScope {
 void CodecPool::release(std::unique_ptr<CodecSlot> slot) {
   if (!slot) return;
   DeviceScope scope(device);  // a slot dropped below is freed on its own device
-  (void)hipStreamSynchronize(slot->stream);
+  (void)slot->sync();
   std::unique_ptr<CodecSlot> drop;  // freed after the lock is released
   {
     std::lock_guard<std::mutex> g(mu);
+    if (slot->stream_idx >= 0) {  // give the shared stream back
+      --users[size_t(slot->stream_idx)];
+      slot->stream_idx = -1;
+    }
     if (free.size() < cached) {
       free.push_back(std::move(slot));
       return;
@@ -175,6 +215,10 @@ void CodecPool::release(std::unique_ptr<CodecSlot> slot) {
 CodecPool::~CodecPool() {
   DeviceScope scope(device);
   free.clear();
+  for (hipStream_t st : streams) {
+    (void)hipStreamSynchronize(st);
+    (void)hipStreamDestroy(st);
+  }
 }
 
 Context::~Context() {
@@ -222,7 +266,18 @@ int Context::init(int dev) {
       return set_error(BFRS_E_INVALID_ARGUMENT,
                        std::string("BFRS_CODEC_STAGING=") + e + ": expected direct or pinned");
   }
+  size_t codec_streams = 4;
+  if (const char *e = std::getenv("BFRS_CODEC_STREAMS")) {
+    char *end = nullptr;
+    const long v = std::strtol(e, &end, 10);
+    if (end == e || v < 0 || v > 64)
+      return set_error(BFRS_E_INVALID_ARGUMENT,
+                       std::string("BFRS_CODEC_STREAMS=") + e + ": expected 0..64");
+    codec_streams = size_t(v);
+  }
   HIP_TRY(hipSetDevice(dev));
+  // the codec streams first: created before any copy, consecutively
+  if (int rc = codec_pool->init_streams(codec_streams)) return rc;
   HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
   for (auto &ps : pipe_stream) HIP_TRY(hipStreamCreateWithFlags(&ps, hipStreamNonBlocking));
   return BFRS_OK;

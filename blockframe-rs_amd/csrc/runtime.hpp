@@ -97,7 +97,13 @@ struct CodecSlot {
   void *d = nullptr;     // nshards x stride bytes of HBM
   uint8_t *h = nullptr;  // nshards x stride bytes of pinned host memory
   size_t stride = 0, nshards = 0;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;  // the pool's stream this slot runs on (or its own)
+  bool own_stream = false;       // BFRS_CODEC_STREAMS=0: one stream per slot
+  int stream_idx = -1;           // index into CodecPool::streams while acquired
+  hipEvent_t done = nullptr;     // marks this slot's last queued operation
+  // Waits for this slot's work queued so far (not for later work of other
+  // slots sharing the stream).
+  int sync();
   ~CodecSlot();
 };
 
@@ -117,12 +123,23 @@ enum class Staging { kDirect, kPinned };
 // The slot cache of one context.  Shared (shared_ptr) by the context and by
 // every live codec object, so an object freed after bfrs_close still returns
 // or frees its slot safely; the pool goes away with the last of them.
+//
+// Streams (round 4): the slots of a context run on a small fixed set of
+// streams created with the context (BFRS_CODEC_STREAMS, default 4 = the HIP
+// runtime's default hardware-queue count per process); an acquired slot takes
+// the stream with the fewest live slots.  One stream per slot (=0, rounds
+// 2-3) let the stream count grow with the slot pool, and concurrent objects'
+// streams then shared hardware queues in whatever pattern their creation
+// order gave.
 struct CodecPool {
   int device = 0;
   Staging staging = Staging::kPinned;
   std::mutex mu;
   std::vector<std::unique_ptr<CodecSlot>> free;
   size_t cached = 2;  // BFRS_CODEC_SLOTS: idle slots kept (0 = none)
+  std::vector<hipStream_t> streams;  // shared codec streams (empty: one per slot)
+  std::vector<int> users;            // live slots per shared stream
+  int init_streams(size_t n);
   int acquire(size_t nshards, size_t shard_bytes, std::unique_ptr<CodecSlot> *out);
   void release(std::unique_ptr<CodecSlot> slot);
   ~CodecPool();

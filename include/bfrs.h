@@ -20,7 +20,8 @@
  * how rayon's one-encoder-per-block use (src/chunker/commit.rs:391-466) maps
  * onto it.  Encoder/decoder objects and the batch calls may run concurrently
  * on one context: each codec object owns a pooled slot (device rows, pinned
- * rows, its own HIP stream), the plan cache and the slot pool are locked, the
+ * rows) and runs on one of the context's codec streams, the plan cache and
+ * the slot pool are locked, the
  * host-batch pipeline and the BLAKE3 work area are serialised.  A single
  * encoder or decoder object is used by one thread at a time (as the crate's
  * &mut self API implies).  A context keeps at most BFRS_CODEC_SLOTS idle codec
@@ -37,6 +38,10 @@
  * Environment, read by bfrs_open (BFRS_HOST_COPY_* on first use, once per
  * process):
  *   BFRS_CODEC_SLOTS    idle codec slots kept (default 2; 0 = none)
+ *   BFRS_CODEC_STREAMS  HIP streams the codec objects of a context share
+ *                       (default 4, created with the context; an object takes
+ *                       the one with the fewest live objects); 0 = one stream
+ *                       per slot, as in rounds 2-3
  *   BFRS_CODEC_STAGING  "pinned" (default: add_*_shard copies into a pinned
  *                       row on several threads and queues its H2D) or
  *                       "direct" (one DMA straight from the caller's buffer);
