@@ -598,14 +598,20 @@ def host_budget(args, world):
         cg = None if t == "max" else int(t)
     except (OSError, ValueError):
         pass
-    node = per_rank * world
+    # rank 0 alone, after the other ranks are done: c4_one_process pins config
+    # 4's whole data, parity and restored shards
+    one_proc = ((sum(shapes) + 6 * len(shapes)) * args.segment_bytes
+                if args.c4 == "auto" and args.pcie == "auto" and not args.strong else 0)
+    node = per_rank * world + one_proc
     avail = min(x for x in (mem.get("MemAvailable"), cg) if x) if (mem.get("MemAvailable") or cg) else None
     return {"pinned_bytes_per_rank": per_rank, "ranks": world, "pinned_bytes_node": node,
-            "c4_pcie_pinned_bytes_per_rank": c4_pinned,
+            "c4_pcie_pinned_bytes_per_rank": c4_pinned, "rank0_c4_one_process_bytes": one_proc,
             "mem_total": mem.get("MemTotal"), "mem_available": mem.get("MemAvailable"),
             "cgroup_memory_max": cg, "fits": None if avail is None else node < avail,
             "what": "largest pinned host buffer set of one rank (c4_strong.pcie_inclusive at N>1; "
-                    "at N=1 also pcie_inclusive's C2 batch) x ranks, against this host"}
+                    "at N=1 also pcie_inclusive's C2 batch) x ranks, plus rank 0's "
+                    "c4_one_process buffers, against this host (upper bound: torch keeps "
+                    "freed pinned blocks cached)"}
 
 
 def check_config1(ctx):

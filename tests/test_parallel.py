@@ -151,6 +151,7 @@ def test_stub_line_reports_rank_devices_and_host_budget():
     assert [d["rank"] for d in line["rank_devices"]] == [0, 1]
     hb = line["host_budget"]
     assert hb["ranks"] == 2 and hb["pinned_bytes_per_rank"] == 0  # the stub pins nothing
+    assert hb["pinned_bytes_node"] == 0
 
 
 def test_host_budget_at_eight_ranks():
@@ -161,5 +162,31 @@ def test_host_budget_at_eight_ranks():
     # c4_strong.pcie_inclusive pins each rank's 4 MiB stripes of config 4's
     # 320 data + 33 parity + 33 restored shards
     assert hb["c4_pcie_pinned_bytes_per_rank"] == (320 + 66) * 4 * 2**20
-    assert hb["pinned_bytes_node"] == 8 * hb["pinned_bytes_per_rank"]
+    assert hb["rank0_c4_one_process_bytes"] == (320 + 66) * 32 * 2**20
+    assert hb["pinned_bytes_node"] == 8 * hb["pinned_bytes_per_rank"] + hb["rank0_c4_one_process_bytes"]
     assert hb["mem_total"] and hb["fits"] in (True, False)
+
+
+def test_torchrun_rank_failure_ends_the_job():
+    """The driver's N>1 launch (torch.distributed.run): a rank that dies after
+    joining the process group ends the job within seconds with a non-zero
+    exit, well inside the process-group timeout (bench.PG_TIMEOUT_S)."""
+    import subprocess
+    import sys
+    import time
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(root, "bench.py"), "--gpus", "4", "--stub", "--segments", "8",
+           "--segment-bytes", "65536", "--steps", "3", "--warmup", "1", "--settle-ms", "5",
+           "--c4-segments", "40"]
+    env = dict(os.environ, BENCH_FAIL_RANK="2")
+    env.pop("WORLD_SIZE", None)
+    t0 = time.time()
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=170, env=env, cwd=root)
+    assert r.returncode != 0
+    assert time.time() - t0 < 120
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
