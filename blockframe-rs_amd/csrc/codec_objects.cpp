@@ -31,6 +31,16 @@ using namespace bfrs;
 
 namespace {
 
+// BFRS_PREFAULT_OUTPUTS (default 1): fault the wrapper's fresh output
+// buffers in while the device works (encoder_encode_to_host).
+bool prefault_outputs() {
+  static const bool on = [] {
+    const char *e = std::getenv("BFRS_PREFAULT_OUTPUTS");
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
+  return on;
+}
+
 int shard_size_error(size_t expected, size_t got) {
   std::ostringstream os;
   os << "different shard size: expected " << expected << " bytes, got " << got << " bytes";
@@ -52,20 +62,37 @@ struct CodecObject {
     shard_bytes = bytes;
     return pool->acquire(k + m, shard_bytes, &slot);
   }
+  // Copy streams (runtime.hpp CodecPool): H2D and D2H of every object of the
+  // context in FIFO order on two streams, or on the object's kernel stream.
+  hipStream_t h2d() const { return pool->h2d ? pool->h2d : slot->stream; }
+  hipStream_t d2h() const { return pool->d2h ? pool->d2h : slot->stream; }
   // Stage a host shard into device row i; the caller's buffer is free again
   // on return.
   int stage(size_t i, const uint8_t *src, size_t len) {
     HIP_TRY(hipSetDevice(pool->device));
     if (pool->staging == Staging::kPinned) {
       // the row's previous H2D (an earlier round on this object) is done:
-      // rows are reused only after encode()/decode() synchronised the stream
+      // rows are reused only after encode()/decode() synchronised the slot
       host_copy(h_row(i), src, len);
-      HIP_TRY(hipMemcpyAsync(d_row(i), h_row(i), len, hipMemcpyHostToDevice, slot->stream));
+      HIP_TRY(hipMemcpyAsync(d_row(i), h_row(i), len, hipMemcpyHostToDevice, h2d()));
+      HIP_TRY(hipEventRecord(slot->ev_h2d, h2d()));
     } else {
-      HIP_TRY(hipMemcpyAsync(d_row(i), src, len, hipMemcpyHostToDevice, slot->stream));
-      int rc = slot->sync();
-      if (rc) return rc;
+      HIP_TRY(hipMemcpyAsync(d_row(i), src, len, hipMemcpyHostToDevice, h2d()));
+      HIP_TRY(hipEventRecord(slot->ev_h2d, h2d()));
+      HIP_TRY(hipEventSynchronize(slot->ev_h2d));
     }
+    return BFRS_OK;
+  }
+  // The kernel stream waits for this object's staged rows (the copy stream's
+  // later work, other objects' copies, is not waited for).
+  int kernel_after_h2d() {
+    if (h2d() != slot->stream) HIP_TRY(hipStreamWaitEvent(slot->stream, slot->ev_h2d, 0));
+    return BFRS_OK;
+  }
+  // After the kernel: mark it, and let the D2H stream wait for it.
+  int d2h_after_kernel() {
+    HIP_TRY(hipEventRecord(slot->ev_k, slot->stream));
+    if (d2h() != slot->stream) HIP_TRY(hipStreamWaitEvent(d2h(), slot->ev_k, 0));
     return BFRS_OK;
   }
   ~CodecObject() {
@@ -143,8 +170,12 @@ int encoder_run(bfrs_encoder *e) {
   for (size_t i = 0; i < e->k; ++i) din[i] = e->d_row(i);
   for (size_t j = 0; j < e->m; ++j) dout[j] = e->d_row(e->k + j);
   const uint32_t kk = uint32_t(e->k);
-  return encode_batch_on(e->ctx, 1, &kk, e->m, e->shard_bytes, din.data(), dout.data(),
-                         e->slot->stream);
+  int rc = e->kernel_after_h2d();
+  if (rc) return rc;
+  if ((rc = encode_batch_on(e->ctx, 1, &kk, e->m, e->shard_bytes, din.data(), dout.data(),
+                            e->slot->stream)))
+    return rc;
+  return e->d2h_after_kernel();
 }
 }  // namespace
 
@@ -157,7 +188,7 @@ int bfrs::encoder_encode_to_host(bfrs_encoder *e, uint8_t *const *outs) {
   // overlaps the D2H of shard j + 1.
   int rc = encoder_run(e);
   if (rc) return rc;
-  hipStream_t st = e->slot->stream;
+  hipStream_t st = e->d2h();
   std::vector<hipEvent_t> done(e->m, nullptr);
   struct Events {
     std::vector<hipEvent_t> &v;
@@ -166,17 +197,47 @@ int bfrs::encoder_encode_to_host(bfrs_encoder *e, uint8_t *const *outs) {
         if (x) (void)hipEventDestroy(x);
     }
   } guard{done};
+  // Fresh output buffers (the reference's to_vec, generate.rs:95-96) take
+  // their page faults here, one helper thread per output, while the H2D
+  // tail, the kernel and the first D2H run: the caller's thread would only
+  // wait in that window.  (Touching them during the adds competed with the
+  // staging copies for host memory bandwidth)  Each output's
+  // thread is joined before its copy-out, and on every exit path.
+  struct Touch {
+    std::vector<std::thread> t;
+    ~Touch() {
+      for (auto &x : t)
+        if (x.joinable()) x.join();
+    }
+  } touch;
+  if (prefault_outputs()) {
+    const size_t n = e->shard_bytes;
+    for (size_t j = 0; j < e->m; ++j) {
+      uint8_t *p = outs[j];
+      try {
+        touch.t.emplace_back([p, n] {
+          volatile uint8_t *q = p;
+          for (size_t o = 0; o < n; o += 4096) q[o] = 0;
+          q[n - 1] = 0;
+        });
+      } catch (...) {  // no thread: the copy-out faults the pages itself
+        break;
+      }
+    }
+  }
   for (size_t j = 0; j < e->m; ++j) {
     HIP_TRY(hipMemcpyAsync(e->h_row(e->k + j), e->d_row(e->k + j), e->shard_bytes,
                            hipMemcpyDeviceToHost, st));
     HIP_TRY(hipEventCreateWithFlags(&done[j], hipEventDisableTiming));
     HIP_TRY(hipEventRecord(done[j], st));
   }
+  HIP_TRY(hipEventRecord(e->slot->ev_d2h, st));
   using clk = std::chrono::steady_clock;
   double wait_ms = 0, copy_ms = 0;
   for (size_t j = 0; j < e->m; ++j) {
     const auto t0 = clk::now();
     HIP_TRY(hipEventSynchronize(done[j]));
+    if (j < touch.t.size()) touch.t[j].join();
     const auto t1 = clk::now();
     host_copy(outs[j], e->h_row(e->k + j), e->shard_bytes);
     wait_ms += std::chrono::duration<double, std::milli>(t1 - t0).count();
@@ -198,10 +259,11 @@ int bfrs_encoder_encode(bfrs_encoder *e) {
   if (!e) return set_error(BFRS_E_INVALID_ARGUMENT, "encode: NULL encoder");
   int rc = encoder_run(e);
   if (rc) return rc;
-  hipStream_t st = e->slot->stream;
+  hipStream_t st = e->d2h();
   for (size_t j = 0; j < e->m; ++j)
     HIP_TRY(hipMemcpyAsync(e->h_row(e->k + j), e->d_row(e->k + j), e->shard_bytes,
                            hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipEventRecord(e->slot->ev_d2h, st));
   if ((rc = e->slot->sync())) return rc;
   e->encoded = true;
   e->fetched_to_pinned = true;
@@ -331,9 +393,12 @@ int bfrs_decoder_decode(bfrs_decoder *d) {
   for (size_t j = 0; j < d->m; ++j)
     if (d->rec_present[j]) drec[j] = d->d_row(d->k + j);
   const uint32_t kk = uint32_t(d->k);
-  int rc = decode_batch_on(d->ctx, 1, &kk, d->m, d->shard_bytes, dorig.data(), drec.data(),
-                           drest.data(), st);
+  int rc = d->kernel_after_h2d();
   if (rc) return rc;
+  if ((rc = decode_batch_on(d->ctx, 1, &kk, d->m, d->shard_bytes, dorig.data(), drec.data(),
+                            drest.data(), st)))
+    return rc;
+  if ((rc = d->d2h_after_kernel())) return rc;
   if ((rc = d->slot->sync())) return rc;
   for (size_t i = 0; i < d->k; ++i) d->restored[i] = !d->orig_present[i];
   return BFRS_OK;
@@ -352,7 +417,8 @@ int bfrs_decoder_restored_original(bfrs_decoder *d, size_t index, const uint8_t 
   if (!d->fetched[index]) {  // D2H of this row on first use
     HIP_TRY(hipSetDevice(d->pool->device));
     HIP_TRY(hipMemcpyAsync(d->h_row(index), d->d_row(index), d->shard_bytes, hipMemcpyDeviceToHost,
-                           d->slot->stream));
+                           d->d2h()));
+    HIP_TRY(hipEventRecord(d->slot->ev_d2h, d->d2h()));
     int rc = d->slot->sync();
     if (rc) return rc;
     d->fetched[index] = 1;
@@ -379,7 +445,7 @@ int bfrs::decoder_restored_to_host(bfrs_decoder *d, size_t index, uint8_t *out) 
     return BFRS_OK;
   }
   HIP_TRY(hipSetDevice(d->pool->device));
-  HIP_TRY(hipMemcpyAsync(out, d->d_row(index), d->shard_bytes, hipMemcpyDeviceToHost,
-                         d->slot->stream));
+  HIP_TRY(hipMemcpyAsync(out, d->d_row(index), d->shard_bytes, hipMemcpyDeviceToHost, d->d2h()));
+  HIP_TRY(hipEventRecord(d->slot->ev_d2h, d->d2h()));
   return d->slot->sync();
 }

@@ -100,16 +100,16 @@ static int upload_plan(Plan *p) {
 }
 
 int CodecSlot::sync() {
-  HIP_TRY(hipEventRecord(done, stream));
-  HIP_TRY(hipEventSynchronize(done));
+  // an event never recorded counts as complete
+  for (hipEvent_t e : {ev_h2d, ev_k, ev_d2h})
+    if (e) HIP_TRY(hipEventSynchronize(e));
   return BFRS_OK;
 }
 
 CodecSlot::~CodecSlot() {
-  if (done) {
-    if (stream) (void)sync();
-    (void)hipEventDestroy(done);
-  }
+  (void)sync();
+  for (hipEvent_t e : {ev_h2d, ev_k, ev_d2h})
+    if (e) (void)hipEventDestroy(e);
   if (stream && own_stream) {
     (void)hipStreamSynchronize(stream);
     (void)hipStreamDestroy(stream);
@@ -118,7 +118,11 @@ CodecSlot::~CodecSlot() {
   if (h) (void)hipHostFree(h);
 }
 
-int CodecPool::init_streams(size_t n) {
+int CodecPool::init_streams(size_t n, bool copy_streams) {
+  if (copy_streams) {
+    HIP_TRY(hipStreamCreateWithFlags(&h2d, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithFlags(&d2h, hipStreamNonBlocking));
+  }
   for (size_t i = 0; i < n; ++i) {
     hipStream_t st;
     HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
@@ -146,7 +150,9 @@ int CodecPool::acquire(size_t nshards, size_t shard_bytes, std::unique_ptr<Codec
     s->stride = stride;
     s->nshards = nshards;
     HIP_TRY(hipSetDevice(device));
-    HIP_TRY(hipEventCreateWithFlags(&s->done, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&s->ev_h2d, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&s->ev_k, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&s->ev_d2h, hipEventDisableTiming));
     if (streams.empty()) {
       HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
       s->own_stream = true;
@@ -219,6 +225,11 @@ CodecPool::~CodecPool() {
     (void)hipStreamSynchronize(st);
     (void)hipStreamDestroy(st);
   }
+  for (hipStream_t st : {h2d, d2h})
+    if (st) {
+      (void)hipStreamSynchronize(st);
+      (void)hipStreamDestroy(st);
+    }
 }
 
 Context::~Context() {
@@ -275,9 +286,17 @@ int Context::init(int dev) {
                        std::string("BFRS_CODEC_STREAMS=") + e + ": expected 0..64");
     codec_streams = size_t(v);
   }
+  bool copy_streams = true;
+  if (const char *e = std::getenv("BFRS_CODEC_COPIES")) {
+    if (std::strcmp(e, "slot") == 0)
+      copy_streams = false;
+    else if (std::strcmp(e, "stream") != 0 && *e)
+      return set_error(BFRS_E_INVALID_ARGUMENT,
+                       std::string("BFRS_CODEC_COPIES=") + e + ": expected stream or slot");
+  }
   HIP_TRY(hipSetDevice(dev));
   // the codec streams first: created before any copy, consecutively
-  if (int rc = codec_pool->init_streams(codec_streams)) return rc;
+  if (int rc = codec_pool->init_streams(codec_streams, copy_streams)) return rc;
   HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
   for (auto &ps : pipe_stream) HIP_TRY(hipStreamCreateWithFlags(&ps, hipStreamNonBlocking));
   return BFRS_OK;

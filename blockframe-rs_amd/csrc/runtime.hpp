@@ -97,12 +97,13 @@ struct CodecSlot {
   void *d = nullptr;     // nshards x stride bytes of HBM
   uint8_t *h = nullptr;  // nshards x stride bytes of pinned host memory
   size_t stride = 0, nshards = 0;
-  hipStream_t stream = nullptr;  // the pool's stream this slot runs on (or its own)
+  hipStream_t stream = nullptr;  // the pool's stream this slot's kernels run on (or its own)
   bool own_stream = false;       // BFRS_CODEC_STREAMS=0: one stream per slot
   int stream_idx = -1;           // index into CodecPool::streams while acquired
-  hipEvent_t done = nullptr;     // marks this slot's last queued operation
+  // the last H2D, kernel and D2H this slot queued (each on its own stream)
+  hipEvent_t ev_h2d = nullptr, ev_k = nullptr, ev_d2h = nullptr;
   // Waits for this slot's work queued so far (not for later work of other
-  // slots sharing the stream).
+  // slots sharing a stream).
   int sync();
   ~CodecSlot();
 };
@@ -139,7 +140,11 @@ struct CodecPool {
   size_t cached = 2;  // BFRS_CODEC_SLOTS: idle slots kept (0 = none)
   std::vector<hipStream_t> streams;  // shared codec streams (empty: one per slot)
   std::vector<int> users;            // live slots per shared stream
-  int init_streams(size_t n);
+  // BFRS_CODEC_COPIES=stream (default): every object's H2D copies go through
+  // one stream and its D2H copies through another, in FIFO order, and the
+  // kernels wait on events; =slot: copies on the object's own kernel stream
+  hipStream_t h2d = nullptr, d2h = nullptr;
+  int init_streams(size_t n, bool copy_streams);
   int acquire(size_t nshards, size_t shard_bytes, std::unique_ptr<CodecSlot> *out);
   void release(std::unique_ptr<CodecSlot> slot);
   ~CodecPool();

@@ -42,6 +42,14 @@
  *                       (default 4, created with the context; an object takes
  *                       the one with the fewest live objects); 0 = one stream
  *                       per slot, as in rounds 2-3
+ *   BFRS_CODEC_COPIES   "stream" (default: every codec object's H2D copies go
+ *                       through one stream of the context and its D2H copies
+ *                       through another, in FIFO order; kernels wait on
+ *                       per-object events) or "slot" (copies on the object's
+ *                       kernel stream, rounds 2-3)
+ *   BFRS_PREFAULT_OUTPUTS  1 (default): bfrs_generate_parity faults the caller's
+ *                       output pages in on helper threads while the device
+ *                       works; 0: the copy-out faults them
  *   BFRS_CODEC_STAGING  "pinned" (default: add_*_shard copies into a pinned
  *                       row on several threads and queues its H2D) or
  *                       "direct" (one DMA straight from the caller's buffer);
