@@ -1100,8 +1100,13 @@ def blake3_device(ctx, sets, calls=10):
         check = {"golden": "tests/golden/blake3_c2.json", "digests": len(hexes),
                  "mismatched": bad, "match": not bad}
     best = min(ts)
+    kern = blake3_kernel_times(ctx, rows)
+    if "group_kernel_ms" in kern:
+        kern["frac_group_kernel"] = round(
+            nbytes / (kern["group_kernel_ms"] * 1e-3) / 1e9 / b3_ceiling_gbps(B3_VALU_PER_64B_ALG), 4)
     return {"GBps": round(nbytes / best / 1e9, 1), "ms": round(best * 1e3, 3),
             "mean_ms": round(sum(ts) / len(ts) * 1e3, 3), "bytes": nbytes,
+            "kernels": kern,
             "roofline": {"bound": "valu", "achieved": round(nbytes / best / 1e9, 1),
                          "peak": round(b3_ceiling_gbps(B3_VALU_PER_64B_ALG), 1), "unit": "GB/s",
                          "frac": round(nbytes / best / 1e9 / b3_ceiling_gbps(B3_VALU_PER_64B_ALG), 4),
@@ -1115,6 +1120,36 @@ def blake3_device(ctx, sets, calls=10):
             "parity_check": check,
             "what": "bfrs_blake3_batch_dev over C2's 128 x 32 MiB data segments in HBM, one call "
                     "(upload + kernels + digest download), best of 10 wall-clock calls"}
+
+
+def blake3_kernel_times(ctx, rows, calls=3):
+    """Kernel time inside bfrs_blake3_batch_dev (torch's profiler, kineto over
+    the ROCm tracer, in this process): per call, the group kernel and the
+    reduce kernels, so the call's wall time splits into device work and the
+    host side (descriptors, launches, digest download)."""
+    import statistics
+    import torch
+    try:
+        from torch.autograd import DeviceType
+        from torch.profiler import ProfilerActivity, profile
+        if ProfilerActivity.CUDA not in torch.profiler.supported_activities():
+            return {"error": "torch profiler has no GPU activity on this build"}
+        ctx.blake3_batch_dev(rows)
+        with profile(activities=[ProfilerActivity.CUDA]) as prof:
+            for _ in range(calls):
+                ctx.blake3_batch_dev(rows)
+        ev = [(e.name(), e.duration_ns() / 1e6) for e in prof.profiler.kineto_results.events()
+              if e.device_type() == DeviceType.CUDA and "blake3" in e.name()]
+        group = [d for n, d in ev if "group" in n]
+        reduce_ = [d for n, d in ev if "reduce" in n]
+        if len(group) < calls:
+            return {"error": f"trace holds {len(group)} group-kernel dispatches"}
+        return {"group_kernel_ms": round(statistics.median(group), 4),
+                "reduce_kernels_ms_per_call": round(sum(reduce_) / calls, 4),
+                "reduce_launches_per_call": len(reduce_) // calls,
+                "how": f"torch.profiler over {calls} calls in this process"}
+    except Exception as e:  # noqa: BLE001 - informative only
+        return {"error": f"{type(e).__name__}: {e}"}
 
 
 def pinned_host_state(rt):
