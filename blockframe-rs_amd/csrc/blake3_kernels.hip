@@ -214,12 +214,38 @@ __device__ __forceinline__ void pair_down(uint32_t *buf0, uint32_t *buf1, uint32
   }
 }
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void blake3_group_kernel(const HashGroup *__restrict__ groups,
-                                                           uint32_t *__restrict__ group_cvs,
-                                                           uint32_t *__restrict__ msg_cvs,
-                                                           uint32_t *__restrict__ digests) {
+// Workgroup w's group: the message whose group range holds w (binary search
+// over first_group, uniform across the workgroup), then its offset in it.
+struct Group {
+  uint64_t addr, chunk0;
+  uint32_t nbytes, msg, single;
+};
+__device__ __forceinline__ Group find_group(const HashMsg *__restrict__ msgs, uint32_t n_msgs,
+                                            uint32_t w) {
+  uint32_t lo = 0, hi = n_msgs - 1;  // the last message with first_group <= w
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi + 1) / 2;
+    if (msgs[mid].first_group <= w) lo = mid;
+    else hi = mid - 1;
+  }
+  const HashMsg m = msgs[lo];
+  const uint32_t g = w - m.first_group;
+  const uint64_t off = uint64_t(g) * kGroupBytes;
+  const uint64_t rem = m.nbytes - off;
+  Group r;
+  r.addr = m.addr + off;
+  r.chunk0 = m.chunk0 + uint64_t(g) * kGroupChunks;
+  r.nbytes = uint32_t(m.nbytes == 0 ? 0 : (rem < kGroupBytes ? rem : kGroupBytes));
+  r.msg = lo;
+  r.single = m.groups == 1;
+  return r;
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void blake3_group_kernel(
+    const HashMsg *__restrict__ msgs, uint32_t n_msgs, uint32_t *__restrict__ group_cvs,
+    uint32_t *__restrict__ msg_cvs, uint32_t *__restrict__ digests) {
   __shared__ uint32_t lds[2][256 * kRow];
-  const HashGroup g = groups[blockIdx.x];
+  const Group g = find_group(msgs, n_msgs, blockIdx.x);
   const uint32_t t = threadIdx.x;
   const uint32_t nchunks = g.nbytes == 0 ? 1 : (g.nbytes + kChunkBytes - 1) / kChunkBytes;
   uint32_t cv[8];
@@ -301,10 +327,11 @@ __global__ __launch_bounds__(256) void blake3_reduce_kernel(const HashReduce *__
 
 }  // namespace
 
-hipError_t launch_blake3_groups(const HashGroup *d_groups, uint32_t n_groups, uint32_t *d_group_cvs,
-                                uint32_t *d_msg_cvs, uint32_t *d_digests, hipStream_t stream) {
-  if (n_groups == 0) return hipSuccess;
-  hipLaunchKernelGGL(blake3_group_kernel, dim3(n_groups), dim3(256), 0, stream, d_groups,
+hipError_t launch_blake3_groups(const HashMsg *d_msgs, uint32_t n_msgs, uint32_t n_groups,
+                                uint32_t *d_group_cvs, uint32_t *d_msg_cvs, uint32_t *d_digests,
+                                hipStream_t stream) {
+  if (n_groups == 0 || n_msgs == 0) return hipSuccess;
+  hipLaunchKernelGGL(blake3_group_kernel, dim3(n_groups), dim3(256), 0, stream, d_msgs, n_msgs,
                      d_group_cvs, d_msg_cvs, d_digests);
   return hipGetLastError();
 }

@@ -26,27 +26,24 @@ int Context::blake3_dev(size_t n, const uint8_t *const *d_msgs, const size_t *le
   std::lock_guard<std::mutex> hash_lock(hash_mu);
   HIP_TRY(hipSetDevice(device));
 
-  // kernel-1 groups (messages in order, groups of a message contiguous)
-  std::vector<HashGroup> groups;
+  // kernel-1 workgroups: messages in order, groups of a message contiguous;
+  // one descriptor per message (the kernel finds its message by group index)
+  std::vector<HashMsg> msgs(n);
   std::vector<uint32_t> g_first(n), g_count(n);
+  size_t n_groups = 0;
   for (size_t i = 0; i < n; ++i) {
     if (lens[i] && !d_msgs[i])
       return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_blake3_batch_dev: NULL message");
     if (reinterpret_cast<uintptr_t>(d_msgs[i]) % 16)
       return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_blake3_batch_dev: message not 16-byte aligned");
     const size_t ng = lens[i] == 0 ? 1 : (lens[i] + kGroupBytes - 1) / kGroupBytes;
-    g_first[i] = uint32_t(groups.size());
+    if (n_groups + ng > (size_t(1) << 31))
+      return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_blake3_batch_dev: batch too large");
+    g_first[i] = uint32_t(n_groups);
     g_count[i] = uint32_t(ng);
-    for (size_t g = 0; g < ng; ++g) {
-      HashGroup h{};
-      h.addr = reinterpret_cast<uint64_t>(d_msgs[i]) + uint64_t(g) * kGroupBytes;
-      h.chunk0 = (chunk_offsets ? chunk_offsets[i] : 0) + uint64_t(g) * kGroupChunks;
-      const size_t rem = lens[i] - g * size_t(kGroupBytes);
-      h.nbytes = uint32_t(lens[i] == 0 ? 0 : (rem < kGroupBytes ? rem : kGroupBytes));
-      h.msg = uint32_t(i);
-      h.single = ng == 1;
-      groups.push_back(h);
-    }
+    msgs[i] = HashMsg{reinterpret_cast<uint64_t>(d_msgs[i]), chunk_offsets ? chunk_offsets[i] : 0,
+                      uint64_t(lens[i]), uint32_t(n_groups), uint32_t(ng)};
+    n_groups += ng;
   }
   // reduction levels: level L's nodes of message i are cur[off[i], off[i]+cnt[i]).
   // Kernel 1 leaves a multi-group message's level-2 nodes (kGroupOut per full
@@ -91,15 +88,15 @@ int Context::blake3_dev(size_t n, const uint8_t *const *d_msgs, const size_t *le
     if (!more) break;
   }
 
-  // device layout: groups | jobs (all levels) | cvA | cvB | msg_cvs | digests
+  // device layout: msgs | jobs (all levels) | cvA | cvB | msg_cvs | digests
   size_t njobs = 0;
   for (auto &l : levels) njobs += l.size();
-  const size_t b_groups = align_up(groups.size() * sizeof(HashGroup), 256);
+  const size_t b_groups = align_up(n * sizeof(HashMsg), 256);
   const size_t b_jobs = align_up(njobs * sizeof(HashReduce) + 16, 256);
   // cvA holds kernel 1's level-2 nodes (and later levels in place); cvB the
   // first reduce level's outputs, <= one per kReduceFanIn nodes per message
-  const size_t b_cv = align_up(groups.size() * kGroupOut * 32, 256);
-  const size_t b_cv1 = align_up((groups.size() * kGroupOut / kReduceFanIn + n + 1) * 32, 256);
+  const size_t b_cv = align_up(n_groups * kGroupOut * 32, 256);
+  const size_t b_cv1 = align_up((n_groups * kGroupOut / kReduceFanIn + n + 1) * 32, 256);
   const size_t b_out = align_up(n * 32, 256);
   const size_t need = b_groups + b_jobs + b_cv + b_cv1 + 2 * b_out;
   const size_t h_need = b_groups + b_jobs + 2 * b_out;
@@ -125,21 +122,22 @@ int Context::blake3_dev(size_t n, const uint8_t *const *d_msgs, const size_t *le
   }
   uint8_t *d = static_cast<uint8_t *>(d_hash);
   uint8_t *h = static_cast<uint8_t *>(h_hash);
-  auto *d_groups = reinterpret_cast<HashGroup *>(d);
+  auto *d_hmsgs = reinterpret_cast<HashMsg *>(d);
   auto *d_jobs = reinterpret_cast<HashReduce *>(d + b_groups);
   auto *d_cv0 = reinterpret_cast<uint32_t *>(d + b_groups + b_jobs);
   auto *d_cv1 = reinterpret_cast<uint32_t *>(d + b_groups + b_jobs + b_cv);
   auto *d_msg_cvs = reinterpret_cast<uint32_t *>(d + b_groups + b_jobs + b_cv + b_cv1);
   auto *d_digests = reinterpret_cast<uint32_t *>(d + b_groups + b_jobs + b_cv + b_cv1 + b_out);
   // descriptors through pinned memory (one async copy)
-  std::memcpy(h, groups.data(), groups.size() * sizeof(HashGroup));
+  std::memcpy(h, msgs.data(), n * sizeof(HashMsg));
   size_t jo = 0;
   for (auto &l : levels) {
     std::memcpy(h + b_groups + jo * sizeof(HashReduce), l.data(), l.size() * sizeof(HashReduce));
     jo += l.size();
   }
   HIP_TRY(hipMemcpyAsync(d, h, b_groups + b_jobs, hipMemcpyHostToDevice, s));
-  HIP_TRY(launch_blake3_groups(d_groups, uint32_t(groups.size()), d_cv0, d_msg_cvs, d_digests, s));
+  HIP_TRY(launch_blake3_groups(d_hmsgs, uint32_t(n), uint32_t(n_groups), d_cv0, d_msg_cvs,
+                               d_digests, s));
   uint32_t *cur = d_cv0, *nxt = d_cv1;
   jo = 0;
   for (auto &l : levels) {

@@ -20,17 +20,19 @@ constexpr uint32_t kReduceFanIn = 512;                  // CVs one kernel-2 work
 constexpr uint32_t kGroupLevels = 2;
 constexpr uint32_t kGroupOut = kGroupChunks >> kGroupLevels;  // level-2 nodes per full group
 
-// One kernel-1 workgroup: <= 256 KiB of one message, starting at a 256 KiB
-// aligned offset (so its chunks form an aligned subtree of the message).  A
-// single-group message is finished in kernel 1; a group of a longer message
-// writes its ceil(chunks / 4) level-2 nodes to group_cvs[kGroupOut * index].
-struct alignas(16) HashGroup {
-  uint64_t addr;    // device address of the group's first byte (16-byte aligned)
-  uint64_t chunk0;  // BLAKE3 chunk counter of its first chunk
-  uint32_t nbytes;  // bytes in the group (0 only for an empty message)
-  uint32_t msg;     // message index (digest / CV slot)
-  uint32_t single;  // 1: the group is the whole message -> finalise in kernel 1
-  uint32_t pad;
+// One message of a kernel-1 launch.  Workgroup w belongs to the message m
+// with first_group(m) <= w < first_group(m + 1) (found by a binary search in
+// the kernel, so the host uploads one descriptor per message, not per group)
+// and hashes <= 256 KiB of it starting at a 256 KiB aligned offset (so its
+// chunks form an aligned subtree of the message).  A single-group message is
+// finished in kernel 1; a group of a longer message writes its ceil(chunks /
+// 4) level-2 nodes to group_cvs[kGroupOut * w].
+struct alignas(16) HashMsg {
+  uint64_t addr;         // device address of the message (16-byte aligned)
+  uint64_t chunk0;       // BLAKE3 chunk counter of its first chunk
+  uint64_t nbytes;       // message length
+  uint32_t first_group;  // its first workgroup
+  uint32_t groups;       // its workgroups (an empty message has one)
 };
 
 // One kernel-2 workgroup: CVs in_cvs[first, first + n) of message `msg`.
@@ -41,8 +43,9 @@ struct alignas(16) HashReduce {
   uint32_t msg, pad[3];
 };
 
-hipError_t launch_blake3_groups(const HashGroup *d_groups, uint32_t n_groups, uint32_t *d_group_cvs,
-                                uint32_t *d_msg_cvs, uint32_t *d_digests, hipStream_t stream);
+hipError_t launch_blake3_groups(const HashMsg *d_msgs, uint32_t n_msgs, uint32_t n_groups,
+                                uint32_t *d_group_cvs, uint32_t *d_msg_cvs, uint32_t *d_digests,
+                                hipStream_t stream);
 hipError_t launch_blake3_reduce(const HashReduce *d_jobs, uint32_t n_jobs, const uint32_t *d_in,
                                 uint32_t *d_out, uint32_t *d_msg_cvs, uint32_t *d_digests,
                                 hipStream_t stream);
