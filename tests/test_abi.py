@@ -65,8 +65,8 @@ PRODUCT_KERNELS = {
     "void bfrs::(anonymous namespace)::gf_apply_ring_kernel<6, false, 16u, 1, 1, 1, 0>(bfrs::KernArgs)",
     "bfrs::(anonymous namespace)::gf_tail_kernel(bfrs::KernArgs)",
     # device BLAKE3 (the Merkle re-verify of the read/repair path)
-    "bfrs::(anonymous namespace)::blake3_group_kernel(bfrs::HashGroup const*, unsigned int*, "
-    "unsigned int*, unsigned int*)",
+    "bfrs::(anonymous namespace)::blake3_group_kernel(bfrs::HashMsg const*, unsigned int, "
+    "unsigned int*, unsigned int*, unsigned int*)",
     "bfrs::(anonymous namespace)::blake3_reduce_kernel(bfrs::HashReduce const*, unsigned int const*, "
     "unsigned int*, unsigned int*, unsigned int*)",
 }
