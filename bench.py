@@ -1152,6 +1152,25 @@ def blake3_kernel_times(ctx, rows, calls=3):
         return {"error": f"{type(e).__name__}: {e}"}
 
 
+def host_pressure():
+    """Load on the host this run shares with the other GPUs' jobs: the load
+    average and the kernel's pressure-stall figures (PSI, % of the last 10 s
+    some task waited for CPU / memory / IO), where the host exposes them."""
+    out = {}
+    try:
+        out["loadavg_1m"] = round(os.getloadavg()[0], 2)
+    except OSError:
+        pass
+    for res in ("cpu", "memory", "io"):
+        try:
+            for line in open(f"/proc/pressure/{res}"):
+                if line.startswith("some"):
+                    out[f"psi_{res}_some_avg10"] = float(line.split()[1].split("=")[1])
+        except (OSError, ValueError, IndexError):
+            pass
+    return out
+
+
 def pinned_host_state(rt):
     """Pinned host memory this process holds at the time (torch's caching host
     allocator: pinned buffers it keeps after they are freed)."""
@@ -1904,9 +1923,11 @@ def main(argv=None):
         if os.environ.get("BENCH_HOST_EMPTY_CACHE") == "1" and not rt.stub:
             rt.torch._C._host_emptyCache()  # A/B: give torch's cached pinned blocks back first
             host_pinned["after_empty_cache"] = pinned_host_state(rt)
+        load_before = host_pressure()
         crate = legs.run("crate_api", crate_api, ctx, sets)
         if isinstance(crate, dict) and "error" not in crate:
             crate["pinned_host_before"] = host_pinned
+            crate["host_pressure"] = {"before": load_before, "after": host_pressure()}
         if rayon_child is not None and "error" not in crate:
             crate["generate_parity_all_blocks_fresh_process"] = rayon_child
     if solo_legs and args.cpu_baseline == "auto":

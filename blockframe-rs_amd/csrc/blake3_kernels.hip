@@ -279,7 +279,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
     pair_down<1>(lds[0], lds[1], nchunks, true, nullptr, msg_cvs + 8 * g.msg, digests + 8 * g.msg);
     return;
   }
-  // kGroupLevels levels (256 -> 64 nodes); an odd last node is carried up
+  // kGroupLevels levels (256 -> 32 nodes); an odd last node is carried up
   uint32_t n = nchunks, *src = lds[0], *dst = lds[1];
 #pragma unroll
   for (uint32_t lv = 0; lv < kGroupLevels; ++lv) {

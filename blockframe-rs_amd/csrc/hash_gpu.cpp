@@ -46,8 +46,9 @@ int Context::blake3_dev(size_t n, const uint8_t *const *d_msgs, const size_t *le
     n_groups += ng;
   }
   // reduction levels: level L's nodes of message i are cur[off[i], off[i]+cnt[i]).
-  // Kernel 1 leaves a multi-group message's level-2 nodes (kGroupOut per full
-  // group, ceil(chunks / 4) for its last one) at group index * kGroupOut.
+  // Kernel 1 leaves a multi-group message's level-kGroupLevels nodes
+  // (kGroupOut per full group, ceil(chunks / 2^kGroupLevels) for its last
+  // one) at group index * kGroupOut.
   std::vector<std::vector<HashReduce>> levels;
   std::vector<uint32_t> cnt(n), off(n);
   for (size_t i = 0; i < n; ++i) {

@@ -12,13 +12,15 @@ constexpr uint32_t kGroupChunks = 256;                  // chunks per workgroup 
 constexpr uint32_t kGroupBytes = kChunkBytes * kGroupChunks;
 constexpr uint32_t kReduceFanIn = 512;                  // CVs one kernel-2 workgroup pairs down
 // Tree levels kernel 1 pairs inside a group of a multi-group message: 256
-// chunk CVs -> 64 level-2 nodes (4 KiB subtrees), written out for kernel 2.
-// Those two levels use every active lane; the upper levels of a group use a
-// fraction of a wave (128 -> 1 nodes: 9 wave-compressions for 255 parents),
-// so they are left to kernel 2, whose first levels over 512 nodes use every
-// lane too.
-constexpr uint32_t kGroupLevels = 2;
-constexpr uint32_t kGroupOut = kGroupChunks >> kGroupLevels;  // level-2 nodes per full group
+// chunk CVs -> 32 level-3 nodes (8 KiB subtrees), written out for kernel 2.
+// Levels 1-2 use every active lane and level 3 half a wave (32 slots idle per
+// group, 0.8% of the group's work); the upper levels of a group would use a
+// fraction of a wave (16 -> 1 nodes: 5 wave-compressions for 31 parents), so
+// they are left to kernel 2, whose first levels over 512 nodes use every
+// lane.  Three levels rather than two also halve kernel 2's first-level jobs,
+// which then fit the chip in one round.
+constexpr uint32_t kGroupLevels = 3;
+constexpr uint32_t kGroupOut = kGroupChunks >> kGroupLevels;  // level-3 nodes per full group
 
 // One message of a kernel-1 launch.  Workgroup w belongs to the message m
 // with first_group(m) <= w < first_group(m + 1) (found by a binary search in
@@ -26,7 +28,7 @@ constexpr uint32_t kGroupOut = kGroupChunks >> kGroupLevels;  // level-2 nodes p
 // and hashes <= 256 KiB of it starting at a 256 KiB aligned offset (so its
 // chunks form an aligned subtree of the message).  A single-group message is
 // finished in kernel 1; a group of a longer message writes its ceil(chunks /
-// 4) level-2 nodes to group_cvs[kGroupOut * w].
+// 8) level-3 nodes to group_cvs[kGroupOut * w].
 struct alignas(16) HashMsg {
   uint64_t addr;         // device address of the message (16-byte aligned)
   uint64_t chunk0;       // BLAKE3 chunk counter of its first chunk

@@ -277,7 +277,10 @@ int Context::init(int dev) {
       return set_error(BFRS_E_INVALID_ARGUMENT,
                        std::string("BFRS_CODEC_STAGING=") + e + ": expected direct or pinned");
   }
-  size_t codec_streams = 4;
+  // defaults: one stream per slot, copies on it (rounds 2-3); the shared
+  // stream set and the FIFO copy streams are kept as options: neither was
+  // consistently faster in the bench process
+  size_t codec_streams = 0;
   if (const char *e = std::getenv("BFRS_CODEC_STREAMS")) {
     char *end = nullptr;
     const long v = std::strtol(e, &end, 10);
@@ -286,11 +289,11 @@ int Context::init(int dev) {
                        std::string("BFRS_CODEC_STREAMS=") + e + ": expected 0..64");
     codec_streams = size_t(v);
   }
-  bool copy_streams = true;
+  bool copy_streams = false;
   if (const char *e = std::getenv("BFRS_CODEC_COPIES")) {
-    if (std::strcmp(e, "slot") == 0)
-      copy_streams = false;
-    else if (std::strcmp(e, "stream") != 0 && *e)
+    if (std::strcmp(e, "stream") == 0)
+      copy_streams = true;
+    else if (std::strcmp(e, "slot") != 0 && *e)
       return set_error(BFRS_E_INVALID_ARGUMENT,
                        std::string("BFRS_CODEC_COPIES=") + e + ": expected stream or slot");
   }

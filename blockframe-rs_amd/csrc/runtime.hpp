@@ -125,13 +125,14 @@ enum class Staging { kDirect, kPinned };
 // every live codec object, so an object freed after bfrs_close still returns
 // or frees its slot safely; the pool goes away with the last of them.
 //
-// Streams (round 4): the slots of a context run on a small fixed set of
-// streams created with the context (BFRS_CODEC_STREAMS, default 4 = the HIP
-// runtime's default hardware-queue count per process); an acquired slot takes
-// the stream with the fewest live slots.  One stream per slot (=0, rounds
-// 2-3) let the stream count grow with the slot pool, and concurrent objects'
-// streams then shared hardware queues in whatever pattern their creation
-// order gave.
+// Streams (round 4): by default every slot has a stream
+// of its own and runs its copies and kernel on it (rounds 2-3).
+// BFRS_CODEC_STREAMS=n > 0 instead shares n streams created with the
+// context (an acquired slot takes the one with the fewest live slots), and
+// BFRS_CODEC_COPIES=stream sends every object's H2D / D2H through two FIFO
+// copy streams with the kernels waiting on per-slot events.  Measured in the
+// bench process over two boxes, neither option was consistently faster than
+// one stream per slot, so they stay options.
 struct CodecPool {
   int device = 0;
   Staging staging = Staging::kPinned;

@@ -20,8 +20,8 @@
  * how rayon's one-encoder-per-block use (src/chunker/commit.rs:391-466) maps
  * onto it.  Encoder/decoder objects and the batch calls may run concurrently
  * on one context: each codec object owns a pooled slot (device rows, pinned
- * rows) and runs on one of the context's codec streams, the plan cache and
- * the slot pool are locked, the
+ * rows, a HIP stream unless BFRS_CODEC_STREAMS shares a set), the plan cache
+ * and the slot pool are locked, the
  * host-batch pipeline and the BLAKE3 work area are serialised.  A single
  * encoder or decoder object is used by one thread at a time (as the crate's
  * &mut self API implies).  A context keeps at most BFRS_CODEC_SLOTS idle codec
@@ -38,15 +38,15 @@
  * Environment, read by bfrs_open (BFRS_HOST_COPY_* on first use, once per
  * process):
  *   BFRS_CODEC_SLOTS    idle codec slots kept (default 2; 0 = none)
- *   BFRS_CODEC_STREAMS  HIP streams the codec objects of a context share
- *                       (default 4, created with the context; an object takes
- *                       the one with the fewest live objects); 0 = one stream
- *                       per slot, as in rounds 2-3
- *   BFRS_CODEC_COPIES   "stream" (default: every codec object's H2D copies go
- *                       through one stream of the context and its D2H copies
- *                       through another, in FIFO order; kernels wait on
- *                       per-object events) or "slot" (copies on the object's
- *                       kernel stream, rounds 2-3)
+ *   BFRS_CODEC_STREAMS  0 (default): one HIP stream per codec slot; n > 0:
+ *                       the codec objects of a context share n streams
+ *                       created with it (an object takes the one with the
+ *                       fewest live objects)
+ *   BFRS_CODEC_COPIES   "slot" (default: an object's copies run on its own
+ *                       stream) or "stream" (every codec object's H2D copies
+ *                       go through one stream of the context and its D2H
+ *                       copies through another, in FIFO order; kernels wait
+ *                       on per-object events)
  *   BFRS_PREFAULT_OUTPUTS  1 (default): bfrs_generate_parity faults the caller's
  *                       output pages in on helper threads while the device
  *                       works; 0: the copy-out faults them

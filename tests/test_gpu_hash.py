@@ -13,10 +13,10 @@ G = 256 * K  # kernel-1 group
 LENS = [0, 1, 63, 64, 65, 1023, 1024, 1025, 2047, 2048, 3000, 64 * K + 1, G - 1, G, G + 1,
         2 * G + 5, 1 << 20, (32 << 20) + 77, 32 << 20,
         512 * G, 512 * G + 1, 513 * G + 1000,  # 512+ groups: multi-level reduction
-        # kernel 1 leaves 4-chunk (level-2) nodes of multi-group messages to
-        # kernel 2: last groups of 4+1 and 5 chunks, exactly one 512-node run,
-        # one run + 1 node
-        G + 4 * K + 1, G + 5 * K, 8 * G, 8 * G + 2 * K]
+        # kernel 1 leaves 8-chunk (level-3) nodes of multi-group messages to
+        # kernel 2: last groups of 4+1, 5, 8+1 and 9 chunks, exactly one
+        # 512-node run, one run + 1 node
+        G + 4 * K + 1, G + 5 * K, G + 8 * K + 1, G + 9 * K, 16 * G, 16 * G + 2 * K]
 
 
 def _dev(a):
