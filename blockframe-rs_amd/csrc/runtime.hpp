@@ -232,6 +232,8 @@ struct bfrs_ctx {
 };
 
 namespace bfrs {
+// [p, p + n) lies inside a range registered with bfrs_host_register.
+bool host_registered(const void *p, size_t n);
 // Pointer and shape checks of the host-memory batch API (one block list).
 int check_host_batch(bfrs_ctx *ctx, size_t nblocks, const uint32_t *ks, size_t m,
                      size_t shard_bytes, bool decode, const uint8_t *const *orig,

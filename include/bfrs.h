@@ -125,6 +125,17 @@ int bfrs_synchronize(bfrs_ctx *ctx);
  * one column of all of them together; a pitch = 12 KiB (mod 64 KiB) spreads
  * them (measured 0.8-5% faster).  Smaller shards: rounded up to 256 B. */
 size_t bfrs_shard_pitch(size_t shard_bytes);
+/* Page-locks a host range the caller keeps for a while -- BlockFrame's mmap
+ * of the file being committed (src/chunker/commit.rs:355-360), or its
+ * segment buffers -- so that codec objects and the wrappers DMA shards that
+ * lie inside it straight to the device, instead of copying them through the
+ * slot's pinned rows first (no reference counterpart; the crate copies every
+ * added shard too).  add_*_shard still returns only when the shard is on the
+ * device, so the caller may reuse its buffer at once.  Process-wide (HIP
+ * registration, any context); unregister before unmapping or freeing the
+ * range.  BFRS_E_HIP if the runtime refuses the range. */
+int bfrs_host_register(void *ptr, size_t len);
+int bfrs_host_unregister(void *ptr);
 
 /* ---- codec rules (pure host logic) ------------------------------------ */
 /* 1 = HighRate, 0 = LowRate (reed-solomon-simd DefaultRate), <0 = unsupported. */

@@ -785,3 +785,41 @@ def test_mixed_entry_points_share_one_context_across_threads(ctx, bfrs, oracle):
     for t in ts:
         t.join(timeout=180)
     assert not errors, errors
+
+
+def test_registered_inputs_dma_straight_and_match(bfrs, oracle):
+    """bfrs_host_register: shards inside a registered range go to the device
+    by DMA straight from it (no staging copy); the bytes equal the oracle's
+    through the wrappers and the objects, the caller may overwrite its buffer
+    as soon as add returns, and the registry refuses overlaps and unknown
+    ranges."""
+    c = bfrs.Context(0)
+    rng = np.random.default_rng(33)
+    n = (1 << 20) + 64 * 5
+    data = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(30)]
+    want = [r.tobytes() for r in oracle.encode(data, 3)]
+    big = np.concatenate(data)  # one registered range, shards are slices of it
+    bfrs.host_register(big)
+    try:
+        segs = [big[i * n:(i + 1) * n] for i in range(30)]
+        outs = [np.empty(n, np.uint8) for _ in range(3)]
+        assert bfrs.Chunker(c).generate_parity_into(segs, 30, 3, outs) == n
+        assert [o.tobytes() for o in outs] == want
+        enc = bfrs.ReedSolomonEncoder(c, 30, 3, n)
+        scratch = big[:n]  # reused between adds: DMA done before add returns
+        for d in data:
+            scratch[:] = d
+            enc.add_original_shard(scratch)
+        assert list(enc.encode().recovery_iter()) == want
+        del enc
+        slots = [None if i in (4, 20) else big[i * n:(i + 1) * n] for i in range(30)]
+        big[:n] = data[0]
+        par = [np.frombuffer(p, np.uint8) for p in want]
+        assert bfrs.recover_segment_rs30_3(c, slots, par, 20) == data[20].tobytes()
+        with pytest.raises(bfrs.BfrsError):
+            bfrs.host_register(big[n:2 * n])  # overlaps the registered range
+    finally:
+        bfrs.host_unregister(big)
+    with pytest.raises(bfrs.BfrsError):
+        bfrs.host_unregister(big)
+    c.close()
