@@ -241,6 +241,7 @@ __device__ __forceinline__ Group find_group(const HashMsg *__restrict__ msgs, ui
   return r;
 }
 
+template <uint32_t kLevels>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void blake3_group_kernel(
     const HashMsg *__restrict__ msgs, uint32_t n_msgs, uint32_t *__restrict__ group_cvs,
     uint32_t *__restrict__ msg_cvs, uint32_t *__restrict__ digests) {
@@ -279,10 +280,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
     pair_down<1>(lds[0], lds[1], nchunks, true, nullptr, msg_cvs + 8 * g.msg, digests + 8 * g.msg);
     return;
   }
-  // kGroupLevels levels (256 -> 32 nodes); an odd last node is carried up
+  // kLevels levels (256 -> 256 >> kLevels nodes); an odd last node is carried up
   uint32_t n = nchunks, *src = lds[0], *dst = lds[1];
 #pragma unroll
-  for (uint32_t lv = 0; lv < kGroupLevels; ++lv) {
+  for (uint32_t lv = 0; lv < kLevels; ++lv) {
     const uint32_t half = (n + 1) / 2;
     if (t < half) {
       uint32_t r[8];
@@ -302,7 +303,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
     n = half;
   }
   if (t < n) {
-    uint32_t *o = group_cvs + 8 * (size_t(blockIdx.x) * kGroupOut + t);
+    uint32_t *o = group_cvs + 8 * (size_t(blockIdx.x) * (kGroupChunks >> kLevels) + t);
 #pragma unroll
     for (int w = 0; w < 8; ++w) o[w] = src[t * kRow + w];
   }
@@ -328,11 +329,17 @@ __global__ __launch_bounds__(256) void blake3_reduce_kernel(const HashReduce *__
 }  // namespace
 
 hipError_t launch_blake3_groups(const HashMsg *d_msgs, uint32_t n_msgs, uint32_t n_groups,
-                                uint32_t *d_group_cvs, uint32_t *d_msg_cvs, uint32_t *d_digests,
-                                hipStream_t stream) {
+                                uint32_t levels, uint32_t *d_group_cvs, uint32_t *d_msg_cvs,
+                                uint32_t *d_digests, hipStream_t stream) {
   if (n_groups == 0 || n_msgs == 0) return hipSuccess;
-  hipLaunchKernelGGL(blake3_group_kernel, dim3(n_groups), dim3(256), 0, stream, d_msgs, n_msgs,
-                     d_group_cvs, d_msg_cvs, d_digests);
+  if (levels == 2)
+    hipLaunchKernelGGL(blake3_group_kernel<2>, dim3(n_groups), dim3(256), 0, stream, d_msgs, n_msgs,
+                       d_group_cvs, d_msg_cvs, d_digests);
+  else if (levels == 3)
+    hipLaunchKernelGGL(blake3_group_kernel<3>, dim3(n_groups), dim3(256), 0, stream, d_msgs, n_msgs,
+                       d_group_cvs, d_msg_cvs, d_digests);
+  else
+    return hipErrorInvalidValue;
   return hipGetLastError();
 }
 

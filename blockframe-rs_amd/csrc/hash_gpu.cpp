@@ -1,6 +1,7 @@
 // hash_gpu.cpp — host side of the device BLAKE3 (blake3_kernels.hip):
 // splits messages into 256 KiB groups, plans the CV reduction levels, and
 // exposes bfrs_blake3_batch_dev / bfrs_blake3_combine.
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -12,6 +13,12 @@ namespace bfrs {
 
 namespace {
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+// Tree levels kernel 1 pairs in a group of a multi-group message
+// (hash_kernels.hpp); BFRS_B3_GROUP_LEVELS = 2 or 3, read per call (A/B).
+uint32_t group_levels() {
+  const char *e = std::getenv("BFRS_B3_GROUP_LEVELS");
+  return e && std::strcmp(e, "2") == 0 ? 2 : e && std::strcmp(e, "3") == 0 ? 3 : kGroupLevels;
+}
 }  // namespace
 
 int Context::blake3_dev(size_t n, const uint8_t *const *d_msgs, const size_t *lens,
@@ -47,10 +54,11 @@ int Context::blake3_dev(size_t n, const uint8_t *const *d_msgs, const size_t *le
   }
   // reduction levels: level L's nodes of message i are cur[off[i], off[i]+cnt[i]).
   // Kernel 1 leaves a multi-group message's level-kGroupLevels nodes
-  // (kGroupOut per full group, ceil(chunks / 2^kGroupLevels) for its last
-  // one) at group index * kGroupOut.
+  // (256 >> levels per full group, ceil(chunks / 2^levels) for its last
+  // one) at group index * (256 >> levels).
   std::vector<std::vector<HashReduce>> levels;
   std::vector<uint32_t> cnt(n), off(n);
+  const uint32_t glv = group_levels(), group_out = kGroupChunks >> glv;
   for (size_t i = 0; i < n; ++i) {
     if (g_count[i] == 1) {  // finalised by kernel 1
       cnt[i] = 1;
@@ -58,9 +66,9 @@ int Context::blake3_dev(size_t n, const uint8_t *const *d_msgs, const size_t *le
     }
     const size_t last = lens[i] - size_t(g_count[i] - 1) * kGroupBytes;
     const uint32_t last_nodes =
-        uint32_t(((last + kChunkBytes - 1) / kChunkBytes + (1u << kGroupLevels) - 1) >> kGroupLevels);
-    off[i] = g_first[i] * kGroupOut;
-    cnt[i] = (g_count[i] - 1) * kGroupOut + last_nodes;
+        uint32_t(((last + kChunkBytes - 1) / kChunkBytes + (1u << glv) - 1) >> glv);
+    off[i] = g_first[i] * group_out;
+    cnt[i] = (g_count[i] - 1) * group_out + last_nodes;
   }
   for (;;) {
     std::vector<HashReduce> jobs;
@@ -96,8 +104,8 @@ int Context::blake3_dev(size_t n, const uint8_t *const *d_msgs, const size_t *le
   const size_t b_jobs = align_up(njobs * sizeof(HashReduce) + 16, 256);
   // cvA holds kernel 1's level-2 nodes (and later levels in place); cvB the
   // first reduce level's outputs, <= one per kReduceFanIn nodes per message
-  const size_t b_cv = align_up(n_groups * kGroupOut * 32, 256);
-  const size_t b_cv1 = align_up((n_groups * kGroupOut / kReduceFanIn + n + 1) * 32, 256);
+  const size_t b_cv = align_up(n_groups * group_out * 32, 256);
+  const size_t b_cv1 = align_up((n_groups * group_out / kReduceFanIn + n + 1) * 32, 256);
   const size_t b_out = align_up(n * 32, 256);
   const size_t need = b_groups + b_jobs + b_cv + b_cv1 + 2 * b_out;
   const size_t h_need = b_groups + b_jobs + 2 * b_out;
@@ -137,7 +145,7 @@ int Context::blake3_dev(size_t n, const uint8_t *const *d_msgs, const size_t *le
     jo += l.size();
   }
   HIP_TRY(hipMemcpyAsync(d, h, b_groups + b_jobs, hipMemcpyHostToDevice, s));
-  HIP_TRY(launch_blake3_groups(d_hmsgs, uint32_t(n), uint32_t(n_groups), d_cv0, d_msg_cvs,
+  HIP_TRY(launch_blake3_groups(d_hmsgs, uint32_t(n), uint32_t(n_groups), glv, d_cv0, d_msg_cvs,
                                d_digests, s));
   uint32_t *cur = d_cv0, *nxt = d_cv1;
   jo = 0;

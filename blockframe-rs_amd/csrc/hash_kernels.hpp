@@ -19,8 +19,8 @@ constexpr uint32_t kReduceFanIn = 512;                  // CVs one kernel-2 work
 // they are left to kernel 2, whose first levels over 512 nodes use every
 // lane.  Three levels rather than two also halve kernel 2's first-level jobs,
 // which then fit the chip in one round.
-constexpr uint32_t kGroupLevels = 3;
-constexpr uint32_t kGroupOut = kGroupChunks >> kGroupLevels;  // level-3 nodes per full group
+constexpr uint32_t kGroupLevels = 3;  // default; BFRS_B3_GROUP_LEVELS = 2 or 3 (A/B)
+constexpr uint32_t kGroupOutMax = kGroupChunks >> 2;  // level-2 nodes per group (the most)
 
 // One message of a kernel-1 launch.  Workgroup w belongs to the message m
 // with first_group(m) <= w < first_group(m + 1) (found by a binary search in
@@ -28,7 +28,7 @@ constexpr uint32_t kGroupOut = kGroupChunks >> kGroupLevels;  // level-3 nodes p
 // and hashes <= 256 KiB of it starting at a 256 KiB aligned offset (so its
 // chunks form an aligned subtree of the message).  A single-group message is
 // finished in kernel 1; a group of a longer message writes its ceil(chunks /
-// 8) level-3 nodes to group_cvs[kGroupOut * w].
+// 2^levels) level-`levels` nodes to group_cvs[(kGroupChunks >> levels) * w].
 struct alignas(16) HashMsg {
   uint64_t addr;         // device address of the message (16-byte aligned)
   uint64_t chunk0;       // BLAKE3 chunk counter of its first chunk
@@ -46,8 +46,8 @@ struct alignas(16) HashReduce {
 };
 
 hipError_t launch_blake3_groups(const HashMsg *d_msgs, uint32_t n_msgs, uint32_t n_groups,
-                                uint32_t *d_group_cvs, uint32_t *d_msg_cvs, uint32_t *d_digests,
-                                hipStream_t stream);
+                                uint32_t levels, uint32_t *d_group_cvs, uint32_t *d_msg_cvs,
+                                uint32_t *d_digests, hipStream_t stream);
 hipError_t launch_blake3_reduce(const HashReduce *d_jobs, uint32_t n_jobs, const uint32_t *d_in,
                                 uint32_t *d_out, uint32_t *d_msg_cvs, uint32_t *d_digests,
                                 hipStream_t stream);
