@@ -332,10 +332,13 @@ hipError_t launch_blake3_groups(const HashMsg *d_msgs, uint32_t n_msgs, uint32_t
                                 uint32_t levels, uint32_t *d_group_cvs, uint32_t *d_msg_cvs,
                                 uint32_t *d_digests, hipStream_t stream) {
   if (n_groups == 0 || n_msgs == 0) return hipSuccess;
+#ifdef BFRS_AB_VARIANTS  // 2 levels: measurement build only (tools/b3_levels_ab.py)
   if (levels == 2)
     hipLaunchKernelGGL(blake3_group_kernel<2>, dim3(n_groups), dim3(256), 0, stream, d_msgs, n_msgs,
                        d_group_cvs, d_msg_cvs, d_digests);
-  else if (levels == 3)
+  else
+#endif
+  if (levels == 3)
     hipLaunchKernelGGL(blake3_group_kernel<3>, dim3(n_groups), dim3(256), 0, stream, d_msgs, n_msgs,
                        d_group_cvs, d_msg_cvs, d_digests);
   else

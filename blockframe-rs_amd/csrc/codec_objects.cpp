@@ -71,11 +71,13 @@ struct CodecObject {
   int stage(size_t i, const uint8_t *src, size_t len) {
     HIP_TRY(hipSetDevice(pool->device));
     if (host_registered(src, len)) {
-      // a registered (page-locked) range: one DMA straight from it, waited
-      // for, so the caller may reuse its buffer on return as with the crate
+      // a registered (page-locked) range: one DMA straight from it, queued
+      // like the pinned rows' copies.  A registered range's bytes must stay
+      // unchanged until the encode()/decode() that consumes them returns
+      // (include/bfrs.h: the caller opted in by registering it; BlockFrame's
+      // mmap'd segments are read-only)
       HIP_TRY(hipMemcpyAsync(d_row(i), src, len, hipMemcpyHostToDevice, h2d()));
       HIP_TRY(hipEventRecord(slot->ev_h2d, h2d()));
-      HIP_TRY(hipEventSynchronize(slot->ev_h2d));
     } else if (pool->staging == Staging::kPinned) {
       // the row's previous H2D (an earlier round on this object) is done:
       // rows are reused only after encode()/decode() synchronised the slot

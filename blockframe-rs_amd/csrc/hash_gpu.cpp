@@ -14,10 +14,14 @@ namespace bfrs {
 namespace {
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 // Tree levels kernel 1 pairs in a group of a multi-group message
-// (hash_kernels.hpp); BFRS_B3_GROUP_LEVELS = 2 or 3, read per call (A/B).
+// (hash_kernels.hpp); the measurement build also takes BFRS_B3_GROUP_LEVELS=2,
+// read per call (same-process A/B, tools/b3_levels_ab.py).
 uint32_t group_levels() {
+#ifdef BFRS_AB_VARIANTS
   const char *e = std::getenv("BFRS_B3_GROUP_LEVELS");
-  return e && std::strcmp(e, "2") == 0 ? 2 : e && std::strcmp(e, "3") == 0 ? 3 : kGroupLevels;
+  if (e && std::strcmp(e, "2") == 0) return 2;
+#endif
+  return kGroupLevels;
 }
 }  // namespace
 

@@ -130,10 +130,11 @@ size_t bfrs_shard_pitch(size_t shard_bytes);
  * segment buffers -- so that codec objects and the wrappers DMA shards that
  * lie inside it straight to the device, instead of copying them through the
  * slot's pinned rows first (no reference counterpart; the crate copies every
- * added shard too).  add_*_shard still returns only when the shard is on the
- * device, so the caller may reuse its buffer at once.  Process-wide (HIP
- * registration, any context); unregister before unmapping or freeing the
- * range.  BFRS_E_HIP if the runtime refuses the range. */
+ * added shard).  Opting in changes one rule: the DMA reads a registered
+ * shard asynchronously, so its bytes must stay unchanged until the encode()
+ * / decode() that consumes it returns (the wrappers return after both).
+ * Process-wide (HIP registration, any context); unregister before unmapping
+ * or freeing the range.  BFRS_E_HIP if the runtime refuses the range. */
 int bfrs_host_register(void *ptr, size_t len);
 int bfrs_host_unregister(void *ptr);
 

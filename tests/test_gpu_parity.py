@@ -790,9 +790,8 @@ def test_mixed_entry_points_share_one_context_across_threads(ctx, bfrs, oracle):
 def test_registered_inputs_dma_straight_and_match(bfrs, oracle):
     """bfrs_host_register: shards inside a registered range go to the device
     by DMA straight from it (no staging copy); the bytes equal the oracle's
-    through the wrappers and the objects, the caller may overwrite its buffer
-    as soon as add returns, and the registry refuses overlaps and unknown
-    ranges."""
+    through the wrappers and the objects, the range may change once encode()
+    returned, and the registry refuses overlaps and unknown ranges."""
     c = bfrs.Context(0)
     rng = np.random.default_rng(33)
     n = (1 << 20) + 64 * 5
@@ -806,14 +805,19 @@ def test_registered_inputs_dma_straight_and_match(bfrs, oracle):
         assert bfrs.Chunker(c).generate_parity_into(segs, 30, 3, outs) == n
         assert [o.tobytes() for o in outs] == want
         enc = bfrs.ReedSolomonEncoder(c, 30, 3, n)
-        scratch = big[:n]  # reused between adds: DMA done before add returns
-        for d in data:
-            scratch[:] = d
-            enc.add_original_shard(scratch)
+        for sg in segs:  # queued DMAs straight from the range; consumed by encode()
+            enc.add_original_shard(sg)
         assert list(enc.encode().recovery_iter()) == want
+        # once encode() returned, the range may change: a second round on the
+        # same object with other bytes gives their parity
+        big[:] = 255 - big
+        for sg in segs:
+            enc.add_original_shard(sg)
+        want2 = [r.tobytes() for r in oracle.encode([255 - d for d in data], 3)]
+        assert list(enc.encode().recovery_iter()) == want2
         del enc
+        big[:] = 255 - big
         slots = [None if i in (4, 20) else big[i * n:(i + 1) * n] for i in range(30)]
-        big[:n] = data[0]
         par = [np.frombuffer(p, np.uint8) for p in want]
         assert bfrs.recover_segment_rs30_3(c, slots, par, 20) == data[20].tobytes()
         with pytest.raises(bfrs.BfrsError):

@@ -1,7 +1,9 @@
 """Same-process A/B of the device BLAKE3's kernel-1 tree depth
 (BFRS_B3_GROUP_LEVELS = 2 / 3, read per call): C2's 128 x 32 MiB HBM-resident
 segments, alternating variants, best and median wall time per call and the
-group / reduce kernel times from torch's profiler.  GPU box only."""
+group / reduce kernel times from torch's profiler.  Loads the measurement
+build (make -C blockframe-rs_amd/csrc ab -> libbfrs_ab.so, BFRS_LIB).  GPU box
+only."""
 import json
 import os
 import statistics
@@ -51,7 +53,7 @@ def main():
             kern[lv].append(kernel_ms(ctx, segs))
     assert digests["2"] == digests["3"]
     out = {"what": "device BLAKE3 of 128 x 32 MiB, kernel-1 tree levels 2 vs 3, alternated in one "
-                   "process (tools/b3_levels_ab.py)", "digests_equal": True}
+                   "process (tools/b3_levels_ab.py, measurement build)", "digests_equal": True}
     for lv in ("2", "3"):
         ts = res[lv]
         out[lv] = {"best_ms": round(min(ts) * 1e3, 4), "median_ms": round(statistics.median(ts) * 1e3, 4),
