@@ -967,6 +967,19 @@ def crate_api(ctx, sets, reps=7, staging_ab=True):
                     ch.generate_parity_into(blocks[0], len(blocks[0]), 3, outs)
                     tg.append(time.perf_counter() - t1)
                 reg["generate_parity"] = tg
+                # recover_segment_rs30_3 with the 29 surviving segments registered
+                # (the parity shards come from fs::read, recovery.rs: unregistered)
+                target = sets.erased[0][0]
+                slots_r = [None if i == target else blocks[0][i] for i in range(len(blocks[0]))]
+                par_r = [np.array(o) for o in outs]
+                tr = []
+                for _ in range(reps):
+                    out = np.empty(S, np.uint8)
+                    t1 = time.perf_counter()
+                    bfrs.recover_segment_rs30_3_into(ctx, slots_r, par_r, target, out)
+                    tr.append(time.perf_counter() - t1)
+                reg["recover_ok"] = bool(np.array_equal(out, blocks[0][target]))
+                reg["recover"] = tr
             finally:
                 for x in done:
                     bfrs.host_unregister(x)
@@ -1045,7 +1058,7 @@ def crate_api(ctx, sets, reps=7, staging_ab=True):
                                    "python_wrapper_ms": round(tr_py * 1e3, 2),
                                    "what": "one erased segment of that block, pageable host in/out"},
         "breakdown": bd,
-        "recover_match": bool(recover_ok) and all(recover_ok),
+        "recover_match": bool(recover_ok) and all(recover_ok) and registered.get("recover_ok", True),
         "generate_parity_all_blocks_threads": {
             "ms": round(min(t_par) * 1e3, 2), "GiBps": round(par_gib / min(t_par), 2),
             "median_ms": round(sorted(t_par)[len(t_par) // 2] * 1e3, 2),
@@ -1066,6 +1079,9 @@ def crate_api(ctx, sets, reps=7, staging_ab=True):
             "generate_parity_all_blocks_threads_median_ms": round(sorted(ra)[len(ra) // 2] * 1e3, 2),
             "generate_parity_ms": round(min(rg) * 1e3, 2),
             "generate_parity_median_ms": round(sorted(rg)[len(rg) // 2] * 1e3, 2),
+            "recover_segment_rs30_3_ms": round(min(registered["recover"]) * 1e3, 2),
+            "recover_segment_rs30_3_median_ms": round(
+                sorted(registered["recover"])[len(registered["recover"]) // 2] * 1e3, 2),
             "register_ms": registered["register_ms"],
             "what": "the same calls with every input segment registered once "
                     "(bfrs_host_register, as a caller registers its file mmap per commit): "
@@ -1092,7 +1108,7 @@ def crate_api(ctx, sets, reps=7, staging_ab=True):
             pg, pr, _, _, _, pg_reuse, pr_reuse, pg_new_in = wrappers(c2)
         finally:
             c2.close()
-        res["recover_match"] = all(recover_ok)
+        res["recover_match"] = all(recover_ok) and registered.get("recover_ok", True)
         res["alt_staging"] = {"staging": alt, "generate_parity_ms": round(pg * 1e3, 2),
                               "generate_parity_touched_outputs_ms": round(pg_reuse * 1e3, 2),
                               "generate_parity_new_inputs_ms": round(pg_new_in * 1e3, 2),
@@ -1346,7 +1362,11 @@ def c4_one_process(args, ctx, world, one_device=False, steps=2):
             if i in er:
                 want.append((3 * b + er.index(i), seg + i))
         seg += k
-    extra = [bfrs.Context(0 if one_device else d) for d in range(1, world)]
+    # one context per GPU this process can see (under a launcher that hides
+    # the other ranks' devices it falls back to the visible ones)
+    visible = torch.cuda.device_count()
+    devs = [0] * (world - 1) if one_device else [d for d in range(world) if d != ctx.device][:max(0, min(world, visible) - 1)]
+    extra = [bfrs.Context(d) for d in devs]
     ctxs = [ctx] + extra
     try:
         def clock(call):
@@ -1366,7 +1386,8 @@ def c4_one_process(args, ctx, world, one_device=False, steps=2):
     gib = nseg * S / 2**30
     del host, par, rest
     return {
-        "devices": len(ctxs), "contexts_on_device_0": one_device or world == 1,
+        "contexts": len(ctxs), "devices": sorted({ctx.device} | set(devs)),
+        "contexts_on_device_0": one_device or world == 1,
         "encode_GiBps": round(gib / t_enc, 2), "decode_GiBps": round(gib / t_dec, 2),
         "encode_ms": round(t_enc * 1e3, 2), "decode_ms": round(t_dec * 1e3, 2),
         "parity_golden": golden, "restored_match": restored_ok,
