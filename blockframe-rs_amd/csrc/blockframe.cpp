@@ -61,6 +61,22 @@ bool overlaps(const uint8_t *a, size_t na, const uint8_t *b, size_t nb) {
   return x < y + nb && y < x + na;
 }
 
+// The slab-pipelined generate_parity (encoder_encode_slabs): pinned staging,
+// shards of >= 16 MiB (at least two ~8 MiB slabs), no registered segment;
+// BFRS_WRAPPER_SLABS=0 turns it off (A/B).
+bool slab_wrapper_ok(bfrs_ctx *ctx, const uint8_t *const *segs, const size_t *lens, size_t n,
+                     size_t shard) {
+  static const bool on = [] {
+    const char *e = std::getenv("BFRS_WRAPPER_SLABS");
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
+  if (!on || shard < (size_t(16) << 20) || ctx->impl.codec_pool->staging != Staging::kPinned)
+    return false;
+  for (size_t i = 0; i < n; ++i)
+    if (!segs[i] || (lens[i] && host_registered(segs[i], lens[i]))) return false;
+  return true;
+}
+
 // RAII holders for the streaming objects.
 struct Enc {
   bfrs_encoder *p = nullptr;
@@ -93,6 +109,13 @@ int bfrs_generate_parity(bfrs_ctx *ctx, const uint8_t *const *segments, const si
   if (!parity_out) return set_error(BFRS_E_INVALID_ARGUMENT, "generate_parity: parity_out NULL");
   for (size_t j = 0; j < parity_shards; ++j)
     if (!parity_out[j]) return set_error(BFRS_E_INVALID_ARGUMENT, "parity buffer is NULL");
+  // A whole block of pageable segments (BlockFrame's case): slab-pipelined,
+  // so each column slab's kernel and D2H run while the next slab's segments
+  // are copied and DMA'd.  Registered segments go straight by
+  // DMA through the adds below, and a segment count other than data_shards
+  // takes the adds too, which report the crate's errors.
+  if (n_segments == data_shards && slab_wrapper_ok(ctx, segments, seg_lens, n_segments, max_len))
+    return encoder_encode_slabs(enc.p, segments, seg_lens, parity_out);
   // generate.rs:75-82 + 87-89 — zero-pad each segment to max_len and add it
   const auto t_add = std::chrono::steady_clock::now();
   std::vector<uint8_t> padded;

@@ -260,6 +260,84 @@ int bfrs::encoder_encode_to_host(bfrs_encoder *e, uint8_t *const *outs) {
   return BFRS_OK;
 }
 
+int bfrs::encoder_encode_slabs(bfrs_encoder *e, const uint8_t *const *segs, const size_t *lens,
+                               uint8_t *const *outs) {
+  const size_t S = e->shard_bytes, k = e->k, m = e->m;
+  if (e->received != 0 || e->encoded)
+    return set_error(BFRS_E_INVALID_ARGUMENT, "encode_slabs: encoder already in use");
+  HIP_TRY(hipSetDevice(e->pool->device));
+  CodecSlot &sl = *e->slot;
+  if (!sl.aux) HIP_TRY(hipStreamCreateWithFlags(&sl.aux, hipStreamNonBlocking));
+  hipStream_t st = sl.stream, ax = sl.aux;
+  // ~8 MiB slabs of 64-byte chunks; the last slab takes the shard's tail
+  const size_t chunks = S / 64;
+  const size_t nslab = std::max<size_t>(1, std::min<size_t>(8, S >> 23));
+  std::vector<hipEvent_t> staged(nslab, nullptr), done(nslab, nullptr);
+  struct Events {
+    std::vector<hipEvent_t> &a, &b;
+    ~Events() {
+      for (auto *v : {&a, &b})
+        for (hipEvent_t x : *v)
+          if (x) (void)hipEventDestroy(x);
+    }
+  } guard{staged, done};
+  std::vector<size_t> off(nslab + 1);
+  for (size_t q = 0; q < nslab; ++q) off[q] = chunks * q / nslab * 64;
+  off[nslab] = S;
+  const uint32_t kk = uint32_t(k);
+  std::vector<const uint8_t *> din(k);
+  std::vector<uint8_t *> dout(m);
+  for (size_t q = 0; q < nslab; ++q) {
+    const size_t o = off[q], len = off[q + 1] - o;
+    for (size_t i = 0; i < k; ++i) {
+      const size_t avail = lens[i] > o ? std::min(len, lens[i] - o) : 0;
+      if (avail) host_copy(e->h_row(i) + o, segs[i] + o, avail);
+      if (avail < len) std::memset(e->h_row(i) + o + avail, 0, len - avail);
+      HIP_TRY(hipMemcpyAsync(e->d_row(i) + o, e->h_row(i) + o, len, hipMemcpyHostToDevice, st));
+      din[i] = e->d_row(i) + o;
+    }
+    HIP_TRY(hipEventCreateWithFlags(&staged[q], hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(staged[q], st));
+    HIP_TRY(hipStreamWaitEvent(ax, staged[q], 0));
+    for (size_t j = 0; j < m; ++j) dout[j] = e->d_row(k + j) + o;
+    int rc = encode_batch_on(e->ctx, 1, &kk, m, len, din.data(), dout.data(), ax);
+    if (rc) return rc;
+    for (size_t j = 0; j < m; ++j)
+      HIP_TRY(hipMemcpyAsync(e->h_row(k + j) + o, e->d_row(k + j) + o, len,
+                             hipMemcpyDeviceToHost, ax));
+    HIP_TRY(hipEventCreateWithFlags(&done[q], hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(done[q], ax));
+  }
+  HIP_TRY(hipEventRecord(sl.ev_h2d, st));
+  HIP_TRY(hipEventRecord(sl.ev_d2h, ax));
+  // the caller's fresh outputs fault in while the last slabs transfer
+  if (prefault_outputs()) {
+    std::vector<std::thread> touch;
+    for (size_t j = 0; j < m; ++j) {
+      uint8_t *p = outs[j];
+      try {
+        touch.emplace_back([p, S] {
+          volatile uint8_t *q = p;
+          for (size_t x = 0; x < S; x += 4096) q[x] = 0;
+          q[S - 1] = 0;
+        });
+      } catch (...) {
+        break;
+      }
+    }
+    for (auto &t : touch) t.join();
+  }
+  for (size_t q = 0; q < nslab; ++q) {
+    HIP_TRY(hipEventSynchronize(done[q]));
+    for (size_t j = 0; j < m; ++j)
+      host_copy(outs[j] + off[q], e->h_row(k + j) + off[q], off[q + 1] - off[q]);
+  }
+  e->received = k;
+  e->encoded = true;
+  e->fetched_to_pinned = true;
+  return BFRS_OK;
+}
+
 extern "C" {
 
 int bfrs_encoder_encode(bfrs_encoder *e) {

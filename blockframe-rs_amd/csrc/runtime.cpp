@@ -114,6 +114,10 @@ CodecSlot::~CodecSlot() {
     (void)hipStreamSynchronize(stream);
     (void)hipStreamDestroy(stream);
   }
+  if (aux) {
+    (void)hipStreamSynchronize(aux);
+    (void)hipStreamDestroy(aux);
+  }
   if (d) (void)hipFree(d);
   if (h) (void)hipHostFree(h);
 }

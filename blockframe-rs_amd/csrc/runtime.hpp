@@ -102,6 +102,10 @@ struct CodecSlot {
   int stream_idx = -1;           // index into CodecPool::streams while acquired
   // the last H2D, kernel and D2H this slot queued (each on its own stream)
   hipEvent_t ev_h2d = nullptr, ev_k = nullptr, ev_d2h = nullptr;
+  // second stream of the slab-pipelined wrapper encode (encoder_encode_slabs):
+  // kernels and D2H of slab s run on it while slab s + 1's H2D runs on
+  // `stream`; created on first use
+  hipStream_t aux = nullptr;
   // Waits for this slot's work queued so far (not for later work of other
   // slots sharing a stream).
   int sync();
@@ -243,6 +247,13 @@ int check_host_batch(bfrs_ctx *ctx, size_t nblocks, const uint32_t *ks, size_t m
 // recovery.rs:166-170) are filled by D2H straight into the caller's buffers.
 // encode into m host buffers of shard_bytes each (object left encoded)
 int encoder_encode_to_host(bfrs_encoder *e, uint8_t *const *outs);
+// generate_parity's whole block at once, for a fresh encoder: column slabs of
+// all k segments staged and DMA'd slab by slab, each slab's kernel and D2H
+// overlapping the next slab's copies, the outputs copied out slab by slab.
+// lens[i] < shard_bytes: zero padding (generate.rs:75-82).  Same results and
+// object state as k adds + encoder_encode_to_host.
+int encoder_encode_slabs(bfrs_encoder *e, const uint8_t *const *segs, const size_t *lens,
+                         uint8_t *const *outs);
 // restored original `index` of a decoded decoder into a host buffer
 int decoder_restored_to_host(bfrs_decoder *d, size_t index, uint8_t *out);
 }  // namespace bfrs
