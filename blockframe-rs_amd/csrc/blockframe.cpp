@@ -65,15 +65,20 @@ bool overlaps(const uint8_t *a, size_t na, const uint8_t *b, size_t nb) {
 // shards of >= 16 MiB (at least two ~8 MiB slabs), no registered segment;
 // BFRS_WRAPPER_SLABS=0 turns it off (A/B).
 bool slab_wrapper_ok(bfrs_ctx *ctx, const uint8_t *const *segs, const size_t *lens, size_t n,
-                     size_t shard) {
+                     size_t shard, bool allow_missing = false) {
   static const bool on = [] {
     const char *e = std::getenv("BFRS_WRAPPER_SLABS");
     return !(e && std::strcmp(e, "0") == 0);
   }();
   if (!on || shard < (size_t(16) << 20) || ctx->impl.codec_pool->staging != Staging::kPinned)
     return false;
-  for (size_t i = 0; i < n; ++i)
-    if (!segs[i] || (lens[i] && host_registered(segs[i], lens[i]))) return false;
+  for (size_t i = 0; i < n; ++i) {
+    if (!segs[i]) {
+      if (allow_missing) continue;
+      return false;
+    }
+    if (lens[i] && host_registered(segs[i], lens[i])) return false;
+  }
   return true;
 }
 
@@ -236,6 +241,25 @@ int bfrs_recover_segment_rs30_3(bfrs_ctx *ctx, const uint8_t *const *segments,
     if (overlaps(out, shard_size, block_parity[j], parity_lens[j]))
       return set_error(BFRS_E_INVALID_ARGUMENT,
                        "recover_segment_rs30_3: out overlaps a parity shard");
+  // Pageable inputs of one size, the target erased, all parity present (the
+  // reference's case): slab-pipelined, each slab's decode and the target's
+  // D2H overlapping the next slab's copies.  Anything else takes the adds,
+  // which report the crate's errors.
+  {
+    bool slabs = !segments[target_index] && missing >= 1 &&
+                 slab_wrapper_ok(ctx, segments, seg_lens, 30, shard_size, true);
+    for (size_t i = 0; slabs && i < 30; ++i)
+      if (segments[i] && seg_lens[i] != shard_size) slabs = false;
+    for (size_t j = 0; slabs && j < 3; ++j)
+      if (!block_parity[j] || parity_lens[j] != shard_size ||
+          host_registered(block_parity[j], parity_lens[j]))
+        slabs = false;
+    if (slabs) {
+      if ((rc = decoder_restore_slabs(dec.p, segments, block_parity, target_index, out))) return rc;
+      *out_len = shard_size;
+      return BFRS_OK;
+    }
+  }
   uint8_t *const outs[1] = {out};
   Prefault pf(outs, 1, shard_size);
   for (size_t i = 0; i < 30; ++i)

@@ -260,6 +260,58 @@ int bfrs::encoder_encode_to_host(bfrs_encoder *e, uint8_t *const *outs) {
   return BFRS_OK;
 }
 
+namespace {
+// First-touch of fresh output buffers (the reference's to_vec / fresh Vec
+// outputs) on `parts` helper threads per buffer; returns when all are done.
+void touch_pages(uint8_t *const *bufs, size_t nbuf, size_t len, size_t parts) {
+  std::vector<std::thread> t;
+  const size_t per = (len + parts - 1) / parts;
+  for (size_t b = 0; b < nbuf; ++b)
+    for (size_t q = 0; q < parts; ++q) {
+      const size_t lo = q * per, hi = std::min(len, lo + per);
+      if (lo >= hi) continue;
+      uint8_t *p = bufs[b];
+      auto f = [p, lo, hi] {
+        volatile uint8_t *x = p;
+        for (size_t o = lo; o < hi; o += 4096) x[o] = 0;
+        x[hi - 1] = 0;
+      };
+      try {
+        t.emplace_back(f);
+      } catch (...) {
+        f();
+      }
+    }
+  for (auto &x : t) x.join();
+}
+
+// Column slabs of ~8 MiB of 64-byte chunks; the last slab takes the tail.
+std::vector<size_t> slab_offsets(size_t S) {
+  const size_t chunks = S / 64;
+  const size_t nslab = std::max<size_t>(1, std::min<size_t>(8, S >> 23));
+  std::vector<size_t> off(nslab + 1);
+  for (size_t q = 0; q < nslab; ++q) off[q] = chunks * q / nslab * 64;
+  off[nslab] = S;
+  return off;
+}
+
+struct EventList {
+  std::vector<hipEvent_t> v;
+  ~EventList() {
+    for (hipEvent_t x : v)
+      if (x) (void)hipEventDestroy(x);
+  }
+  int add(hipStream_t st, hipEvent_t *out) {
+    hipEvent_t e = nullptr;
+    HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    v.push_back(e);
+    HIP_TRY(hipEventRecord(e, st));
+    *out = e;
+    return BFRS_OK;
+  }
+};
+}  // namespace
+
 int bfrs::encoder_encode_slabs(bfrs_encoder *e, const uint8_t *const *segs, const size_t *lens,
                                uint8_t *const *outs) {
   const size_t S = e->shard_bytes, k = e->k, m = e->m;
@@ -269,21 +321,10 @@ int bfrs::encoder_encode_slabs(bfrs_encoder *e, const uint8_t *const *segs, cons
   CodecSlot &sl = *e->slot;
   if (!sl.aux) HIP_TRY(hipStreamCreateWithFlags(&sl.aux, hipStreamNonBlocking));
   hipStream_t st = sl.stream, ax = sl.aux;
-  // ~8 MiB slabs of 64-byte chunks; the last slab takes the shard's tail
-  const size_t chunks = S / 64;
-  const size_t nslab = std::max<size_t>(1, std::min<size_t>(8, S >> 23));
-  std::vector<hipEvent_t> staged(nslab, nullptr), done(nslab, nullptr);
-  struct Events {
-    std::vector<hipEvent_t> &a, &b;
-    ~Events() {
-      for (auto *v : {&a, &b})
-        for (hipEvent_t x : *v)
-          if (x) (void)hipEventDestroy(x);
-    }
-  } guard{staged, done};
-  std::vector<size_t> off(nslab + 1);
-  for (size_t q = 0; q < nslab; ++q) off[q] = chunks * q / nslab * 64;
-  off[nslab] = S;
+  const std::vector<size_t> off = slab_offsets(S);
+  const size_t nslab = off.size() - 1;
+  EventList ev;
+  std::vector<hipEvent_t> done(nslab);
   const uint32_t kk = uint32_t(k);
   std::vector<const uint8_t *> din(k);
   std::vector<uint8_t *> dout(m);
@@ -296,37 +337,21 @@ int bfrs::encoder_encode_slabs(bfrs_encoder *e, const uint8_t *const *segs, cons
       HIP_TRY(hipMemcpyAsync(e->d_row(i) + o, e->h_row(i) + o, len, hipMemcpyHostToDevice, st));
       din[i] = e->d_row(i) + o;
     }
-    HIP_TRY(hipEventCreateWithFlags(&staged[q], hipEventDisableTiming));
-    HIP_TRY(hipEventRecord(staged[q], st));
-    HIP_TRY(hipStreamWaitEvent(ax, staged[q], 0));
+    hipEvent_t staged;
+    if (int rc = ev.add(st, &staged)) return rc;
+    HIP_TRY(hipStreamWaitEvent(ax, staged, 0));
     for (size_t j = 0; j < m; ++j) dout[j] = e->d_row(k + j) + o;
     int rc = encode_batch_on(e->ctx, 1, &kk, m, len, din.data(), dout.data(), ax);
     if (rc) return rc;
     for (size_t j = 0; j < m; ++j)
       HIP_TRY(hipMemcpyAsync(e->h_row(k + j) + o, e->d_row(k + j) + o, len,
                              hipMemcpyDeviceToHost, ax));
-    HIP_TRY(hipEventCreateWithFlags(&done[q], hipEventDisableTiming));
-    HIP_TRY(hipEventRecord(done[q], ax));
+    if ((rc = ev.add(ax, &done[q]))) return rc;
   }
   HIP_TRY(hipEventRecord(sl.ev_h2d, st));
   HIP_TRY(hipEventRecord(sl.ev_d2h, ax));
   // the caller's fresh outputs fault in while the last slabs transfer
-  if (prefault_outputs()) {
-    std::vector<std::thread> touch;
-    for (size_t j = 0; j < m; ++j) {
-      uint8_t *p = outs[j];
-      try {
-        touch.emplace_back([p, S] {
-          volatile uint8_t *q = p;
-          for (size_t x = 0; x < S; x += 4096) q[x] = 0;
-          q[S - 1] = 0;
-        });
-      } catch (...) {
-        break;
-      }
-    }
-    for (auto &t : touch) t.join();
-  }
+  if (prefault_outputs()) touch_pages(outs, m, S, 1);
   for (size_t q = 0; q < nslab; ++q) {
     HIP_TRY(hipEventSynchronize(done[q]));
     for (size_t j = 0; j < m; ++j)
@@ -534,4 +559,61 @@ int bfrs::decoder_restored_to_host(bfrs_decoder *d, size_t index, uint8_t *out) 
   HIP_TRY(hipMemcpyAsync(out, d->d_row(index), d->shard_bytes, hipMemcpyDeviceToHost, d->d2h()));
   HIP_TRY(hipEventRecord(d->slot->ev_d2h, d->d2h()));
   return d->slot->sync();
+}
+
+int bfrs::decoder_restore_slabs(bfrs_decoder *d, const uint8_t *const *segs,
+                                const uint8_t *const *par, size_t target, uint8_t *out) {
+  const size_t S = d->shard_bytes, k = d->k, m = d->m;
+  if (d->decoded || std::count(d->orig_present.begin(), d->orig_present.end(), 1) ||
+      std::count(d->rec_present.begin(), d->rec_present.end(), 1))
+    return set_error(BFRS_E_INVALID_ARGUMENT, "restore_slabs: decoder already in use");
+  HIP_TRY(hipSetDevice(d->pool->device));
+  CodecSlot &sl = *d->slot;
+  if (!sl.aux) HIP_TRY(hipStreamCreateWithFlags(&sl.aux, hipStreamNonBlocking));
+  hipStream_t st = sl.stream, ax = sl.aux;
+  for (size_t i = 0; i < k; ++i) d->orig_present[i] = segs[i] != nullptr;
+  for (size_t j = 0; j < m; ++j) d->rec_present[j] = par[j] != nullptr;
+  const std::vector<size_t> off = slab_offsets(S);
+  const size_t nslab = off.size() - 1;
+  EventList ev;
+  std::vector<hipEvent_t> done(nslab);
+  const uint32_t kk = uint32_t(k);
+  std::vector<const uint8_t *> dorig(k), drec(m);
+  std::vector<uint8_t *> drest(k);
+  for (size_t q = 0; q < nslab; ++q) {
+    const size_t o = off[q], len = off[q + 1] - o;
+    for (size_t r = 0; r < k + m; ++r) {
+      const uint8_t *src = r < k ? segs[r] : par[r - k];
+      if (!src) continue;
+      host_copy(d->h_row(r) + o, src + o, len);
+      HIP_TRY(hipMemcpyAsync(d->d_row(r) + o, d->h_row(r) + o, len, hipMemcpyHostToDevice, st));
+    }
+    for (size_t i = 0; i < k; ++i) {
+      dorig[i] = segs[i] ? d->d_row(i) + o : nullptr;
+      drest[i] = segs[i] ? nullptr : d->d_row(i) + o;
+    }
+    for (size_t j = 0; j < m; ++j) drec[j] = par[j] ? d->d_row(k + j) + o : nullptr;
+    hipEvent_t staged;
+    if (int rc = ev.add(st, &staged)) return rc;
+    HIP_TRY(hipStreamWaitEvent(ax, staged, 0));
+    int rc = decode_batch_on(d->ctx, 1, &kk, m, len, dorig.data(), drec.data(), drest.data(), ax);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(d->h_row(target) + o, d->d_row(target) + o, len, hipMemcpyDeviceToHost,
+                           ax));
+    if ((rc = ev.add(ax, &done[q]))) return rc;
+  }
+  HIP_TRY(hipEventRecord(sl.ev_h2d, st));
+  HIP_TRY(hipEventRecord(sl.ev_d2h, ax));
+  uint8_t *const outs[1] = {out};
+  if (prefault_outputs()) touch_pages(outs, 1, S, 4);
+  for (size_t q = 0; q < nslab; ++q) {
+    HIP_TRY(hipEventSynchronize(done[q]));
+    host_copy(out + off[q], d->h_row(target) + off[q], off[q + 1] - off[q]);
+  }
+  d->decoded = true;
+  d->restored.assign(k, 0);
+  d->fetched.assign(k, 0);
+  for (size_t i = 0; i < k; ++i) d->restored[i] = !d->orig_present[i];
+  d->fetched[target] = 1;  // its pinned row holds the whole shard
+  return BFRS_OK;
 }

@@ -256,4 +256,11 @@ int encoder_encode_slabs(bfrs_encoder *e, const uint8_t *const *segs, const size
                          uint8_t *const *outs);
 // restored original `index` of a decoded decoder into a host buffer
 int decoder_restored_to_host(bfrs_decoder *d, size_t index, uint8_t *out);
+// recover_segment_rs30_3's whole decode at once, for a fresh decoder: segs[k]
+// (NULL = missing, segs[target] among them), all m parity shards, every
+// length shard_bytes; slab-pipelined like encoder_encode_slabs, only the
+// target leaves the device.  Object state as after the adds + decode +
+// restored_original(target).
+int decoder_restore_slabs(bfrs_decoder *d, const uint8_t *const *segs, const uint8_t *const *par,
+                          size_t target, uint8_t *out);
 }  // namespace bfrs

@@ -856,3 +856,32 @@ def test_generate_parity_slab_pipeline_vs_oracle(bfrs, oracle, monkeypatch, stag
         assert list(enc.encode().recovery_iter()) == want
         del enc
     c.close()
+
+
+def test_recover_rs30_3_slab_pipeline_vs_originals(bfrs, oracle):
+    """recover_segment_rs30_3 on >= 16 MiB shards runs slab by slab
+    (decoder_restore_slabs): 1, 2 and 3 erased segments with the target among
+    them, a ragged shard size (tail in the last slab); the restored target
+    equals the original.  A present target and a mismatched segment size still
+    take the adds and give the reference's errors."""
+    c = bfrs.Context(0)
+    rng = np.random.default_rng(78)
+    n = (16 << 20) + 64 * 3 + 2
+    data = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(30)]
+    par = [np.frombuffer(p, np.uint8) for p in
+           [r.tobytes() for r in oracle.encode(data, 3)]]
+    for erased, target in (([7], 7), ([0, 29], 29), ([3, 14, 25], 14)):
+        slots = [None if i in erased else data[i] for i in range(30)]
+        out = np.empty(n, np.uint8)
+        assert bfrs.recover_segment_rs30_3_into(c, slots, par, target, out) == n
+        assert np.array_equal(out, data[target]), (erased, target)
+    slots = [None if i == 5 else data[i] for i in range(30)]
+    with pytest.raises(bfrs.BfrsError) as e:  # target present: restored_original is None
+        bfrs.recover_segment_rs30_3_into(c, slots, par, 6, np.empty(n, np.uint8))
+    assert "Failed to restore target segment" in str(e.value)
+    short = list(slots)
+    short[9] = data[9][:-2]
+    with pytest.raises(bfrs.BfrsError) as e:  # the crate's DifferentShardSize
+        bfrs.recover_segment_rs30_3_into(c, short, par, 5, np.empty(n, np.uint8))
+    assert e.value.code == bfrs.E_DIFFERENT_SHARD_SIZE
+    c.close()
