@@ -19,6 +19,7 @@
 // (shared), so it may be freed after bfrs_close; every other call needs the
 // context open.
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstring>
@@ -295,6 +296,27 @@ std::vector<size_t> slab_offsets(size_t S) {
   return off;
 }
 
+// done() of the slab copies: the H2D of row rows[i] (or row i) of a slab,
+// queued by the copy thread that filled it (the stream is thread-safe).
+struct SlabH2D {
+  const CodecObject *obj;
+  hipStream_t st;
+  size_t off, len;
+  std::vector<size_t> rows;  // empty: job i is row i
+  std::atomic<int> err_{0};
+  hipError_t err = hipSuccess;
+  SlabH2D(const CodecObject *o, hipStream_t s, size_t of, size_t ln, std::vector<size_t> r)
+      : obj(o), st(s), off(of), len(ln), rows(std::move(r)) {}
+  static void row_done(void *p, size_t i) {
+    auto *h = static_cast<SlabH2D *>(p);
+    const size_t r = h->rows.empty() ? i : h->rows[i];
+    const hipError_t e = hipMemcpyAsync(h->obj->d_row(r) + h->off, h->obj->h_row(r) + h->off,
+                                        h->len, hipMemcpyHostToDevice, h->st);
+    int expect = 0;
+    if (e != hipSuccess && h->err_.compare_exchange_strong(expect, 1)) h->err = e;
+  }
+};
+
 struct EventList {
   std::vector<hipEvent_t> v;
   ~EventList() {
@@ -328,15 +350,19 @@ int bfrs::encoder_encode_slabs(bfrs_encoder *e, const uint8_t *const *segs, cons
   const uint32_t kk = uint32_t(k);
   std::vector<const uint8_t *> din(k);
   std::vector<uint8_t *> dout(m);
+  std::vector<CopyJob> jobs(k);
   for (size_t q = 0; q < nslab; ++q) {
     const size_t o = off[q], len = off[q + 1] - o;
+    // slab q of every segment into the pinned rows on the copy threads, each
+    // row's H2D queued by the thread that copied it
     for (size_t i = 0; i < k; ++i) {
       const size_t avail = lens[i] > o ? std::min(len, lens[i] - o) : 0;
-      if (avail) host_copy(e->h_row(i) + o, segs[i] + o, avail);
-      if (avail < len) std::memset(e->h_row(i) + o + avail, 0, len - avail);
-      HIP_TRY(hipMemcpyAsync(e->d_row(i) + o, e->h_row(i) + o, len, hipMemcpyHostToDevice, st));
+      jobs[i] = CopyJob{e->h_row(i) + o, avail ? segs[i] + o : nullptr, avail, len - avail};
       din[i] = e->d_row(i) + o;
     }
+    SlabH2D h2d{e, st, o, len, {}};
+    host_copy_batch(jobs.data(), k, &SlabH2D::row_done, &h2d);
+    if (h2d.err) return hip_error(h2d.err, "slab H2D");
     hipEvent_t staged;
     if (int rc = ev.add(st, &staged)) return rc;
     HIP_TRY(hipStreamWaitEvent(ax, staged, 0));
@@ -582,12 +608,17 @@ int bfrs::decoder_restore_slabs(bfrs_decoder *d, const uint8_t *const *segs,
   std::vector<uint8_t *> drest(k);
   for (size_t q = 0; q < nslab; ++q) {
     const size_t o = off[q], len = off[q + 1] - o;
+    std::vector<CopyJob> jobs;
+    std::vector<size_t> rows;
     for (size_t r = 0; r < k + m; ++r) {
       const uint8_t *src = r < k ? segs[r] : par[r - k];
       if (!src) continue;
-      host_copy(d->h_row(r) + o, src + o, len);
-      HIP_TRY(hipMemcpyAsync(d->d_row(r) + o, d->h_row(r) + o, len, hipMemcpyHostToDevice, st));
+      jobs.push_back(CopyJob{d->h_row(r) + o, src + o, len, 0});
+      rows.push_back(r);
     }
+    SlabH2D h2d{d, st, o, len, rows};
+    host_copy_batch(jobs.data(), jobs.size(), &SlabH2D::row_done, &h2d);
+    if (h2d.err) return hip_error(h2d.err, "slab H2D");
     for (size_t i = 0; i < k; ++i) {
       dorig[i] = segs[i] ? d->d_row(i) + o : nullptr;
       drest[i] = segs[i] ? nullptr : d->d_row(i) + o;

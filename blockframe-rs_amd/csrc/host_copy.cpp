@@ -112,4 +112,39 @@ void host_copy(uint8_t *dst, const uint8_t *src, size_t n) {
   g_helpers.fetch_sub(helpers, std::memory_order_relaxed);
 }
 
+void host_copy_batch(const CopyJob *jobs, size_t count, void (*done)(void *, size_t), void *arg) {
+  if (count == 0) return;
+  size_t bytes = 0;
+  for (size_t i = 0; i < count; ++i) bytes += jobs[i].n + jobs[i].pad;
+  struct InFlight {
+    long calls = g_calls.fetch_add(1, std::memory_order_relaxed) + 1;
+    ~InFlight() { g_calls.fetch_sub(1, std::memory_order_relaxed); }
+  } in_flight;
+  constexpr size_t kPart = 4u << 20, kMaxParts = 8;
+  const size_t want = std::min<size_t>({max_parts(), count, std::max<size_t>(1, bytes / kPart)});
+  const long helpers = want > 1 ? reserve_helpers(long(want) - 1, in_flight.calls) : 0;
+  std::atomic<size_t> next{0};
+  auto work = [&] {
+    for (size_t i; (i = next.fetch_add(1, std::memory_order_relaxed)) < count;) {
+      const CopyJob &j = jobs[i];
+      if (j.n) std::memcpy(j.dst, j.src, j.n);
+      if (j.pad) std::memset(j.dst + j.n, 0, j.pad);
+      if (done) done(arg, i);
+    }
+  };
+  std::thread th[kMaxParts];
+  bool started[kMaxParts] = {};
+  for (long t = 0; t < helpers && size_t(t) < kMaxParts; ++t) {
+    try {
+      th[t] = std::thread(work);
+      started[t] = true;
+    } catch (...) {  // no thread: the others take its jobs
+    }
+  }
+  work();
+  for (size_t t = 0; t < kMaxParts; ++t)
+    if (started[t]) th[t].join();
+  g_helpers.fetch_sub(helpers, std::memory_order_relaxed);
+}
+
 }  // namespace bfrs

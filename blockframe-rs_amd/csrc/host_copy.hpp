@@ -10,4 +10,16 @@ namespace bfrs {
 // Never throws: a thread that cannot start leaves its part to the caller.
 void host_copy(uint8_t *dst, const uint8_t *src, size_t n);
 
+// Many copies at once (the slab-pipelined wrappers: one column slab of every
+// shard): job i copies n[i] bytes and zero-fills pad[i] more after them;
+// the calling thread and the helpers the shared budget grants (as host_copy)
+// take jobs in order, and done(i) runs on the thread that finished job i.
+// Never throws.
+struct CopyJob {
+  uint8_t *dst;
+  const uint8_t *src;
+  size_t n, pad;
+};
+void host_copy_batch(const CopyJob *jobs, size_t count, void (*done)(void *, size_t), void *arg);
+
 }  // namespace bfrs
