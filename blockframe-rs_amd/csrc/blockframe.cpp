@@ -33,12 +33,7 @@ class Prefault {
  public:
   Prefault(uint8_t *const *bufs, size_t n, size_t len) {
     auto touch = [bufs, n, len] {
-      for (size_t j = 0; j < n; ++j) {
-        volatile uint8_t *p = bufs[j];
-        if (!p || !len) continue;
-        for (size_t o = 0; o < len; o += 4096) p[o] = 0;
-        p[len - 1] = 0;
-      }
+      for (size_t j = 0; j < n; ++j) prefault_range(bufs[j], len);
     };
     try {
       th_ = std::thread(touch);

@@ -224,11 +224,7 @@ int bfrs::encoder_encode_to_host(bfrs_encoder *e, uint8_t *const *outs) {
     for (size_t j = 0; j < e->m; ++j) {
       uint8_t *p = outs[j];
       try {
-        touch.t.emplace_back([p, n] {
-          volatile uint8_t *q = p;
-          for (size_t o = 0; o < n; o += 4096) q[o] = 0;
-          q[n - 1] = 0;
-        });
+        touch.t.emplace_back([p, n] { prefault_range(p, n); });
       } catch (...) {  // no thread: the copy-out faults the pages itself
         break;
       }
@@ -263,28 +259,33 @@ int bfrs::encoder_encode_to_host(bfrs_encoder *e, uint8_t *const *outs) {
 
 namespace {
 // First-touch of fresh output buffers (the reference's to_vec / fresh Vec
-// outputs) on `parts` helper threads per buffer; returns when all are done.
-void touch_pages(uint8_t *const *bufs, size_t nbuf, size_t len, size_t parts) {
+// outputs) on `parts` helper threads per buffer, joined by join() or on
+// destruction (every exit path).
+struct TouchThreads {
   std::vector<std::thread> t;
-  const size_t per = (len + parts - 1) / parts;
-  for (size_t b = 0; b < nbuf; ++b)
-    for (size_t q = 0; q < parts; ++q) {
-      const size_t lo = q * per, hi = std::min(len, lo + per);
-      if (lo >= hi) continue;
-      uint8_t *p = bufs[b];
-      auto f = [p, lo, hi] {
-        volatile uint8_t *x = p;
-        for (size_t o = lo; o < hi; o += 4096) x[o] = 0;
-        x[hi - 1] = 0;
-      };
-      try {
-        t.emplace_back(f);
-      } catch (...) {
-        f();
+  void start(uint8_t *const *bufs, size_t nbuf, size_t len, size_t parts) {
+    const size_t per = (len + parts - 1) / parts;
+    for (size_t b = 0; b < nbuf; ++b)
+      for (size_t q = 0; q < parts; ++q) {
+        const size_t lo = q * per, hi = std::min(len, lo + per);
+        if (lo >= hi) continue;
+        uint8_t *p = bufs[b];
+        auto f = [p, lo, hi] { prefault_range(p + lo, hi - lo); };
+        try {
+          t.emplace_back(f);
+        } catch (...) {
+          f();
+        }
       }
-    }
-  for (auto &x : t) x.join();
-}
+  }
+  void join() {
+    for (auto &x : t)
+      if (x.joinable()) x.join();
+    t.clear();
+  }
+  ~TouchThreads() { join(); }
+};
+
 
 // Column slabs of ~8 MiB of 64-byte chunks; the last slab takes the tail.
 std::vector<size_t> slab_offsets(size_t S) {
@@ -351,6 +352,7 @@ int bfrs::encoder_encode_slabs(bfrs_encoder *e, const uint8_t *const *segs, cons
   std::vector<const uint8_t *> din(k);
   std::vector<uint8_t *> dout(m);
   std::vector<CopyJob> jobs(k);
+  TouchThreads touch;
   for (size_t q = 0; q < nslab; ++q) {
     const size_t o = off[q], len = off[q + 1] - o;
     // slab q of every segment into the pinned rows on the copy threads, each
@@ -376,8 +378,11 @@ int bfrs::encoder_encode_slabs(bfrs_encoder *e, const uint8_t *const *segs, cons
   }
   HIP_TRY(hipEventRecord(sl.ev_h2d, st));
   HIP_TRY(hipEventRecord(sl.ev_d2h, ax));
-  // the caller's fresh outputs fault in while the last slabs transfer
-  if (prefault_outputs()) touch_pages(outs, m, S, 1);
+  // the caller's fresh outputs fault in while the last slabs transfer (from
+  // the start of the call, beside the input copies, they cost more: r04n,
+  // DESIGN.md §7c)
+  if (prefault_outputs()) touch.start(outs, m, S, 1);
+  touch.join();
   for (size_t q = 0; q < nslab; ++q) {
     HIP_TRY(hipEventSynchronize(done[q]));
     for (size_t j = 0; j < m; ++j)
@@ -606,6 +611,8 @@ int bfrs::decoder_restore_slabs(bfrs_decoder *d, const uint8_t *const *segs,
   const uint32_t kk = uint32_t(k);
   std::vector<const uint8_t *> dorig(k), drec(m);
   std::vector<uint8_t *> drest(k);
+  uint8_t *const outs[1] = {out};
+  TouchThreads touch;
   for (size_t q = 0; q < nslab; ++q) {
     const size_t o = off[q], len = off[q + 1] - o;
     std::vector<CopyJob> jobs;
@@ -635,8 +642,8 @@ int bfrs::decoder_restore_slabs(bfrs_decoder *d, const uint8_t *const *segs,
   }
   HIP_TRY(hipEventRecord(sl.ev_h2d, st));
   HIP_TRY(hipEventRecord(sl.ev_d2h, ax));
-  uint8_t *const outs[1] = {out};
-  if (prefault_outputs()) touch_pages(outs, 1, S, 4);
+  if (prefault_outputs()) touch.start(outs, 1, S, 4);
+  touch.join();
   for (size_t q = 0; q < nslab; ++q) {
     HIP_TRY(hipEventSynchronize(done[q]));
     host_copy(out + off[q], d->h_row(target) + off[q], off[q + 1] - off[q]);

@@ -4,6 +4,8 @@
 #include "host_copy.hpp"
 
 #include <sched.h>
+#include <sys/mman.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -110,6 +112,31 @@ void host_copy(uint8_t *dst, const uint8_t *src, size_t n) {
   for (size_t t = 1; t < parts; ++t)
     if (started[t]) th[t].join();
   g_helpers.fetch_sub(helpers, std::memory_order_relaxed);
+}
+
+void prefault_range(uint8_t *p, size_t n) {
+  if (!p || !n) return;
+#ifndef MADV_POPULATE_WRITE
+#define MADV_POPULATE_WRITE 23
+#endif
+  static const uintptr_t page = uintptr_t(sysconf(_SC_PAGESIZE) > 0 ? sysconf(_SC_PAGESIZE) : 4096);
+  static std::atomic<bool> populate_ok{[] {  // BFRS_PREFAULT_POPULATE=0: always touch (A/B)
+    const char *e = std::getenv("BFRS_PREFAULT_POPULATE");
+    return !(e && e[0] == '0');
+  }()};
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p), e = a + n;
+  const uintptr_t lo = (a + page - 1) / page * page, hi = e / page * page;
+  volatile uint8_t *q = p;
+  if (hi > lo && populate_ok.load(std::memory_order_relaxed)) {
+    if (madvise(reinterpret_cast<void *>(lo), hi - lo, MADV_POPULATE_WRITE) == 0) {
+      q[0] = 0;  // the partial pages at either end
+      q[n - 1] = 0;
+      return;
+    }
+    populate_ok.store(false, std::memory_order_relaxed);  // older kernel: touch instead
+  }
+  for (size_t o = 0; o < n; o += 4096) q[o] = 0;
+  q[n - 1] = 0;
 }
 
 void host_copy_batch(const CopyJob *jobs, size_t count, void (*done)(void *, size_t), void *arg) {
