@@ -1146,12 +1146,20 @@ def blake3_device(ctx, sets, calls=10):
     nbytes = sum(r.numel() for r in rows)
     for _ in range(3):
         ctx.blake3_batch_dev(rows)
+    torch.cuda.synchronize()
+    wrapper = []
+    for _ in range(calls):  # the Python wrapper: marshalling + call + hex digests
+        t0 = time.perf_counter()
+        ctx.blake3_batch_dev(rows)
+        wrapper.append(time.perf_counter() - t0)
+    call, dig = ctx.blake3_batch_dev_call(rows)
     ts = []
-    for _ in range(calls):
+    for _ in range(calls):  # the C-ABI call itself, arguments marshalled once
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        hexes = ctx.blake3_batch_dev(rows)
+        call()
         ts.append(time.perf_counter() - t0)
+    hexes = [bytes(d).hex() for d in dig]
     check = None
     try:
         g = json.load(open(B3_GOLDEN))
@@ -1168,6 +1176,7 @@ def blake3_device(ctx, sets, calls=10):
             nbytes / (kern["group_kernel_ms"] * 1e-3) / 1e9 / b3_ceiling_gbps(B3_VALU_PER_64B_ALG), 4)
     return {"GBps": round(nbytes / best / 1e9, 1), "ms": round(best * 1e3, 3),
             "mean_ms": round(sum(ts) / len(ts) * 1e3, 3), "bytes": nbytes,
+            "python_wrapper_ms": round(min(wrapper) * 1e3, 3),
             "kernels": kern,
             "roofline": {"bound": "valu", "achieved": round(nbytes / best / 1e9, 1),
                          "peak": round(b3_ceiling_gbps(B3_VALU_PER_64B_ALG), 1), "unit": "GB/s",
@@ -1180,8 +1189,10 @@ def blake3_device(ctx, sets, calls=10):
                                  "(one parent per 1 KiB chunk) = the algorithm's VALU per 64 B of "
                                  "input; 256 CUs x 64 lane-ops per clock at 2.4 GHz"},
             "parity_check": check,
-            "what": "bfrs_blake3_batch_dev over C2's 128 x 32 MiB data segments in HBM, one call "
-                    "(upload + kernels + digest download), best of 10 wall-clock calls"}
+            "what": "bfrs_blake3_batch_dev over C2's 128 x 32 MiB data segments in HBM, one C-ABI "
+                    "call through ctypes (upload + kernels + digest download), arguments "
+                    "marshalled once, best of 10 wall-clock calls; python_wrapper_ms: the same "
+                    "through Context.blake3_batch_dev (per-call marshalling and hex digests)"}
 
 
 def blake3_kernel_times(ctx, rows, calls=3):
@@ -1196,20 +1207,43 @@ def blake3_kernel_times(ctx, rows, calls=3):
         from torch.profiler import ProfilerActivity, profile
         if ProfilerActivity.CUDA not in torch.profiler.supported_activities():
             return {"error": "torch profiler has no GPU activity on this build"}
-        ctx.blake3_batch_dev(rows)
+        call, _ = ctx.blake3_batch_dev_call(rows)
+        call()
+        torch.cuda.synchronize()
         with profile(activities=[ProfilerActivity.CUDA]) as prof:
             for _ in range(calls):
-                ctx.blake3_batch_dev(rows)
-        ev = [(e.name(), e.duration_ns() / 1e6) for e in prof.profiler.kineto_results.events()
-              if e.device_type() == DeviceType.CUDA and "blake3" in e.name()]
-        group = [d for n, d in ev if "group" in n]
-        reduce_ = [d for n, d in ev if "reduce" in n]
+                call()
+        allev = sorted((e.start_ns(), e.duration_ns(), e.name())
+                       for e in prof.profiler.kineto_results.events()
+                       if e.device_type() == DeviceType.CUDA)
+        group = [d / 1e6 for _, d, n in allev if "blake3" in n and "group" in n]
+        reduce_ = [d / 1e6 for _, d, n in allev if "blake3" in n and "reduce" in n]
         if len(group) < calls:
             return {"error": f"trace holds {len(group)} group-kernel dispatches"}
-        return {"group_kernel_ms": round(statistics.median(group), 4),
-                "reduce_kernels_ms_per_call": round(sum(reduce_) / calls, 4),
-                "reduce_launches_per_call": len(reduce_) // calls,
-                "how": f"torch.profiler over {calls} calls in this process"}
+        # each call's device span: its descriptor upload (the HtoD copy before
+        # its group kernel) to the end of its last reduce kernel or download
+        starts = [t for t, _, n in allev if "blake3" in n and "group" in n]
+        spans, timeline = [], None
+        for j, g0 in enumerate(starts):
+            g1 = starts[j + 1] if j + 1 < len(starts) else float("inf")
+            mine = [(t, d, n) for t, d, n in allev
+                    if (g0 <= t < g1 and "HtoD" not in n)
+                    or ("HtoD" in n and t < g0 and (j == 0 or t >= starts[j - 1]))]
+            if "HtoD" not in " ".join(n for _, _, n in mine):
+                continue
+            t0 = min(t for t, _, _ in mine)
+            spans.append((max(t + d for t, d, _ in mine) - t0) / 1e6)
+            timeline = [(round((t - t0) / 1e3, 1), round(d / 1e3, 1), n[:60]) for t, d, n in mine]
+        out = {"group_kernel_ms": round(statistics.median(group), 4),
+               "reduce_kernels_ms_per_call": round(sum(reduce_) / calls, 4),
+               "reduce_launches_per_call": len(reduce_) // calls,
+               "how": f"torch.profiler over {calls} C-ABI calls in this process"}
+        if not spans:
+            out["event_names"] = sorted({n[:60] for _, _, n in allev})[:12]
+        if spans:
+            out["device_span_ms"] = round(min(spans), 4)
+            out["last_call_timeline_us"] = timeline  # (start, duration, name)
+        return out
     except Exception as e:  # noqa: BLE001 - informative only
         return {"error": f"{type(e).__name__}: {e}"}
 

@@ -412,6 +412,26 @@ class Context:
             return hexes, [cvs[32 * i:32 * i + 32].tobytes() for i in range(n)]
         return hexes
 
+    def blake3_batch_dev_call(self, d_msgs, stream=None):
+        """bfrs_blake3_batch_dev with its arguments marshalled once: returns
+        (call, digests), where call() hashes the same device messages again
+        into the numpy array digests (n x 32 bytes) and raises BfrsError on
+        failure.  For timing the library call without Python's per-call
+        marshalling (bench.py); the tensors must outlive call."""
+        import numpy as np
+        n = len(d_msgs)
+        lens = [t.numel() for t in d_msgs]
+        pm, km = _ptr_array([self._addr(t) if l else None for t, l in zip(d_msgs, lens)])
+        ls = (_sz * max(1, n))(*lens)
+        dig = np.zeros((max(1, n), 32), np.uint8)
+        st = _stream_handle(stream, list(d_msgs))
+        fn, h, out = lib().bfrs_blake3_batch_dev, self.handle, dig.ctypes.data
+
+        def call():
+            _check(fn(h, n, pm, ls, None, out, None, st))
+            return km, ls  # keeps the ctypes arrays referenced by the closure
+        return call, dig[:n]
+
     # ---- host-memory batch API (host buffers: numpy arrays or CPU torch tensors)
     @staticmethod
     def _haddr(t) -> Optional[int]:
