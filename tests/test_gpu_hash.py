@@ -35,7 +35,14 @@ def test_gpu_blake3_batch_mixed(ctx, oracle):
     lens = [int(x) for x in rng.integers(0, 3 * G, size=40)] + [0, 1, 1024, G]
     arrs = [rng.integers(0, 256, size=n, dtype=np.uint8) for n in lens]
     ts = [_dev(a) if a.size else torch.empty(0, dtype=torch.uint8, device="cuda") for a in arrs]
-    assert ctx.blake3_batch_dev(ts) == [oracle.blake3_hex(a) for a in arrs]
+    want = [oracle.blake3_hex(a) for a in arrs]
+    assert ctx.blake3_batch_dev(ts) == want
+    # the prepared C-ABI call bench.py times: same digests, call after call
+    call, dig = ctx.blake3_batch_dev_call(ts)
+    for _ in range(2):
+        dig[:] = 0
+        call()
+        assert [bytes(d).hex() for d in dig] == want
 
 
 def test_gpu_blake3_rs_block(ctx, oracle):
