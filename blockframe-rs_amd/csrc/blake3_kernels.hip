@@ -174,18 +174,135 @@ __device__ __forceinline__ void parent_final(const uint32_t *a, const uint32_t *
 
 constexpr int kRow = 9;  // LDS row stride in words (odd: spreads a row's reads over banks)
 
+// ---- Quad-cooperative parent compression (the tree's narrow levels).
+// A lone wave compressing alone is latency-bound: ~700 dependent VALU ops per
+// compression, ~2.4 us each on the box, and the upper tree
+// levels are a chain of such compressions.  Here the four lanes of a quad
+// share one compression: lane q holds column q of the 4x4 state (v[q],
+// v[4+q], v[8+q], v[12+q]) and applies G to it; for the diagonal step rows
+// b, c, d rotate by 1, 2, 3 lanes inside the quad (DPP quad_perm), and back.
+// ~4x fewer dependent ops per compression; the message words come from the
+// children's LDS rows at lane-dependent offsets (left row, right row = left
+// + kRow), per round through the permuted schedule below.
+struct QuadSched {
+  // off[r][k] byte q: LDS word offset (from the left child's row) of the
+  // message word lane q uses in round r: k = 0, 1 column step (words 2q,
+  // 2q+1 of the round's message), k = 2, 3 diagonal step (8+2q, 9+2q)
+  uint32_t off[7][4];
+};
+constexpr QuadSched make_quad_sched() {
+  constexpr uint8_t P[16] = {2, 6, 3, 10, 7, 0, 4, 13, 1, 11, 12, 5, 9, 14, 15, 8};
+  QuadSched s{};
+  uint8_t S[16] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15};  // round r: word at i
+  for (int r = 0; r < 7; ++r) {
+    for (uint32_t q = 0; q < 4; ++q) {
+      const uint8_t pos[4] = {uint8_t(2 * q), uint8_t(2 * q + 1), uint8_t(8 + 2 * q),
+                              uint8_t(9 + 2 * q)};
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t w = S[pos[k]];
+        s.off[r][k] |= (w + (w >> 3) * (kRow - 8)) << (8 * q);  // words 8-15: the right row
+      }
+    }
+    uint8_t T[16] = {};
+    for (int i = 0; i < 16; ++i) T[i] = S[P[i]];
+    for (int i = 0; i < 16; ++i) S[i] = T[i];
+  }
+  return s;
+}
+constexpr QuadSched kQuadSched = make_quad_sched();
+
+// DPP quad_perm controls: lane i of each quad reads lane p_i
+constexpr int kQuadRot1 = 1 | (2 << 2) | (3 << 4) | (0 << 6);  // [1,2,3,0]
+constexpr int kQuadRot2 = 2 | (3 << 2) | (0 << 4) | (1 << 6);  // [2,3,0,1]
+constexpr int kQuadRot3 = 3 | (0 << 2) | (1 << 4) | (2 << 6);  // [3,0,1,2]
+
+template <int kCtrl>
+__device__ __forceinline__ uint32_t quad_perm(uint32_t x) {
+  return uint32_t(__builtin_amdgcn_mov_dpp(int(x), kCtrl, 0xF, 0xF, true));
+}
+
+// Parent of the two children whose rows start at `left` (right = left +
+// kRow) with `flags`, computed by the whole quad (all four lanes active, q =
+// lane & 3); lane q returns output words q (lo) and 4 + q (hi).
+__device__ __forceinline__ void parent_quad(const uint32_t *left, uint32_t q, uint32_t flags,
+                                            uint32_t &lo, uint32_t &hi) {
+  const uint32_t iv_a = q == 0 ? 0x6A09E667u : q == 1 ? 0xBB67AE85u : q == 2 ? 0x3C6EF372u : 0xA54FF53Au;
+  const uint32_t iv_b = q == 0 ? 0x510E527Fu : q == 1 ? 0x9B05688Cu : q == 2 ? 0x1F83D9ABu : 0x5BE0CD19u;
+  uint32_t a = iv_a, b = iv_b, c = iv_a;
+  uint32_t d = q == 2 ? 64u : q == 3 ? flags : 0u;  // counter lo, counter hi, block len, flags
+  const uint32_t sh = 8 * q;
+#pragma unroll
+  for (int r = 0; r < 7; ++r) {
+    const uint32_t x0 = left[__builtin_amdgcn_ubfe(kQuadSched.off[r][0], sh, 8)];
+    const uint32_t y0 = left[__builtin_amdgcn_ubfe(kQuadSched.off[r][1], sh, 8)];
+    const uint32_t x1 = left[__builtin_amdgcn_ubfe(kQuadSched.off[r][2], sh, 8)];
+    const uint32_t y1 = left[__builtin_amdgcn_ubfe(kQuadSched.off[r][3], sh, 8)];
+    B3_G(a, b, c, d, x0, y0);  // column step
+    b = quad_perm<kQuadRot1>(b);
+    c = quad_perm<kQuadRot2>(c);
+    d = quad_perm<kQuadRot3>(d);
+    B3_G(a, b, c, d, x1, y1);  // diagonal step
+    b = quad_perm<kQuadRot3>(b);
+    c = quad_perm<kQuadRot2>(c);
+    d = quad_perm<kQuadRot1>(d);
+  }
+  lo = a ^ c;
+  hi = b ^ d;
+}
+
+// One tree level of up to 64 parents by quads (quad i: parent i); an odd
+// last node is carried up unchanged.  Whole quads are active or not, so the
+// DPP reads inside a quad see only active lanes.
+__device__ __forceinline__ void level_by_quads(const uint32_t *src, uint32_t *dst, uint32_t n,
+                                               uint32_t t) {
+  const uint32_t i = t >> 2, q = t & 3, half = (n + 1) / 2;
+  if (i < half) {
+    uint32_t lo, hi;
+    if (2 * i + 1 < n) {
+      parent_quad(src + 2 * i * kRow, q, kParent, lo, hi);
+    } else {
+      lo = src[2 * i * kRow + q];
+      hi = src[2 * i * kRow + 4 + q];
+    }
+    dst[i * kRow + q] = lo;
+    dst[i * kRow + 4 + q] = hi;
+  }
+}
+
 // Pairs n <= 2 * 256 * per_lane nodes down to one in LDS (ping-pong buffers).
 // If `final_msg`, the top pair is finalised into msg_cv/digest instead.
-template <int kPerLane>
+// Levels of at most kQuadMax parents run by quads (latency), wider ones one
+// parent per lane (throughput); kQuadMax = 0: lanes only.
+template <int kPerLane, uint32_t kQuadMax>
 __device__ __forceinline__ void pair_down(uint32_t *buf0, uint32_t *buf1, uint32_t n, bool final_msg,
                                           uint32_t *out_cv, uint32_t *msg_cv, uint32_t *digest) {
+  static_assert(kQuadMax <= 64, "a quad level covers at most 64 parents");
   uint32_t *src = buf0, *dst = buf1;
   const uint32_t t = threadIdx.x;
   while (n > 1) {
     const uint32_t half = (n + 1) / 2;
     if (n == 2 && final_msg) {
-      if (t == 0) parent_final(src, src + kRow, msg_cv, digest);
+      if (kQuadMax > 0) {  // quad 0: the subtree CV, quad 1: the ROOT digest
+        if (t < 8) {
+          uint32_t lo, hi;
+          parent_quad(src, t & 3, t < 4 ? kParent : kParent | kRoot, lo, hi);
+          uint32_t *o = t < 4 ? msg_cv : digest;
+          o[t & 3] = lo;
+          o[4 + (t & 3)] = hi;
+        }
+      } else if (t == 0) {
+        parent_final(src, src + kRow, msg_cv, digest);
+      }
       return;
+    }
+    if (half <= kQuadMax) {
+      level_by_quads(src, dst, n, t);
+      __syncthreads();
+      uint32_t *tmp = src;
+      src = dst;
+      dst = tmp;
+      n = half;
+      continue;
     }
 #pragma unroll
     for (int j = 0; j < kPerLane; ++j) {
@@ -241,7 +358,11 @@ __device__ __forceinline__ Group find_group(const HashMsg *__restrict__ msgs, ui
   return r;
 }
 
-template <uint32_t kLevels>
+// kQuadMax: levels of at most that many parents by quads.  Kernel 1 is
+// throughput-bound and launched with 0: quads at its level 3 (32 parents)
+// would save ~0.4% of its issue slots, but the quad code pushed the kernel
+// past its 64-VGPR cap (17 spilled registers), DESIGN.md §7b.
+template <uint32_t kLevels, uint32_t kQuadMax>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void blake3_group_kernel(
     const HashMsg *__restrict__ msgs, uint32_t n_msgs, uint32_t *__restrict__ group_cvs,
     uint32_t *__restrict__ msg_cvs, uint32_t *__restrict__ digests) {
@@ -277,7 +398,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
   for (int w = 0; w < 8; ++w) lds[0][t * kRow + w] = cv[w];
   __syncthreads();
   if (g.single) {  // the whole message: pair down to the root here
-    pair_down<1>(lds[0], lds[1], nchunks, true, nullptr, msg_cvs + 8 * g.msg, digests + 8 * g.msg);
+    pair_down<1, kQuadMax>(lds[0], lds[1], nchunks, true, nullptr, msg_cvs + 8 * g.msg,
+                           digests + 8 * g.msg);
     return;
   }
   // kLevels levels (256 -> 256 >> kLevels nodes); an odd last node is carried up
@@ -285,7 +407,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
 #pragma unroll
   for (uint32_t lv = 0; lv < kLevels; ++lv) {
     const uint32_t half = (n + 1) / 2;
-    if (t < half) {
+    if (half <= kQuadMax) {
+      level_by_quads(src, dst, n, t);
+    } else if (t < half) {
       uint32_t r[8];
       if (2 * t + 1 < n) {
         parent_cv(src + 2 * t * kRow, src + (2 * t + 1) * kRow, r);
@@ -309,6 +433,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
   }
 }
 
+// Latency-bound (a chain of levels per job): every level of <= 64 parents by quads.
+template <uint32_t kQuadMax>
 __global__ __launch_bounds__(256) void blake3_reduce_kernel(const HashReduce *__restrict__ jobs,
                                                             const uint32_t *__restrict__ in_cvs,
                                                             uint32_t *__restrict__ out_cvs,
@@ -321,7 +447,7 @@ __global__ __launch_bounds__(256) void blake3_reduce_kernel(const HashReduce *__
 #pragma unroll
     for (int w = 0; w < 8; ++w) lds[0][i * kRow + w] = in_cvs[8 * (j.first + i) + w];
   __syncthreads();
-  pair_down<kReduceFanIn / 512>(lds[0], lds[1], j.n, j.final != 0,
+  pair_down<kReduceFanIn / 512, kQuadMax>(lds[0], lds[1], j.n, j.final != 0,
                                 j.final ? nullptr : out_cvs + 8 * j.out, msg_cvs + 8 * j.msg,
                                 digests + 8 * j.msg);
 }
@@ -332,26 +458,27 @@ hipError_t launch_blake3_groups(const HashMsg *d_msgs, uint32_t n_msgs, uint32_t
                                 uint32_t levels, uint32_t *d_group_cvs, uint32_t *d_msg_cvs,
                                 uint32_t *d_digests, hipStream_t stream) {
   if (n_groups == 0 || n_msgs == 0) return hipSuccess;
-#ifdef BFRS_AB_VARIANTS  // 2 levels: measurement build only (tools/b3_levels_ab.py)
-  if (levels == 2)
-    hipLaunchKernelGGL(blake3_group_kernel<2>, dim3(n_groups), dim3(256), 0, stream, d_msgs, n_msgs,
-                       d_group_cvs, d_msg_cvs, d_digests);
-  else
-#endif
-  if (levels == 3)
-    hipLaunchKernelGGL(blake3_group_kernel<3>, dim3(n_groups), dim3(256), 0, stream, d_msgs, n_msgs,
-                       d_group_cvs, d_msg_cvs, d_digests);
-  else
-    return hipErrorInvalidValue;
+  if (levels != 3) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((blake3_group_kernel<3, 0>), dim3(n_groups), dim3(256), 0, stream, d_msgs,
+                     n_msgs, d_group_cvs, d_msg_cvs, d_digests);
   return hipGetLastError();
 }
 
-hipError_t launch_blake3_reduce(const HashReduce *d_jobs, uint32_t n_jobs, const uint32_t *d_in,
-                                uint32_t *d_out, uint32_t *d_msg_cvs, uint32_t *d_digests,
-                                hipStream_t stream) {
+hipError_t launch_blake3_reduce(const HashReduce *d_jobs, uint32_t n_jobs, bool quads,
+                                const uint32_t *d_in, uint32_t *d_out, uint32_t *d_msg_cvs,
+                                uint32_t *d_digests, hipStream_t stream) {
   if (n_jobs == 0) return hipSuccess;
-  hipLaunchKernelGGL(blake3_reduce_kernel, dim3(n_jobs), dim3(256), 0, stream, d_jobs, d_in, d_out,
-                     d_msg_cvs, d_digests);
+#ifdef BFRS_AB_VARIANTS
+  if (!quads) {
+    hipLaunchKernelGGL((blake3_reduce_kernel<0>), dim3(n_jobs), dim3(256), 0, stream, d_jobs, d_in,
+                       d_out, d_msg_cvs, d_digests);
+    return hipGetLastError();
+  }
+#else
+  if (!quads) return hipErrorInvalidValue;
+#endif
+  hipLaunchKernelGGL((blake3_reduce_kernel<64>), dim3(n_jobs), dim3(256), 0, stream, d_jobs, d_in,
+                     d_out, d_msg_cvs, d_digests);
   return hipGetLastError();
 }
 

@@ -13,15 +13,14 @@ namespace bfrs {
 
 namespace {
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
-// Tree levels kernel 1 pairs in a group of a multi-group message
-// (hash_kernels.hpp); the measurement build also takes BFRS_B3_GROUP_LEVELS=2,
-// read per call (same-process A/B, tools/b3_levels_ab.py).
-uint32_t group_levels() {
+// Narrow tree levels by quads (the product); the measurement build also
+// takes BFRS_B3_QUADS=0, read per call (same-process A/B, tools/b3_levels_ab.py).
+bool quads() {
 #ifdef BFRS_AB_VARIANTS
-  const char *e = std::getenv("BFRS_B3_GROUP_LEVELS");
-  if (e && std::strcmp(e, "2") == 0) return 2;
+  const char *e = std::getenv("BFRS_B3_QUADS");
+  if (e && std::strcmp(e, "0") == 0) return false;
 #endif
-  return kGroupLevels;
+  return true;
 }
 }  // namespace
 
@@ -62,7 +61,8 @@ int Context::blake3_dev(size_t n, const uint8_t *const *d_msgs, const size_t *le
   // one) at group index * (256 >> levels).
   std::vector<std::vector<HashReduce>> levels;
   std::vector<uint32_t> cnt(n), off(n);
-  const uint32_t glv = group_levels(), group_out = kGroupChunks >> glv;
+  const uint32_t glv = kGroupLevels, group_out = kGroupChunks >> glv;
+  const bool q = quads();
   for (size_t i = 0; i < n; ++i) {
     if (g_count[i] == 1) {  // finalised by kernel 1
       cnt[i] = 1;
@@ -154,7 +154,8 @@ int Context::blake3_dev(size_t n, const uint8_t *const *d_msgs, const size_t *le
   uint32_t *cur = d_cv0, *nxt = d_cv1;
   jo = 0;
   for (auto &l : levels) {
-    HIP_TRY(launch_blake3_reduce(d_jobs + jo, uint32_t(l.size()), cur, nxt, d_msg_cvs, d_digests, s));
+    HIP_TRY(launch_blake3_reduce(d_jobs + jo, uint32_t(l.size()), q, cur, nxt, d_msg_cvs, d_digests,
+                                 s));
     jo += l.size();
     std::swap(cur, nxt);
   }

@@ -19,7 +19,7 @@ constexpr uint32_t kReduceFanIn = 512;                  // CVs one kernel-2 work
 // they are left to kernel 2, whose first levels over 512 nodes use every
 // lane.  Three levels rather than two also halve kernel 2's first-level jobs,
 // which then fit the chip in one round.
-constexpr uint32_t kGroupLevels = 3;  // default; BFRS_B3_GROUP_LEVELS = 2 or 3 (A/B)
+constexpr uint32_t kGroupLevels = 3;
 constexpr uint32_t kGroupOutMax = kGroupChunks >> 2;  // level-2 nodes per group (the most)
 
 // One message of a kernel-1 launch.  Workgroup w belongs to the message m
@@ -48,8 +48,11 @@ struct alignas(16) HashReduce {
 hipError_t launch_blake3_groups(const HashMsg *d_msgs, uint32_t n_msgs, uint32_t n_groups,
                                 uint32_t levels, uint32_t *d_group_cvs, uint32_t *d_msg_cvs,
                                 uint32_t *d_digests, hipStream_t stream);
-hipError_t launch_blake3_reduce(const HashReduce *d_jobs, uint32_t n_jobs, const uint32_t *d_in,
-                                uint32_t *d_out, uint32_t *d_msg_cvs, uint32_t *d_digests,
-                                hipStream_t stream);
+// quads: kernel 2's levels of <= 64 parents by quad-cooperative compressions
+// (the product); false (one parent per lane) exists in the measurement build
+// alone.
+hipError_t launch_blake3_reduce(const HashReduce *d_jobs, uint32_t n_jobs, bool quads,
+                                const uint32_t *d_in, uint32_t *d_out, uint32_t *d_msg_cvs,
+                                uint32_t *d_digests, hipStream_t stream);
 
 }  // namespace bfrs

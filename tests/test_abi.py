@@ -65,11 +65,12 @@ PRODUCT_KERNELS = {
     "void bfrs::(anonymous namespace)::gf_apply_ring_kernel<6, false, 16u, 1, 1, 1, 0>(bfrs::KernArgs)",
     "bfrs::(anonymous namespace)::gf_tail_kernel(bfrs::KernArgs)",
     # device BLAKE3 (the Merkle re-verify of the read/repair path)
-    # (3 tree levels inside a group; the 2-level A/B variant is in libbfrs_ab.so)
-    "void bfrs::(anonymous namespace)::blake3_group_kernel<3u>(bfrs::HashMsg const*, unsigned int, "
-    "unsigned int*, unsigned int*, unsigned int*)",
-    "bfrs::(anonymous namespace)::blake3_reduce_kernel(bfrs::HashReduce const*, unsigned int const*, "
-    "unsigned int*, unsigned int*, unsigned int*)",
+    # (3 tree levels inside a group; kernel 2's levels of <= 64 parents by
+    # quads -- the lanes-only kernel 2 is in libbfrs_ab.so)
+    "void bfrs::(anonymous namespace)::blake3_group_kernel<3u, 0u>(bfrs::HashMsg const*, "
+    "unsigned int, unsigned int*, unsigned int*, unsigned int*)",
+    "void bfrs::(anonymous namespace)::blake3_reduce_kernel<64u>(bfrs::HashReduce const*, "
+    "unsigned int const*, unsigned int*, unsigned int*, unsigned int*)",
 }
 
 

@@ -1,9 +1,11 @@
-"""Same-process A/B of the device BLAKE3's kernel-1 tree depth
-(BFRS_B3_GROUP_LEVELS = 2 / 3, read per call): C2's 128 x 32 MiB HBM-resident
-segments, alternating variants, best and median wall time per call and the
-group / reduce kernel times from torch's profiler.  Loads the measurement
-build (make -C blockframe-rs_amd/csrc ab -> libbfrs_ab.so, BFRS_LIB).  GPU box
-only."""
+"""Same-process A/B of a device BLAKE3 variant of the measurement build, read
+per call from the environment: round 4's kernel-1 tree depth
+(BFRS_B3_GROUP_LEVELS = 2 / 3, since removed) and now kernel 2's quad levels
+(AB_VAR=BFRS_B3_QUADS, values 1 / 0, the default).  C2's 128 x 32 MiB
+HBM-resident segments, alternating variants, best and median wall time per
+call and the group / reduce kernel times from torch's profiler.  Loads the
+measurement build (make -C blockframe-rs_amd/csrc ab -> libbfrs_ab.so,
+BFRS_LIB).  GPU box only."""
 import json
 import os
 import statistics
@@ -35,12 +37,14 @@ def main():
     g = torch.Generator(device="cuda").manual_seed(1)
     buf = torch.randint(0, 256, (nseg * S,), dtype=torch.uint8, device="cuda", generator=g)
     segs = [buf[i * S:(i + 1) * S] for i in range(nseg)]
-    res = {"2": [], "3": []}
-    kern = {"2": [], "3": []}
+    var = os.environ.get("AB_VAR", "BFRS_B3_QUADS")
+    va, vb = os.environ.get("AB_VALUES", "1,0").split(",")
+    res = {va: [], vb: []}
+    kern = {va: [], vb: []}
     digests = {}
     for r in range(rounds):
-        for lv in (("2", "3") if r % 2 == 0 else ("3", "2")):
-            os.environ["BFRS_B3_GROUP_LEVELS"] = lv
+        for lv in ((va, vb) if r % 2 == 0 else (vb, va)):
+            os.environ[var] = lv
             t0 = time.perf_counter()
             while time.perf_counter() - t0 < 0.3:  # settle
                 ctx.blake3_batch_dev(segs)
@@ -51,10 +55,10 @@ def main():
                 res[lv].append(time.perf_counter() - t1)
             digests[lv] = d
             kern[lv].append(kernel_ms(ctx, segs))
-    assert digests["2"] == digests["3"]
-    out = {"what": "device BLAKE3 of 128 x 32 MiB, kernel-1 tree levels 2 vs 3, alternated in one "
+    assert digests[va] == digests[vb]
+    out = {"what": f"device BLAKE3 of 128 x 32 MiB, {var} = {va} vs {vb}, alternated in one "
                    "process (tools/b3_levels_ab.py, measurement build)", "digests_equal": True}
-    for lv in ("2", "3"):
+    for lv in (va, vb):
         ts = res[lv]
         out[lv] = {"best_ms": round(min(ts) * 1e3, 4), "median_ms": round(statistics.median(ts) * 1e3, 4),
                    "GBps_best": round(nseg * S / min(ts) / 1e9, 1),
