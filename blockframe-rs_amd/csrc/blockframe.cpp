@@ -33,7 +33,8 @@ class Prefault {
  public:
   Prefault(uint8_t *const *bufs, size_t n, size_t len) {
     auto touch = [bufs, n, len] {
-      for (size_t j = 0; j < n; ++j) prefault_range(bufs[j], len);
+      for (size_t j = 0; j < n; ++j)
+        if (!host_registered(bufs[j], len)) prefault_range(bufs[j], len);  // registered: pinned
     };
     try {
       th_ = std::thread(touch);
