@@ -32,8 +32,6 @@ using namespace bfrs;
 
 namespace {
 
-// BFRS_PREFAULT_OUTPUTS (default 1): fault the wrapper's fresh output
-// buffers in while the device works (encoder_encode_to_host).
 // Helper threads per output buffer that fault it in (BFRS_PREFAULT_PARTS,
 // 1-8; 0 or unset: the call's default).  A/B knob.
 size_t prefault_parts(size_t dflt) {
@@ -44,6 +42,8 @@ size_t prefault_parts(size_t dflt) {
   return v >= 1 && v <= 8 ? size_t(v) : dflt;
 }
 
+// BFRS_PREFAULT_OUTPUTS (default 1): fault the wrapper's fresh output
+// buffers in while the device works (encoder_encode_to_host).
 bool prefault_outputs() {
   static const bool on = [] {
     const char *e = std::getenv("BFRS_PREFAULT_OUTPUTS");
@@ -229,18 +229,12 @@ int bfrs::encoder_encode_to_host(bfrs_encoder *e, uint8_t *const *outs) {
         if (x.joinable()) x.join();
     }
   } touch;
-  // A registered output (bfrs_host_register: BlockFrame's reused parity
-  // buffers or output mmap) takes its D2H straight from the device: no
-  // pinned row, no copy-out, no first touch.
-  std::vector<char> direct(e->m);
-  bool any_direct = false;
-  for (size_t j = 0; j < e->m; ++j) any_direct |= (direct[j] = host_registered(outs[j], e->shard_bytes));
   if (prefault_outputs()) {
     const size_t n = e->shard_bytes;
     for (size_t j = 0; j < e->m; ++j) {
       uint8_t *p = outs[j];
       try {
-        if (direct[j]) touch.t.emplace_back();  // nothing to fault: an empty slot
+        if (host_registered(p, n)) touch.t.emplace_back();  // pinned already: an empty slot
         else touch.t.emplace_back([p, n] { prefault_range(p, n); });
       } catch (...) {  // no thread: the copy-out faults the pages itself
         break;
@@ -248,8 +242,8 @@ int bfrs::encoder_encode_to_host(bfrs_encoder *e, uint8_t *const *outs) {
     }
   }
   for (size_t j = 0; j < e->m; ++j) {
-    HIP_TRY(hipMemcpyAsync(direct[j] ? outs[j] : e->h_row(e->k + j), e->d_row(e->k + j),
-                           e->shard_bytes, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(e->h_row(e->k + j), e->d_row(e->k + j), e->shard_bytes,
+                           hipMemcpyDeviceToHost, st));
     HIP_TRY(hipEventCreateWithFlags(&done[j], hipEventDisableTiming));
     HIP_TRY(hipEventRecord(done[j], st));
   }
@@ -261,17 +255,16 @@ int bfrs::encoder_encode_to_host(bfrs_encoder *e, uint8_t *const *outs) {
     HIP_TRY(hipEventSynchronize(done[j]));
     if (j < touch.t.size() && touch.t[j].joinable()) touch.t[j].join();
     const auto t1 = clk::now();
-    if (!direct[j]) host_copy(outs[j], e->h_row(e->k + j), e->shard_bytes);
+    host_copy(outs[j], e->h_row(e->k + j), e->shard_bytes);
     wait_ms += std::chrono::duration<double, std::milli>(t1 - t0).count();
     copy_ms += std::chrono::duration<double, std::milli>(clk::now() - t1).count();
   }
   if (std::getenv("BFRS_TRACE"))  // measurement aid (tools/crate_probe.py)
     std::fprintf(stderr, "bfrs trace: encode_to_host wait %.3f ms, copy-out %.3f ms\n", wait_ms,
                  copy_ms);
-  // the pinned rows hold the recovery shards too, as after encode() (unless
-  // some went straight to registered outputs)
+  // the pinned rows hold the recovery shards too, as after encode()
   e->encoded = true;
-  e->fetched_to_pinned = !any_direct;
+  e->fetched_to_pinned = true;
   return BFRS_OK;
 }
 
@@ -372,9 +365,6 @@ int bfrs::encoder_encode_slabs(bfrs_encoder *e, const uint8_t *const *segs, cons
   std::vector<uint8_t *> dout(m);
   std::vector<CopyJob> jobs(k);
   TouchThreads touch;
-  std::vector<char> direct(m);  // registered outputs: D2H straight into them
-  bool any_direct = false;
-  for (size_t j = 0; j < m; ++j) any_direct |= (direct[j] = host_registered(outs[j], S));
   for (size_t q = 0; q < nslab; ++q) {
     const size_t o = off[q], len = off[q + 1] - o;
     // slab q of every segment into the pinned rows on the copy threads, each
@@ -394,7 +384,7 @@ int bfrs::encoder_encode_slabs(bfrs_encoder *e, const uint8_t *const *segs, cons
     int rc = encode_batch_on(e->ctx, 1, &kk, m, len, din.data(), dout.data(), ax);
     if (rc) return rc;
     for (size_t j = 0; j < m; ++j)
-      HIP_TRY(hipMemcpyAsync((direct[j] ? outs[j] : e->h_row(k + j)) + o, e->d_row(k + j) + o, len,
+      HIP_TRY(hipMemcpyAsync(e->h_row(k + j) + o, e->d_row(k + j) + o, len,
                              hipMemcpyDeviceToHost, ax));
     if ((rc = ev.add(ax, &done[q]))) return rc;
   }
@@ -408,11 +398,11 @@ int bfrs::encoder_encode_slabs(bfrs_encoder *e, const uint8_t *const *segs, cons
   for (size_t q = 0; q < nslab; ++q) {
     HIP_TRY(hipEventSynchronize(done[q]));
     for (size_t j = 0; j < m; ++j)
-      if (!direct[j]) host_copy(outs[j] + off[q], e->h_row(k + j) + off[q], off[q + 1] - off[q]);
+      host_copy(outs[j] + off[q], e->h_row(k + j) + off[q], off[q + 1] - off[q]);
   }
   e->received = k;
   e->encoded = true;
-  e->fetched_to_pinned = !any_direct;
+  e->fetched_to_pinned = true;
   return BFRS_OK;
 }
 
@@ -600,8 +590,7 @@ void bfrs_decoder_free(bfrs_decoder *d) { delete d; }
 int bfrs::decoder_restored_to_host(bfrs_decoder *d, size_t index, uint8_t *out) {
   if (!d->decoded || index >= d->restored.size() || !d->restored[index])
     return set_error(BFRS_E_NOT_RESTORED, "original shard was not restored");
-  const bool direct = !d->fetched[index] && host_registered(out, d->shard_bytes);
-  if (!direct && (d->pool->staging == Staging::kPinned || d->fetched[index])) {  // via the pinned row
+  if (d->pool->staging == Staging::kPinned || d->fetched[index]) {  // via the pinned row
     const uint8_t *data;
     size_t len;
     int rc = bfrs_decoder_restored_original(d, index, &data, &len);
@@ -636,7 +625,6 @@ int bfrs::decoder_restore_slabs(bfrs_decoder *d, const uint8_t *const *segs,
   std::vector<uint8_t *> drest(k);
   uint8_t *const outs[1] = {out};
   TouchThreads touch;
-  const bool direct = host_registered(out, S);  // registered: D2H straight into it
   for (size_t q = 0; q < nslab; ++q) {
     const size_t o = off[q], len = off[q + 1] - o;
     std::vector<CopyJob> jobs;
@@ -660,8 +648,8 @@ int bfrs::decoder_restore_slabs(bfrs_decoder *d, const uint8_t *const *segs,
     HIP_TRY(hipStreamWaitEvent(ax, staged, 0));
     int rc = decode_batch_on(d->ctx, 1, &kk, m, len, dorig.data(), drec.data(), drest.data(), ax);
     if (rc) return rc;
-    HIP_TRY(hipMemcpyAsync((direct ? out : d->h_row(target)) + o, d->d_row(target) + o, len,
-                           hipMemcpyDeviceToHost, ax));
+    HIP_TRY(hipMemcpyAsync(d->h_row(target) + o, d->d_row(target) + o, len, hipMemcpyDeviceToHost,
+                           ax));
     if ((rc = ev.add(ax, &done[q]))) return rc;
   }
   HIP_TRY(hipEventRecord(sl.ev_h2d, st));
@@ -670,12 +658,12 @@ int bfrs::decoder_restore_slabs(bfrs_decoder *d, const uint8_t *const *segs,
   touch.join();
   for (size_t q = 0; q < nslab; ++q) {
     HIP_TRY(hipEventSynchronize(done[q]));
-    if (!direct) host_copy(out + off[q], d->h_row(target) + off[q], off[q + 1] - off[q]);
+    host_copy(out + off[q], d->h_row(target) + off[q], off[q + 1] - off[q]);
   }
   d->decoded = true;
   d->restored.assign(k, 0);
   d->fetched.assign(k, 0);
   for (size_t i = 0; i < k; ++i) d->restored[i] = !d->orig_present[i];
-  d->fetched[target] = !direct;  // its pinned row holds the whole shard
+  d->fetched[target] = 1;  // its pinned row holds the whole shard
   return BFRS_OK;
 }

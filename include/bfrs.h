@@ -133,10 +133,9 @@ size_t bfrs_shard_pitch(size_t shard_bytes);
  * added shard).  Opting in changes one rule: the DMA reads a registered
  * shard asynchronously, so its bytes must stay unchanged until the encode()
  * / decode() that consumes it returns (the wrappers return after both).
- * An OUTPUT buffer of bfrs_generate_parity / bfrs_recover_segment_rs30_3
- * that lies inside a registered range (a caller reusing its parity buffers
- * across blocks) receives its D2H straight from the device, with no pinned
- * row and no copy-out.
+ * Outputs are always written through the slot's pinned rows: device writes
+ * straight into a caller-registered range, once that range was unregistered
+ * and freed, left the runtime faulting a later pageable copy.
  * Process-wide (HIP registration, any context); unregister before unmapping
  * or freeing the range.  BFRS_E_HIP if the runtime refuses the range. */
 int bfrs_host_register(void *ptr, size_t len);

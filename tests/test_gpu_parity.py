@@ -842,14 +842,18 @@ def _page_isolated(nbytes, fill):
 
 @pytest.mark.parametrize("inputs_registered", [False, True])
 @pytest.mark.parametrize("n", [(1 << 20) + 64 * 5, (16 << 20) + 38])
-def test_registered_outputs_take_the_d2h_straight(bfrs, oracle, inputs_registered, n):
-    """Outputs the caller registered (BlockFrame reusing its parity buffers
-    across blocks) receive their D2H straight from the device, with no pinned
-    row and no copy-out.  That holds on both the whole-shard path (small
-    shards, registered inputs) and the slab-pipelined one (>= 16 MiB, staged
-    inputs). One output of three is left unregistered, so one call mixes both
-    kinds. Every byte is checked against the oracle, and the bytes next to
-    each output stay untouched."""
+def test_registered_outputs_written_through_pinned_rows(bfrs, oracle, inputs_registered, n):
+    """Outputs inside a registered range (a caller reusing registered buffers)
+    are written like any other output: D2H into the slot's pinned rows, then
+    copied out.  They skip only the first-touch helper, because registered
+    pages are resident.  The test covers the whole-shard path (small shards,
+    registered inputs) and the slab-pipelined one (>= 16 MiB, staged
+    inputs). Every byte is checked against the oracle, and the bytes next to
+    each output stay untouched.  Regression: a version that DMA'd straight
+    into registered outputs left the HIP runtime in a state where, once those
+    ranges were unregistered and freed, the next pageable H2D faulted the GPU
+    (test_generate_parity_slab_pipeline_vs_oracle[direct] right after this
+    one, r04t)."""
     c = bfrs.Context(0)
     rng = np.random.default_rng(n % 977 + inputs_registered)
     data = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(30)]
