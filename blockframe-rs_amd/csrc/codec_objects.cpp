@@ -390,10 +390,10 @@ int bfrs::encoder_encode_slabs(bfrs_encoder *e, const uint8_t *const *segs, cons
   }
   HIP_TRY(hipEventRecord(sl.ev_h2d, st));
   HIP_TRY(hipEventRecord(sl.ev_d2h, ax));
-  // the caller's fresh outputs fault in while the last slabs transfer (from
-  // the start of the call, beside the input copies, they cost more: r04n,
-  // DESIGN.md §7c)
-  if (prefault_outputs()) touch.start(outs, m, S, prefault_parts(1));
+  // the caller's fresh outputs fault in while the last slabs transfer, 4
+  // threads per output (from the start of the call, beside the input copies,
+  // they cost more: r04n; 1 thread per output: r04v)
+  if (prefault_outputs()) touch.start(outs, m, S, prefault_parts(4));
   touch.join();
   for (size_t q = 0; q < nslab; ++q) {
     HIP_TRY(hipEventSynchronize(done[q]));

@@ -4,7 +4,7 @@
 # (1, default) against one written byte per page (0).  MODE=early: the slab
 # paths fault the outputs in from the start of the call (1) or after the last
 # slab's copies (0); that knob was removed after r04n (worse).  MODE=parts:
-# helper threads per fresh output, 4 against the encode default of 1.
+# helper threads per fresh output, 4 against 1 (the encode default until r04v).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out; mkdir -p "$OUT"
@@ -14,7 +14,7 @@ MODE=${MODE:-populate}
 case $MODE in
   populate) VAR=BFRS_PREFAULT_POPULATE; VALS="1 0 1 0";;
   early) VAR=BFRS_PREFAULT_EARLY; VALS="1 0 1 0";;
-  parts) VAR=BFRS_PREFAULT_PARTS; VALS="4 1 4 1";;  # threads per output (encode default 1)
+  parts) VAR=BFRS_PREFAULT_PARTS; VALS="4 1 4 1";;  # threads per output (r04v: encode 1 -> 4)
 esac
 for v in $VALS; do
   env $VAR=$v timeout -k 10 300 python bench.py $ARGS > "$OUT/pf_${TAG}_${MODE}$v.json" 2> "$OUT/pf_${TAG}_${MODE}$v.err"
