@@ -950,3 +950,39 @@ def test_recover_rs30_3_slab_pipeline_vs_originals(bfrs, oracle):
         bfrs.recover_segment_rs30_3_into(c, short, par, 5, np.empty(n, np.uint8))
     assert e.value.code == bfrs.E_DIFFERENT_SHARD_SIZE
     c.close()
+
+
+@pytest.mark.parametrize("k,m,erased,use", [
+    (30, 3, [2, 11, 29], [0, 1, 2]), (8, 3, [0, 7], [2, 1]), (20, 3, [5], [1]),
+    (3, 5, [0, 1, 2], [0, 3, 4]), (17, 6, [1, 4, 9, 16], [5, 0, 2, 3])])
+def test_product_follows_the_algebra(ctx, oracle, k, m, erased, use):
+    """The HIP path against plain algebra rather than the oracle's transform
+    (tests/test_rs_interpolation.py): encode = per-chunk Lagrange
+    interpolation on the field points, decode from exactly k shards with a
+    corrupted recovery shard = the linear system's unique solution."""
+    import test_rs_interpolation as alg
+    exp = np.array([oracle.gf_exp(i) for i in range(alg.ORDER)], np.int64)
+    log = np.zeros(65536, np.int64)
+    log[1:] = [oracle.gf_log(x) for x in range(1, 65536)]
+    gf = (exp, log)
+    rng = np.random.default_rng(31 * k + m)
+    n = 4096 + 64 * 3
+    originals = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(k)]
+    rec = ctx.encode(originals, m)
+    want = alg.interpolated_parity(gf, oracle, originals, m)
+    assert all(np.array_equal(rec[j], want[j]) for j in range(m))
+    rec = [r.copy() for r in rec]
+    rec[use[0]][int(rng.integers(0, n))] ^= 0x3C
+    out = ctx.decode([None if i in erased else originals[i] for i in range(k)],
+                     [rec[j] if j in use else None for j in range(m)])
+    coef = alg._coef_logs(gf, oracle, k, m)
+    rhs = []
+    for j in use:
+        r = alg._symbols(rec[j])
+        for i in range(k):
+            if i not in erased:
+                r = r ^ alg._mul(gf, coef[j, i], alg._symbols(originals[i]))
+        rhs.append(r)
+    x = alg._solve(gf, coef[np.ix_(use, erased)], np.stack(rhs))
+    for a, i in enumerate(erased):
+        assert np.array_equal(out[i], alg._bytes(x[a])), (k, m, i)
