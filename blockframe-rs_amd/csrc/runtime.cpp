@@ -268,6 +268,8 @@ int Context::init(int dev) {
   if (dev < 0 || dev >= n) return set_error(BFRS_E_NO_DEVICE, "HIP device id out of range");
   device = dev;
   if (const char *e = std::getenv("BFRS_PLAN_CACHE")) max_plans = std::max(1, atoi(e));
+  if (const char *e = std::getenv("BFRS_PIPE_SLOTS"))
+    pipe_slots = std::min(kPipeSlotsMax, std::max(2, atoi(e)));
   codec_pool->device = dev;
   if (const char *e = std::getenv("BFRS_CODEC_SLOTS")) {
     char *end = nullptr;
@@ -305,7 +307,8 @@ int Context::init(int dev) {
   // the codec streams first: created before any copy, consecutively
   if (int rc = codec_pool->init_streams(codec_streams, copy_streams)) return rc;
   HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
-  for (auto &ps : pipe_stream) HIP_TRY(hipStreamCreateWithFlags(&ps, hipStreamNonBlocking));
+  for (int i = 0; i < pipe_slots; ++i)
+    HIP_TRY(hipStreamCreateWithFlags(&pipe_stream[i], hipStreamNonBlocking));
   return BFRS_OK;
 }
 
@@ -325,11 +328,11 @@ int Context::run_host(bool decode, size_t nblocks, const uint32_t *ks, size_t m,
   const size_t stride = round_up(slab + 64, 256);
   const size_t need = stride * (kmax + m);
   if (need > pipe_cap) {
-    for (auto &ps : pipe_stream) HIP_TRY(hipStreamSynchronize(ps));
+    for (int i = 0; i < pipe_slots; ++i) HIP_TRY(hipStreamSynchronize(pipe_stream[i]));
     if (pipe_buf) HIP_TRY(hipFree(pipe_buf));
     pipe_buf = nullptr;
     pipe_cap = 0;
-    HIP_TRY(hipMalloc(&pipe_buf, need * kPipeSlots));
+    HIP_TRY(hipMalloc(&pipe_buf, need * pipe_slots));
     pipe_cap = need;
   }
   int slot = 0;
@@ -373,11 +376,11 @@ int Context::run_host(bool decode, size_t nblocks, const uint32_t *ks, size_t m,
       if (rc) return rc;
       for (size_t t = 0; t < dout.size(); ++t)
         if (dout[t]) HIP_TRY(hipMemcpyAsync(bout[t] + off, dout[t], len, hipMemcpyDeviceToHost, st));
-      slot = (slot + 1) % kPipeSlots;
+      slot = (slot + 1) % pipe_slots;
       off += len;
     }
   }
-  for (auto &ps : pipe_stream) HIP_TRY(hipStreamSynchronize(ps));
+  for (int i = 0; i < pipe_slots; ++i) HIP_TRY(hipStreamSynchronize(pipe_stream[i]));
   return BFRS_OK;
 }
 

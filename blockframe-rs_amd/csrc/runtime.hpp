@@ -166,9 +166,12 @@ struct Context {
   // Host-path pipeline: slots of device slab buffers, one stream each.
   // pipe_mu serialises run_host: archive prefetch threads, repair and the
   // owner's host-batch calls may share one context.
-  static constexpr int kPipeSlots = 3;
+  // pipe_slots (default 5; BFRS_PIPE_SLOTS = 2..kPipeSlotsMax, A/B knob):
+  // 5-6 slots ran the pinned host batches ~1.5% faster than 3
+  static constexpr int kPipeSlotsMax = 6;
+  int pipe_slots = 5;
   std::mutex pipe_mu;
-  hipStream_t pipe_stream[kPipeSlots] = {};
+  hipStream_t pipe_stream[kPipeSlotsMax] = {};
   void *pipe_buf = nullptr;
   size_t pipe_cap = 0;  // bytes per slot
 
