@@ -1357,7 +1357,7 @@ def pcie_inclusive(ctx, sets, steps=2, rt=None, job_bytes=None):
         "encode_GiBps": round(gib / t_enc, 2), "decode_GiBps": round(gib / t_dec, 2),
         "encode_ms": round(t_enc * 1e3, 2), "decode_ms": round(t_dec * 1e3, 2),
         "h2d_bytes_encode": nseg * S, "d2h_bytes_encode": 3 * nb * S,
-        "note": "pinned host buffers; bfrs_*_host_batch (8 MiB column slabs over 3 HIP streams)",
+        "note": "pinned host buffers; bfrs_*_host_batch (8 MiB column slabs over 5 HIP streams)",
     }
 
 
