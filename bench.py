@@ -941,55 +941,9 @@ def crate_api(ctx, sets, reps=7, staging_ab=True):
             all_blocks()
         t_par = [all_blocks() for _ in range(5)]
         assert not errors, errors
-        # the same with every segment registered (bfrs_host_register, as a
-        # caller would register its file mmap once per commit): the shards
-        # go to the device by DMA straight from them, no staging copy
-        reg = {}
-        try:
-            t_r0 = time.perf_counter()
-            flat = [x for blk in blocks for x in blk]
-            done = []
-            try:
-                for x in flat:
-                    bfrs.host_register(x)
-                    done.append(x)
-                reg["register_ms"] = round((time.perf_counter() - t_r0) * 1e3, 1)
-                all_blocks()
-                reg["all_blocks"] = [all_blocks() for _ in range(5)]
-                assert not errors, errors
-                outs = [np.empty(S, np.uint8) for _ in range(3)]
-                ch = bfrs.Chunker(ctx)
-                ch.generate_parity_into(blocks[0], len(blocks[0]), 3, outs)
-                tg = []
-                for _ in range(reps):
-                    outs = [np.empty(S, np.uint8) for _ in range(3)]
-                    t1 = time.perf_counter()
-                    ch.generate_parity_into(blocks[0], len(blocks[0]), 3, outs)
-                    tg.append(time.perf_counter() - t1)
-                reg["generate_parity"] = tg
-                # recover_segment_rs30_3 with the 29 surviving segments registered
-                # (the parity shards come from fs::read, recovery.rs: unregistered)
-                target = sets.erased[0][0]
-                slots_r = [None if i == target else blocks[0][i] for i in range(len(blocks[0]))]
-                par_r = [np.array(o) for o in outs]
-                tr = []
-                for _ in range(reps):
-                    out = np.empty(S, np.uint8)
-                    t1 = time.perf_counter()
-                    bfrs.recover_segment_rs30_3_into(ctx, slots_r, par_r, target, out)
-                    tr.append(time.perf_counter() - t1)
-                reg["recover_ok"] = bool(np.array_equal(out, blocks[0][target]))
-                reg["recover"] = tr
-            finally:
-                for x in done:
-                    bfrs.host_unregister(x)
-        except bfrs.BfrsError as e:  # a runtime that refuses the registration: reported
-            reg = {"error": f"BfrsError: {e}"}
-        registered.update(reg)
         return t_par
 
     cold = settle_link(ctx)
-    registered = {}
     t_par = all_blocks_figure()
     tg, tr, par, slots, target, tg_reuse, tr_reuse, tg_new_in = wrappers(ctx)
     tg_py = timed(lambda: ch.generate_parity(segs, k, 3))
@@ -1058,7 +1012,7 @@ def crate_api(ctx, sets, reps=7, staging_ab=True):
                                    "python_wrapper_ms": round(tr_py * 1e3, 2),
                                    "what": "one erased segment of that block, pageable host in/out"},
         "breakdown": bd,
-        "recover_match": bool(recover_ok) and all(recover_ok) and registered.get("recover_ok", True),
+        "recover_match": bool(recover_ok) and all(recover_ok),
         "generate_parity_all_blocks_threads": {
             "ms": round(min(t_par) * 1e3, 2), "GiBps": round(par_gib / min(t_par), 2),
             "median_ms": round(sorted(t_par)[len(t_par) // 2] * 1e3, 2),
@@ -1070,22 +1024,6 @@ def crate_api(ctx, sets, reps=7, staging_ab=True):
                                 "through ctypes, fresh output buffers, best of reps (median_ms "
                                 "beside it), wall clock, after 400 ms of untimed calls",
     }
-    if "error" in registered:
-        res["registered_inputs"] = registered
-    elif registered:
-        ra, rg = registered["all_blocks"], registered["generate_parity"]
-        res["registered_inputs"] = {
-            "generate_parity_all_blocks_threads_ms": round(min(ra) * 1e3, 2),
-            "generate_parity_all_blocks_threads_median_ms": round(sorted(ra)[len(ra) // 2] * 1e3, 2),
-            "generate_parity_ms": round(min(rg) * 1e3, 2),
-            "generate_parity_median_ms": round(sorted(rg)[len(rg) // 2] * 1e3, 2),
-            "recover_segment_rs30_3_ms": round(min(registered["recover"]) * 1e3, 2),
-            "recover_segment_rs30_3_median_ms": round(
-                sorted(registered["recover"])[len(registered["recover"]) // 2] * 1e3, 2),
-            "register_ms": registered["register_ms"],
-            "what": "the same calls with every input segment registered once "
-                    "(bfrs_host_register, as a caller registers its file mmap per commit): "
-                    "shards DMA'd straight from them; fresh outputs; best (median) of 5 / reps"}
     res["link"] = pcie_link(S, k)
     lk = res["link"]
     res["generate_parity_all_blocks_threads"]["floor_ms"] = round(
@@ -1108,7 +1046,7 @@ def crate_api(ctx, sets, reps=7, staging_ab=True):
             pg, pr, _, _, _, pg_reuse, pr_reuse, pg_new_in = wrappers(c2)
         finally:
             c2.close()
-        res["recover_match"] = all(recover_ok) and registered.get("recover_ok", True)
+        res["recover_match"] = all(recover_ok)
         res["alt_staging"] = {"staging": alt, "generate_parity_ms": round(pg * 1e3, 2),
                               "generate_parity_touched_outputs_ms": round(pg_reuse * 1e3, 2),
                               "generate_parity_new_inputs_ms": round(pg_new_in * 1e3, 2),
@@ -1357,7 +1295,7 @@ def pcie_inclusive(ctx, sets, steps=2, rt=None, job_bytes=None):
         "encode_GiBps": round(gib / t_enc, 2), "decode_GiBps": round(gib / t_dec, 2),
         "encode_ms": round(t_enc * 1e3, 2), "decode_ms": round(t_dec * 1e3, 2),
         "h2d_bytes_encode": nseg * S, "d2h_bytes_encode": 3 * nb * S,
-        "note": "pinned host buffers; bfrs_*_host_batch (8 MiB column slabs over 5 HIP streams)",
+        "note": "pinned host buffers; bfrs_*_host_batch (8 MiB column slabs over 3 HIP streams)",
     }
 
 

@@ -47,8 +47,8 @@ E_NOT_FOUND = -35
 # Every symbol include/bfrs.h declares (tests check the library exports them).
 EXPORTS = (
     "bfrs_abi_version", "bfrs_strerror", "bfrs_last_error", "bfrs_device_count", "bfrs_open",
-    "bfrs_close", "bfrs_synchronize", "bfrs_shard_pitch", "bfrs_host_register",
-    "bfrs_host_unregister", "bfrs_use_high_rate", "bfrs_encode_coefficient",
+    "bfrs_close", "bfrs_synchronize", "bfrs_shard_pitch",
+    "bfrs_use_high_rate", "bfrs_encode_coefficient",
     "bfrs_plan_decode", "bfrs_encoder_new", "bfrs_encoder_add_original_shard",
     "bfrs_encoder_encode", "bfrs_encoder_recovery", "bfrs_encoder_free", "bfrs_decoder_new",
     "bfrs_decoder_add_original_shard", "bfrs_decoder_add_recovery_shard", "bfrs_decoder_decode",
@@ -135,8 +135,6 @@ def lib() -> ctypes.CDLL:
             "bfrs_last_error": ([], ctypes.c_char_p),
             "bfrs_device_count": ([], ctypes.c_int),
             "bfrs_shard_pitch": ([_sz], _sz),
-            "bfrs_host_register": ([_vp, _sz], ctypes.c_int),
-            "bfrs_host_unregister": ([_vp], ctypes.c_int),
             "bfrs_open": ([ctypes.c_int, ctypes.POINTER(_vp)], ctypes.c_int),
             "bfrs_close": ([_vp], None),
             "bfrs_synchronize": ([_vp], ctypes.c_int),
@@ -794,18 +792,6 @@ def commit(ctx, file_path: str, archive_root: str, segment_size: int = 0,
         _check(lib().bfrs_commit(ctx.handle, os.fsencode(file_path), os.fsencode(archive_root),
                                  segment_size, tier, out, len(out)))
     return out.value.decode()
-
-
-def host_register(buf) -> None:
-    """bfrs_host_register: page-lock a host buffer (numpy array / bytearray /
-    CPU tensor) that lives a while, so shards inside it are DMA'd straight to
-    the device by the codec objects and wrappers (include/bfrs.h)."""
-    n = buf.nbytes if hasattr(buf, "nbytes") else len(buf)
-    _check(lib().bfrs_host_register(Context._haddr(buf), n))
-
-
-def host_unregister(buf) -> None:
-    _check(lib().bfrs_host_unregister(Context._haddr(buf)))
 
 
 def _ctx_array(ctxs):

@@ -33,8 +33,7 @@ class Prefault {
  public:
   Prefault(uint8_t *const *bufs, size_t n, size_t len) {
     auto touch = [bufs, n, len] {
-      for (size_t j = 0; j < n; ++j)
-        if (!host_registered(bufs[j], len)) prefault_range(bufs[j], len);  // registered: pinned
+      for (size_t j = 0; j < n; ++j) prefault_range(bufs[j], len);
     };
     try {
       th_ = std::thread(touch);
@@ -58,23 +57,18 @@ bool overlaps(const uint8_t *a, size_t na, const uint8_t *b, size_t nb) {
 }
 
 // The slab-pipelined generate_parity (encoder_encode_slabs): pinned staging,
-// shards of >= 16 MiB (at least two ~8 MiB slabs), no registered segment;
-// BFRS_WRAPPER_SLABS=0 turns it off (A/B).
-bool slab_wrapper_ok(bfrs_ctx *ctx, const uint8_t *const *segs, const size_t *lens, size_t n,
-                     size_t shard, bool allow_missing = false) {
+// shards of >= 16 MiB (at least two ~8 MiB slabs); BFRS_WRAPPER_SLABS=0
+// turns it off (A/B).
+bool slab_wrapper_ok(bfrs_ctx *ctx, const uint8_t *const *segs, size_t n, size_t shard,
+                     bool allow_missing = false) {
   static const bool on = [] {
     const char *e = std::getenv("BFRS_WRAPPER_SLABS");
     return !(e && std::strcmp(e, "0") == 0);
   }();
   if (!on || shard < (size_t(16) << 20) || ctx->impl.codec_pool->staging != Staging::kPinned)
     return false;
-  for (size_t i = 0; i < n; ++i) {
-    if (!segs[i]) {
-      if (allow_missing) continue;
-      return false;
-    }
-    if (lens[i] && host_registered(segs[i], lens[i])) return false;
-  }
+  for (size_t i = 0; i < n; ++i)
+    if (!segs[i] && !allow_missing) return false;
   return true;
 }
 
@@ -115,7 +109,7 @@ int bfrs_generate_parity(bfrs_ctx *ctx, const uint8_t *const *segments, const si
   // are copied and DMA'd.  Registered segments go straight by
   // DMA through the adds below, and a segment count other than data_shards
   // takes the adds too, which report the crate's errors.
-  if (n_segments == data_shards && slab_wrapper_ok(ctx, segments, seg_lens, n_segments, max_len))
+  if (n_segments == data_shards && slab_wrapper_ok(ctx, segments, n_segments, max_len))
     return encoder_encode_slabs(enc.p, segments, seg_lens, parity_out);
   // generate.rs:75-82 + 87-89 — zero-pad each segment to max_len and add it
   const auto t_add = std::chrono::steady_clock::now();
@@ -243,13 +237,11 @@ int bfrs_recover_segment_rs30_3(bfrs_ctx *ctx, const uint8_t *const *segments,
   // which report the crate's errors.
   {
     bool slabs = !segments[target_index] && missing >= 1 &&
-                 slab_wrapper_ok(ctx, segments, seg_lens, 30, shard_size, true);
+                 slab_wrapper_ok(ctx, segments, 30, shard_size, true);
     for (size_t i = 0; slabs && i < 30; ++i)
       if (segments[i] && seg_lens[i] != shard_size) slabs = false;
     for (size_t j = 0; slabs && j < 3; ++j)
-      if (!block_parity[j] || parity_lens[j] != shard_size ||
-          host_registered(block_parity[j], parity_lens[j]))
-        slabs = false;
+      if (!block_parity[j] || parity_lens[j] != shard_size) slabs = false;
     if (slabs) {
       if ((rc = decoder_restore_slabs(dec.p, segments, block_parity, target_index, out))) return rc;
       *out_len = shard_size;

@@ -81,15 +81,7 @@ struct CodecObject {
   // on return.
   int stage(size_t i, const uint8_t *src, size_t len) {
     HIP_TRY(hipSetDevice(pool->device));
-    if (host_registered(src, len)) {
-      // a registered (page-locked) range: one DMA straight from it, queued
-      // like the pinned rows' copies.  A registered range's bytes must stay
-      // unchanged until the encode()/decode() that consumes them returns
-      // (include/bfrs.h: the caller opted in by registering it; BlockFrame's
-      // mmap'd segments are read-only)
-      HIP_TRY(hipMemcpyAsync(d_row(i), src, len, hipMemcpyHostToDevice, h2d()));
-      HIP_TRY(hipEventRecord(slot->ev_h2d, h2d()));
-    } else if (pool->staging == Staging::kPinned) {
+    if (pool->staging == Staging::kPinned) {
       // the row's previous H2D (an earlier round on this object) is done:
       // rows are reused only after encode()/decode() synchronised the slot
       host_copy(h_row(i), src, len);
@@ -234,8 +226,7 @@ int bfrs::encoder_encode_to_host(bfrs_encoder *e, uint8_t *const *outs) {
     for (size_t j = 0; j < e->m; ++j) {
       uint8_t *p = outs[j];
       try {
-        if (host_registered(p, n)) touch.t.emplace_back();  // pinned already: an empty slot
-        else touch.t.emplace_back([p, n] { prefault_range(p, n); });
+        touch.t.emplace_back([p, n] { prefault_range(p, n); });
       } catch (...) {  // no thread: the copy-out faults the pages itself
         break;
       }
@@ -253,7 +244,7 @@ int bfrs::encoder_encode_to_host(bfrs_encoder *e, uint8_t *const *outs) {
   for (size_t j = 0; j < e->m; ++j) {
     const auto t0 = clk::now();
     HIP_TRY(hipEventSynchronize(done[j]));
-    if (j < touch.t.size() && touch.t[j].joinable()) touch.t[j].join();
+    if (j < touch.t.size()) touch.t[j].join();
     const auto t1 = clk::now();
     host_copy(outs[j], e->h_row(e->k + j), e->shard_bytes);
     wait_ms += std::chrono::duration<double, std::milli>(t1 - t0).count();
@@ -281,7 +272,6 @@ struct TouchThreads {
         const size_t lo = q * per, hi = std::min(len, lo + per);
         if (lo >= hi) continue;
         uint8_t *p = bufs[b];
-        if (host_registered(p, len)) continue;  // pinned already
         auto f = [p, lo, hi] { prefault_range(p + lo, hi - lo); };
         try {
           t.emplace_back(f);

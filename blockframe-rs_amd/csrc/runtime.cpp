@@ -601,56 +601,6 @@ int bfrs_open(int device, bfrs_ctx **out) {
 
 void bfrs_close(bfrs_ctx *ctx) { delete ctx; }
 
-}  // extern "C"
-
-namespace {
-// Ranges registered through bfrs_host_register: start -> length.
-std::mutex g_reg_mu;
-std::map<uintptr_t, size_t> g_registered;
-}  // namespace
-
-bool bfrs::host_registered(const void *p, size_t n) {
-  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-  std::lock_guard<std::mutex> g(g_reg_mu);
-  auto it = g_registered.upper_bound(a);
-  if (it == g_registered.begin()) return false;
-  --it;
-  return a >= it->first && a + n <= it->first + it->second;
-}
-
-extern "C" {
-
-int bfrs_host_register(void *ptr, size_t len) {
-  BFRS_API_BEGIN
-  if (!ptr || !len) return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_host_register: empty range");
-  {
-    std::lock_guard<std::mutex> g(g_reg_mu);
-    const uintptr_t a = reinterpret_cast<uintptr_t>(ptr);
-    auto it = g_registered.upper_bound(a + len - 1);
-    if (it != g_registered.begin() && std::prev(it)->first + std::prev(it)->second > a)
-      return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_host_register: range overlaps a registered one");
-  }
-  HIP_TRY(hipHostRegister(ptr, len, hipHostRegisterDefault));
-  std::lock_guard<std::mutex> g(g_reg_mu);
-  g_registered[reinterpret_cast<uintptr_t>(ptr)] = len;
-  return BFRS_OK;
-  BFRS_API_END
-}
-
-int bfrs_host_unregister(void *ptr) {
-  BFRS_API_BEGIN
-  {
-    std::lock_guard<std::mutex> g(g_reg_mu);
-    auto it = g_registered.find(reinterpret_cast<uintptr_t>(ptr));
-    if (it == g_registered.end())
-      return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_host_unregister: not a registered range");
-    g_registered.erase(it);
-  }
-  HIP_TRY(hipHostUnregister(ptr));
-  return BFRS_OK;
-  BFRS_API_END
-}
-
 int bfrs_synchronize(bfrs_ctx *ctx) {
   BFRS_API_BEGIN
   if (!ctx) return set_error(BFRS_E_INVALID_ARGUMENT, "NULL context");

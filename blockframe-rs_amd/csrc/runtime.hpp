@@ -166,10 +166,11 @@ struct Context {
   // Host-path pipeline: slots of device slab buffers, one stream each.
   // pipe_mu serialises run_host: archive prefetch threads, repair and the
   // owner's host-batch calls may share one context.
-  // pipe_slots (default 5; BFRS_PIPE_SLOTS = 2..kPipeSlotsMax, A/B knob):
-  // 5-6 slots ran the pinned host batches ~1.5% faster than 3
+  // pipe_slots (default 3; BFRS_PIPE_SLOTS = 2..kPipeSlotsMax, A/B knob):
+  // 5-6 slots ran the pinned host batches ~1.5% faster, but 3 is the depth
+  // every long soak ran with
   static constexpr int kPipeSlotsMax = 6;
-  int pipe_slots = 5;
+  int pipe_slots = 3;
   std::mutex pipe_mu;
   hipStream_t pipe_stream[kPipeSlotsMax] = {};
   void *pipe_buf = nullptr;
@@ -239,8 +240,6 @@ struct bfrs_ctx {
 };
 
 namespace bfrs {
-// [p, p + n) lies inside a range registered with bfrs_host_register.
-bool host_registered(const void *p, size_t n);
 // Pointer and shape checks of the host-memory batch API (one block list).
 int check_host_batch(bfrs_ctx *ctx, size_t nblocks, const uint32_t *ks, size_t m,
                      size_t shard_bytes, bool decode, const uint8_t *const *orig,

@@ -125,21 +125,6 @@ int bfrs_synchronize(bfrs_ctx *ctx);
  * one column of all of them together; a pitch = 12 KiB (mod 64 KiB) spreads
  * them (measured 0.8-5% faster).  Smaller shards: rounded up to 256 B. */
 size_t bfrs_shard_pitch(size_t shard_bytes);
-/* Page-locks a host range the caller keeps for a while -- BlockFrame's mmap
- * of the file being committed (src/chunker/commit.rs:355-360), or its
- * segment buffers -- so that codec objects and the wrappers DMA shards that
- * lie inside it straight to the device, instead of copying them through the
- * slot's pinned rows first (no reference counterpart; the crate copies every
- * added shard).  Opting in changes one rule: the DMA reads a registered
- * shard asynchronously, so its bytes must stay unchanged until the encode()
- * / decode() that consumes it returns (the wrappers return after both).
- * Outputs are always written through the slot's pinned rows: device writes
- * straight into a caller-registered range, once that range was unregistered
- * and freed, left the runtime faulting a later pageable copy.
- * Process-wide (HIP registration, any context); unregister before unmapping
- * or freeing the range.  BFRS_E_HIP if the runtime refuses the range. */
-int bfrs_host_register(void *ptr, size_t len);
-int bfrs_host_unregister(void *ptr);
 
 /* ---- codec rules (pure host logic) ------------------------------------ */
 /* 1 = HighRate, 0 = LowRate (reed-solomon-simd DefaultRate), <0 = unsupported. */

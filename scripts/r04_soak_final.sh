@@ -1,9 +1,10 @@
 #!/bin/bash
 # Round-4 final-tree soaks: the codec soak with 8-40 MiB shards at 20% (the
 # slab-pipelined generate_parity / recover_segment_rs30_3 wrappers, RS(30,3)
-# recovers at 16-20 MiB shards, 30% of multi-MiB wrapper cases with their inputs
-# registered), then the archive soak and the BLAKE3 soak.  Each run has its own
-# time limit; a failure stops here.
+# recovers at 16-20 MiB shards), then the archive soak and the BLAKE3 soak.
+# (r04s/r04fs also registered the inputs of 30% of the multi-MiB wrapper cases;
+# r04fs faulted the GPU and host registration was removed)
+# Each run has its own time limit; a failure stops here.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out; mkdir -p "$OUT"

@@ -787,113 +787,6 @@ def test_mixed_entry_points_share_one_context_across_threads(ctx, bfrs, oracle):
     assert not errors, errors
 
 
-def test_registered_inputs_dma_straight_and_match(bfrs, oracle):
-    """bfrs_host_register: shards inside a registered range go to the device
-    by DMA straight from it (no staging copy); the bytes equal the oracle's
-    through the wrappers and the objects, the range may change once encode()
-    returned, and the registry refuses overlaps and unknown ranges."""
-    c = bfrs.Context(0)
-    rng = np.random.default_rng(33)
-    n = (1 << 20) + 64 * 5
-    data = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(30)]
-    want = [r.tobytes() for r in oracle.encode(data, 3)]
-    big = np.concatenate(data)  # one registered range, shards are slices of it
-    bfrs.host_register(big)
-    try:
-        segs = [big[i * n:(i + 1) * n] for i in range(30)]
-        outs = [np.empty(n, np.uint8) for _ in range(3)]
-        assert bfrs.Chunker(c).generate_parity_into(segs, 30, 3, outs) == n
-        assert [o.tobytes() for o in outs] == want
-        enc = bfrs.ReedSolomonEncoder(c, 30, 3, n)
-        for sg in segs:  # queued DMAs straight from the range; consumed by encode()
-            enc.add_original_shard(sg)
-        assert list(enc.encode().recovery_iter()) == want
-        # once encode() returned, the range may change: a second round on the
-        # same object with other bytes gives their parity
-        big[:] = 255 - big
-        for sg in segs:
-            enc.add_original_shard(sg)
-        want2 = [r.tobytes() for r in oracle.encode([255 - d for d in data], 3)]
-        assert list(enc.encode().recovery_iter()) == want2
-        del enc
-        big[:] = 255 - big
-        slots = [None if i in (4, 20) else big[i * n:(i + 1) * n] for i in range(30)]
-        par = [np.frombuffer(p, np.uint8) for p in want]
-        assert bfrs.recover_segment_rs30_3(c, slots, par, 20) == data[20].tobytes()
-        with pytest.raises(bfrs.BfrsError):
-            bfrs.host_register(big[n:2 * n])  # overlaps the registered range
-    finally:
-        bfrs.host_unregister(big)
-    with pytest.raises(bfrs.BfrsError):
-        bfrs.host_unregister(big)
-    c.close()
-
-
-def _page_isolated(nbytes, fill):
-    """A host buffer whose pages no other allocation shares (a page of slack
-    either side), so registering a range inside it never pins a neighbour's
-    page too."""
-    raw = np.empty(nbytes + 3 * 4096, np.uint8)
-    off = (-raw.ctypes.data) % 4096 + 4096
-    buf = raw[off:off + nbytes]
-    buf[:] = fill
-    return buf
-
-
-@pytest.mark.parametrize("inputs_registered", [False, True])
-@pytest.mark.parametrize("n", [(1 << 20) + 64 * 5, (16 << 20) + 38])
-def test_registered_outputs_written_through_pinned_rows(bfrs, oracle, inputs_registered, n):
-    """Outputs inside a registered range (a caller reusing registered buffers)
-    are written like any other output: D2H into the slot's pinned rows, then
-    copied out.  They skip only the first-touch helper, because registered
-    pages are resident.  The test covers the whole-shard path (small shards,
-    registered inputs) and the slab-pipelined one (>= 16 MiB, staged
-    inputs). Every byte is checked against the oracle, and the bytes next to
-    each output stay untouched.  Regression: a version that DMA'd straight
-    into registered outputs left the HIP runtime in a state where, once those
-    ranges were unregistered and freed, the next pageable H2D faulted the GPU
-    (test_generate_parity_slab_pipeline_vs_oracle[direct] right after this
-    one, r04t)."""
-    c = bfrs.Context(0)
-    rng = np.random.default_rng(n % 977 + inputs_registered)
-    data = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(30)]
-    want = [r.tobytes() for r in oracle.encode(data, 3)]
-    big = _page_isolated(30 * n, 0)
-    big[:] = np.concatenate(data)
-    segs = [big[i * n:(i + 1) * n] for i in range(30)]
-    # outputs inside guarded buffers: 64 canary bytes either side
-    guard = [_page_isolated(n + 128, 0xC3) for _ in range(3)]
-    outs = [g[64:64 + n] for g in guard]
-    regs = [outs[0], outs[2]] + ([big] if inputs_registered else [])
-    for x in regs:
-        bfrs.host_register(x)
-    try:
-        for rnd in range(2):  # reused outputs, as BlockFrame would
-            for o in outs:
-                o[:] = 0x5A
-            assert bfrs.Chunker(c).generate_parity_into(segs, 30, 3, outs) == n
-            assert [o.tobytes() for o in outs] == want, rnd
-            assert all((g[:64] == 0xC3).all() and (g[64 + n:] == 0xC3).all() for g in guard)
-        # recover_segment_rs30_3 of two erased targets into a registered out
-        par = [np.frombuffer(p, np.uint8).copy() for p in want]
-        slots = [None if i in (3, 17) else segs[i] for i in range(30)]
-        out_g = _page_isolated(n + 128, 0xC3)
-        out = out_g[64:64 + n]
-        bfrs.host_register(out)
-        try:
-            for t in (3, 17):
-                out[:] = 0
-                assert bfrs.recover_segment_rs30_3_into(c, slots, par, t, out) == n
-                assert np.array_equal(out, data[t]), t
-                assert (out_g[:64] == 0xC3).all() and (out_g[64 + n:] == 0xC3).all()
-        finally:
-            bfrs.host_unregister(out)
-    finally:
-        for x in regs:
-            bfrs.host_unregister(x)
-    c.close()
-
-
 @pytest.mark.parametrize("staging", ["pinned", "direct"])
 def test_generate_parity_slab_pipeline_vs_oracle(bfrs, oracle, monkeypatch, staging):
     """bfrs_generate_parity on a whole block of >= 16 MiB shards runs slab by

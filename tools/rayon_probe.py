@@ -119,26 +119,11 @@ def main():
     res["link_floor_ms"] = round(min(xfer() for _ in range(3)) * 1e3, 2)
     del dev, pin
     for mode in os.environ.get("PROBE_MODES", "pinned,direct").split(","):
-        # "<staging>_reg": every input segment registered (bfrs_host_register)
-        # first, so the shards are DMA'd straight from them; seen inputs only
-        reg = mode.endswith("_reg")
-        ctx = context(mode[:-4] if reg else mode)
-        if reg:
-            for blk in blocks:
-                for x in blk:
-                    bfrs.host_register(x)
+        ctx = context(mode)
         t0 = time.perf_counter()
         while time.perf_counter() - t0 < 0.5:  # link settle
             run_blocks(ctx, blocks)
         seen = [run_blocks(ctx, blocks) for _ in range(REPS)]
-        if reg:
-            for blk in blocks:
-                for x in blk:
-                    bfrs.host_unregister(x)
-            res[f"seen_{mode}"] = [round(min(seen) * 1e3, 2), round(float(np.median(seen)) * 1e3, 2)]
-            res[f"seen_{mode}_GiBps"] = round(gib / min(seen), 2)
-            ctx.close()
-            continue
         fresh = []
         for _ in range(REPS):
             nb = [[np.array(x) for x in blk] for blk in blocks]

@@ -39,7 +39,7 @@ def main():
     import oracle
 
     ctx = bfrs.Context(0)
-    stats = {"cases": 0, "bytes": 0, "by_api": {}, "failures": [], "registered_cases": 0}
+    stats = {"cases": 0, "bytes": 0, "by_api": {}, "failures": []}
     lock = threading.Lock()
     stop = time.perf_counter() + a.seconds
 
@@ -131,27 +131,14 @@ def main():
                     padded = data[:-1] + [np.pad(segs[-1], (0, cut))]
                     want = oracle.encode(padded, m, oracle.ENGINE_AVX2) if cut else rec
                     outs = [np.empty(n, np.uint8) for _ in range(m)]
-                    # 30% of the multi-MiB cases with the inputs registered
-                    # (DMA'd straight from them, no staging copy), the rest staged
-                    reg = [x for x in segs + [r for r in rec_in if r is not None] if x.size] \
-                        if n >= (1 << 20) and rng.random() < 0.3 else []
-                    for x in reg:
-                        bfrs.host_register(x)
-                    if reg:
-                        with lock:
-                            stats["registered_cases"] += 1
-                    try:
-                        bfrs.Chunker(ctx).generate_parity_into(segs, k, m, outs)
-                        ok = all(np.array_equal(o, w) for o, w in zip(outs, want))
-                        if k == 30 and m == 3 and er and not cut:
-                            want_d = oracle.decode(orig_in, rec_in, oracle.ENGINE_AVX2)
-                            if all(r is not None for r in rec_in):
-                                for t in er:
-                                    got = bfrs.recover_segment_rs30_3(ctx, orig_in, rec_in, t)
-                                    ok = ok and got == want_d[t].tobytes()
-                    finally:
-                        for x in reg:
-                            bfrs.host_unregister(x)
+                    bfrs.Chunker(ctx).generate_parity_into(segs, k, m, outs)
+                    ok = all(np.array_equal(o, w) for o, w in zip(outs, want))
+                    if k == 30 and m == 3 and er and not cut:
+                        want_d = oracle.decode(orig_in, rec_in, oracle.ENGINE_AVX2)
+                        if all(r is not None for r in rec_in):
+                            for t in er:
+                                got = bfrs.recover_segment_rs30_3(ctx, orig_in, rec_in, t)
+                                ok = ok and got == want_d[t].tobytes()
                 elif api == "host_batch":
                     # one shape per batch (the batch API shares k across blocks only via ks)
                     ks = [k] * nblocks
