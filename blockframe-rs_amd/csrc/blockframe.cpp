@@ -106,9 +106,8 @@ int bfrs_generate_parity(bfrs_ctx *ctx, const uint8_t *const *segments, const si
     if (!parity_out[j]) return set_error(BFRS_E_INVALID_ARGUMENT, "parity buffer is NULL");
   // A whole block of pageable segments (BlockFrame's case): slab-pipelined,
   // so each column slab's kernel and D2H run while the next slab's segments
-  // are copied and DMA'd.  Registered segments go straight by
-  // DMA through the adds below, and a segment count other than data_shards
-  // takes the adds too, which report the crate's errors.
+  // are copied and DMA'd.  A segment count other than
+  // data_shards takes the adds below, which report the crate's errors.
   if (n_segments == data_shards && slab_wrapper_ok(ctx, segments, n_segments, max_len))
     return encoder_encode_slabs(enc.p, segments, seg_lens, parity_out);
   // generate.rs:75-82 + 87-89 — zero-pad each segment to max_len and add it
