@@ -15,6 +15,7 @@ case $MODE in
   populate) VAR=BFRS_PREFAULT_POPULATE; VALS="1 0 1 0";;
   early) VAR=BFRS_PREFAULT_EARLY; VALS="1 0 1 0";;
   parts) VAR=BFRS_PREFAULT_PARTS; VALS="4 1 4 1";;  # threads per output (r04v: encode 1 -> 4)
+  huge) VAR=BFRS_PREFAULT_HUGE; VALS="1 0 1 0";;  # MADV_HUGEPAGE first (r04h2; knob removed)
 esac
 for v in $VALS; do
   env $VAR=$v timeout -k 10 300 python bench.py $ARGS > "$OUT/pf_${TAG}_${MODE}$v.json" 2> "$OUT/pf_${TAG}_${MODE}$v.err"
