@@ -117,6 +117,23 @@ def parse(argv=None):
 T_START = time.perf_counter()
 
 
+# The JSON line's channel.  Run as a script, stdout carries nothing else
+# (claim_stdout): C++ code in the process (gloo prints its "[Gloo] Rank ...
+# connected" lines to fd 1, RCCL its debug output) writes to stderr instead.
+JSON_OUT = None
+
+
+def claim_stdout():
+    global JSON_OUT
+    sys.stdout.flush()
+    JSON_OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+
+
+def emit(obj):
+    print(json.dumps(obj), file=JSON_OUT or sys.stdout, flush=True)
+
+
 def progress(msg):
     """One stderr line per bench phase (a long run shows it is alive)."""
     print(f"bench.py [{time.perf_counter() - T_START:7.1f} s] {msg}", file=sys.stderr, flush=True)
@@ -148,7 +165,8 @@ def launch_ranks(args, argv=None) -> int:
     for r in range(args.gpus):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
                    LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
+                                      stdout=JSON_OUT))  # rank 0's line on this stdout
     by_pid = {p.pid: (r, p) for r, p in enumerate(procs)}
     failed = None
     while by_pid and failed is None:
@@ -1538,8 +1556,7 @@ def trace_probe(args):
         enc(sh)
         dec(sh)
     _, elapsed, launch_ms = device_loop(rt, step, stream, args)
-    print(json.dumps({"launch_ms": launch_ms, "steps": args.steps,
-                      "ms_per_step": elapsed / args.steps * 1e3}), flush=True)
+    emit({"launch_ms": launch_ms, "steps": args.steps, "ms_per_step": elapsed / args.steps * 1e3})
     return 0
 
 
@@ -1839,7 +1856,7 @@ def main(argv=None):
         line = run_c5(args)
         line.update({"n_gpus": 1, "higher_is_better": True, "vs_baseline": None, "dtype": "u8",
                      "data": "synthetic splitmix64 bytes; files in the page cache"})
-        print(json.dumps(line), flush=True)
+        emit(line)
         return 0 if line["blake3_match"] else 1
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return launch_ranks(args, argv)
@@ -2106,7 +2123,7 @@ def main(argv=None):
         "when": "after the timed region, on the buffers the timed launches wrote"})
     if legs.aborted:
         line["parity_check"]["aborted"] = legs.aborted
-    print(json.dumps(line), flush=True)
+    emit(line)
     rt.close()
     return 0 if line["parity_check"]["all_ok"] else 1
 
@@ -2119,4 +2136,5 @@ def sets_pitch(S, args, rt):
 
 
 if __name__ == "__main__":
+    claim_stdout()
     sys.exit(main())
