@@ -1976,8 +1976,13 @@ def main(argv=None):
         pcie = legs.run("pcie_inclusive", pcie_inclusive, ctx, sets)
     if solo_legs and args.crate == "auto":
         host_pinned = pinned_host_state(rt)
-        if os.environ.get("BENCH_HOST_EMPTY_CACHE") == "1" and not rt.stub:
-            rt.torch._C._host_emptyCache()  # A/B: give torch's cached pinned blocks back first
+        if os.environ.get("BENCH_HOST_EMPTY_CACHE", "1") == "1" and not rt.stub:
+            # The earlier legs leave ~27 GB of pinned blocks in torch's caching
+            # host allocator.  Held, they slowed the five concurrent blocks by
+            # ~20% (r04ec: 85.4/87.4 ms emptied against 104.8/102.0 ms held, one
+            # box, alternating).  A BlockFrame process holds no
+            # such memory, so give it back first (BENCH_HOST_EMPTY_CACHE=0: keep it)
+            rt.torch._C._host_emptyCache()
             host_pinned["after_empty_cache"] = pinned_host_state(rt)
         load_before = host_pressure()
         crate = legs.run("crate_api", crate_api, ctx, sets)
