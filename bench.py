@@ -32,8 +32,17 @@ Sub-objects of the same JSON line:
   pcie_inclusive  the same batch from pinned host memory (H2D + kernel + D2H)
   c5           BASELINE configs[4]: read of a corrupted 4 GiB tier-3 archive
                through the mount's read core (bfrs_archive_read)
+
+Process layout (round 5): run as a script, bench.py is a
+GPU-free supervisor that starts the measurement as a child process (no
+re-exec) and prints the line.  The child writes the line-so-far to the
+supervisor's state file after the timed region and before and after every
+leg, so a signal anywhere after the timed region still yields the headline,
+with `parity_check.aborted` naming the leg and the signal, all_ok false and a
+non-zero exit.  faulthandler is on in both processes.
 """
 import argparse
+import faulthandler
 import json
 import os
 import socket
@@ -103,7 +112,13 @@ def parse(argv=None):
     ap.add_argument("--stub", action="store_true",
                     help="CPU-only rehearsal of the launcher/partition/timing path: no GPU, "
                          "the codec calls replaced by a stand-in (tests only, never a bench line)")
+    ap.add_argument("--no-supervisor", action="store_true",
+                    help="run the measurement in this process (no GPU-free parent)")
+    ap.add_argument("--stub-crash-leg", default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--stub-legs-builtin", action="store_true", help=argparse.SUPPRESS)
     a = ap.parse_args(argv)
+    if a.stub_legs_builtin:  # a subprocess test: bench.py's own stand-ins run the legs
+        a.stub = a.stub_legs = True
     if a.strong and a.segments == 128:
         a.segments = 320
     if a.stub:
@@ -131,12 +146,156 @@ def claim_stdout():
 
 
 def emit(obj):
+    """The line: printed on the JSON channel, or, in the supervisor's
+    measurement child, written as the final state for the supervisor to print."""
+    if STATE.path:
+        STATE.line = obj
+        STATE.save(final=True)
+        return
     print(json.dumps(obj), file=JSON_OUT or sys.stdout, flush=True)
 
 
 def progress(msg):
     """One stderr line per bench phase (a long run shows it is alive)."""
     print(f"bench.py [{time.perf_counter() - T_START:7.1f} s] {msg}", file=sys.stderr, flush=True)
+
+
+# ---------------------------------------------------------------- supervisor
+STATE_ENV = "BENCH_STATE_FILE"  # set by the supervisor in its measurement child
+
+
+class LineState:
+    """The line under construction in the measurement child (rank 0).  save()
+    replaces the supervisor's state file atomically with the line so far, the
+    leg running now (and the line key its result goes to) and whether the
+    line is final."""
+
+    def __init__(self, path):
+        self.path = path
+        self.line = None
+
+    def save(self, running=None, key=None, final=False):
+        if not self.path or self.line is None:
+            return
+        tmp = self.path + ".tmp"
+        with open(tmp, "w") as f:
+            json.dump({"line": self.line, "running": running, "running_key": key,
+                       "final": final}, f)
+        os.replace(tmp, self.path)
+
+
+STATE = LineState(os.environ.get(STATE_ENV))
+
+
+def wants_supervisor(args) -> bool:
+    """Run as a script, the measurement goes to a child of a GPU-free parent,
+    except: in the child itself, in the probe children, with --no-supervisor,
+    under rocprofv3 (its preloaded library has already initialised the GPU
+    in this process, so this process must not start another program: the
+    profiled process itself is the measurement) and in the spawn launcher
+    (each rank process it starts supervises its own child)."""
+    if STATE.path or args.no_supervisor or args.traffic_probe or args.trace_probe:
+        return False
+    if under_rocprof():
+        return False
+    return not (args.gpus > 1 and "WORLD_SIZE" not in os.environ)
+
+
+def probe_env(**extra) -> dict:
+    """Environment of a probe child (PMC and trace passes, the rayon probe):
+    this process's, without the supervisor's state file (a probe's line must
+    never land in it; round 5's first box run lost both live passes that
+    way: the probes took the child's exit path, which skips rocprofv3's
+    output at exit) and without torchrun's job id (a probe never joins a
+    process group)."""
+    env = dict(os.environ, **extra)
+    env.pop(STATE_ENV, None)
+    env.pop("TORCHELASTIC_RUN_ID", None)
+    return env
+
+
+def exit_status(rc: int) -> str:
+    """A child's return code as a shell reports it: `SIGSEGV` or `exit 3`."""
+    import signal
+    if rc < 0:
+        try:
+            return signal.Signals(-rc).name
+        except ValueError:
+            return f"signal {-rc}"
+    return f"exit {rc}"
+
+
+def shell_rc(rc: int) -> int:
+    return rc if rc >= 0 else 128 - rc  # a signal (-N) becomes 128 + N
+
+
+def supervise(argv) -> int:
+    """The GPU-free parent: start the measurement child (`-X faulthandler`,
+    same argv and environment, plus the state file's path), forward
+    SIGTERM / SIGINT / SIGHUP to it, wait, and print its line."""
+    import signal
+    import tempfile
+    fd, path = tempfile.mkstemp(prefix="bench_state_", suffix=".json")
+    os.close(fd)
+    os.unlink(path)  # the child creates it at its first checkpoint
+    env = dict(os.environ, **{STATE_ENV: path})
+    child = subprocess.Popen([sys.executable, "-X", "faulthandler", os.path.abspath(__file__)]
+                             + list(argv), env=env)
+
+    def forward(sig, _frame):
+        try:
+            child.send_signal(sig)
+        except OSError:
+            pass
+    for sig in (signal.SIGTERM, signal.SIGINT, signal.SIGHUP):
+        signal.signal(sig, forward)
+    rc = child.wait()
+    st = None
+    try:
+        with open(path) as f:
+            st = json.load(f)
+    except (OSError, ValueError):
+        pass
+    finally:
+        for p in (path, path + ".tmp"):
+            try:
+                os.unlink(p)
+            except OSError:
+                pass
+    return finish_supervised(st, rc)
+
+
+def finish_supervised(st, rc: int) -> int:
+    """Print the child's line and return the bench's exit code.  A final line
+    is printed as the child wrote it, with the child's code.  Otherwise the
+    last checkpoint is printed with parity_check.aborted = "<leg>: <signal>"
+    (or the exit code), all_ok false, the running leg's entry replaced by an
+    error, and the exit code is non-zero.  Without any checkpoint (the child
+    died before its timed region ended) there is no line."""
+    if st is None or not st.get("line"):
+        if rc != 0:
+            progress(f"measurement child ended with {exit_status(rc)} before the timed region "
+                     "was complete: no line")
+        return shell_rc(rc)
+    line = st["line"]
+    if st.get("final"):
+        if rc != 0 and rc != 1:  # died after writing a complete line (teardown)
+            line.setdefault("parity_check", {})["aborted"] = f"after the line: {exit_status(rc)}"
+            line["parity_check"]["all_ok"] = False
+        emit(line)
+        return shell_rc(rc)
+    why = exit_status(rc) if rc != 0 else "exit 0 without a final line"
+    leg = st.get("running")
+    pc = line.setdefault("parity_check", {})
+    pc["aborted"] = f"{leg or 'between legs'}: {why}"
+    pc["all_ok"] = False
+    if leg:
+        pc.setdefault("failed", []).append(f"leg {leg}")
+        if st.get("running_key"):
+            line[st["running_key"]] = {"error": f"measurement child died in this leg: {why}"}
+    progress(f"measurement child ended with {why} in leg {leg}: printing the line so far")
+    emit(line)
+    return shell_rc(rc) if rc != 0 else 1
 
 
 # ---------------------------------------------------------------- launcher
@@ -891,11 +1050,6 @@ def crate_api(ctx, sets, reps=7, staging_ab=True):
         # the first second or so of crate_api saw sporadic 2x slower H2D/D2H
         # waits in every bench run (BFRS_TRACE: waits of 28-34 ms instead of
         # 2-7 ms), whichever figure was timed first
-        late = os.environ.get("BENCH_CRATE_ORDER", "late") == "late"
-        if not late:
-            tg = timed(lambda: chk.generate_parity_into(segs, k, 3,
-                                                        [np.empty(S, np.uint8) for _ in range(3)]),
-                       key=f"generate_parity_{id(c)}")
         par = [np.empty(S, np.uint8) for _ in range(3)]
         chk.generate_parity_into(segs, k, 3, par)
         tg_reuse = timed(lambda: chk.generate_parity_into(segs, k, 3, par))
@@ -910,10 +1064,9 @@ def crate_api(ctx, sets, reps=7, staging_ab=True):
             tg_new_in.append(time.perf_counter() - t0)
             del fresh, outs
         tg_new_in = min(tg_new_in)
-        if late:
-            tg = timed(lambda: chk.generate_parity_into(segs, k, 3,
-                                                        [np.empty(S, np.uint8) for _ in range(3)]),
-                       key=f"generate_parity_{id(c)}")
+        tg = timed(lambda: chk.generate_parity_into(segs, k, 3,
+                                                    [np.empty(S, np.uint8) for _ in range(3)]),
+                   key=f"generate_parity_{id(c)}")
         target = sets.erased[0][0]
         slots = [None if i == target else segs[i] for i in range(k)] + [None] * (30 - k)
         tr = timed(lambda: bfrs.recover_segment_rs30_3_into(c, slots, par, target,
@@ -1044,6 +1197,14 @@ def crate_api(ctx, sets, reps=7, staging_ab=True):
     }
     res["link"] = pcie_link(S, k)
     lk = res["link"]
+    ref = reference_copies(segs, S, reps)
+    res["reference_copies"] = ref
+    res["generate_parity"]["floor_plus_copy_out_ms"] = round(
+        lk["floor_generate_parity_ms"] + ref["copy_out_3_shards_ms"], 2)
+    res["generate_parity"]["at_or_under_floor_plus_copy_out"] = bool(
+        res["generate_parity"]["ms"] <= res["generate_parity"]["floor_plus_copy_out_ms"])
+    res["recover_segment_rs30_3"]["floor_plus_copy_out_ms"] = round(
+        lk["floor_recover_one_target_ms"] + ref["copy_out_1_shard_ms"], 2)
     res["generate_parity_all_blocks_threads"]["floor_ms"] = round(
         (sum(sets.shapes) * S / (max(lk["h2d_pageable_GBps"], lk["h2d_pinned_GBps"]) * 1e9) +
          3 * len(sets.shapes) * S / (max(lk["d2h_pinned_GBps"], lk["d2h_pageable_GBps"]) * 1e9))
@@ -1071,6 +1232,38 @@ def crate_api(ctx, sets, reps=7, staging_ab=True):
                               "recover_segment_rs30_3_ms": round(pr * 1e3, 2),
                               "what": f"BFRS_CODEC_STAGING={alt} on a second context, same block"}
     return res
+
+
+def reference_copies(segs, S, reps=7):
+    """The reference's own host copies on this box, in its shape: one thread,
+    fresh heap memory per call (glibc serves 32 MiB from new mmap pages, as it
+    does Rust's Vec), page faults included, best of reps.
+      copy_out_3_shards   generate.rs:95-96: recovery_iter().to_vec() of 3 shards
+      copy_out_1_shard    recovery.rs:166-170: restored_original(target).to_vec()
+      pad_copies          generate.rs:75-82: every segment's to_vec() + resize
+    A crate-shaped call that returns fresh Vecs pays the copy-out on top of
+    the link floor; generate_parity.floor_plus_copy_out_ms is that sum."""
+    import numpy as np
+
+    def best(n_out, srcs):
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            outs = []
+            for j in range(n_out):
+                o = np.empty(S, np.uint8)
+                o[:] = srcs[j % len(srcs)]
+                outs.append(o)
+            ts.append(time.perf_counter() - t0)
+            del outs
+        return min(ts)
+    return {"copy_out_3_shards_ms": round(best(3, segs) * 1e3, 2),
+            "copy_out_1_shard_ms": round(best(1, segs) * 1e3, 2),
+            "pad_copies_ms": round(best(len(segs), segs) * 1e3, 2),
+            "what": "numpy copies into fresh np.empty buffers on one thread (the reference's "
+                    "to_vec() shape: new mmap pages, faulted by the copy), best of "
+                    f"{reps}: 3 shards (generate.rs:95-96), 1 shard (recovery.rs:166-170), "
+                    f"all {len(segs)} segments (the pad copies, generate.rs:75-82)"}
 
 
 B3_GOLDEN = os.path.join(ROOT, "tests", "golden", "blake3_c2.json")
@@ -1126,14 +1319,10 @@ def blake3_device(ctx, sets, calls=10):
         check = {"golden": "tests/golden/blake3_c2.json", "digests": len(hexes),
                  "mismatched": bad, "match": not bad}
     best = min(ts)
-    kern = blake3_kernel_times(ctx, rows)
-    if "group_kernel_ms" in kern:
-        kern["frac_group_kernel"] = round(
-            nbytes / (kern["group_kernel_ms"] * 1e-3) / 1e9 / b3_ceiling_gbps(B3_VALU_PER_64B_ALG), 4)
     return {"GBps": round(nbytes / best / 1e9, 1), "ms": round(best * 1e3, 3),
             "mean_ms": round(sum(ts) / len(ts) * 1e3, 3), "bytes": nbytes,
             "python_wrapper_ms": round(min(wrapper) * 1e3, 3),
-            "kernels": kern,
+            "kernels": None,
             "roofline": {"bound": "valu", "achieved": round(nbytes / best / 1e9, 1),
                          "peak": round(b3_ceiling_gbps(B3_VALU_PER_64B_ALG), 1), "unit": "GB/s",
                          "frac": round(nbytes / best / 1e9 / b3_ceiling_gbps(B3_VALU_PER_64B_ALG), 4),
@@ -1149,59 +1338,6 @@ def blake3_device(ctx, sets, calls=10):
                     "call through ctypes (upload + kernels + digest download), arguments "
                     "marshalled once, best of 10 wall-clock calls; python_wrapper_ms: the same "
                     "through Context.blake3_batch_dev (per-call marshalling and hex digests)"}
-
-
-def blake3_kernel_times(ctx, rows, calls=3):
-    """Kernel time inside bfrs_blake3_batch_dev (torch's profiler, kineto over
-    the ROCm tracer, in this process): per call, the group kernel and the
-    reduce kernels, so the call's wall time splits into device work and the
-    host side (descriptors, launches, digest download)."""
-    import statistics
-    import torch
-    try:
-        from torch.autograd import DeviceType
-        from torch.profiler import ProfilerActivity, profile
-        if ProfilerActivity.CUDA not in torch.profiler.supported_activities():
-            return {"error": "torch profiler has no GPU activity on this build"}
-        call, _ = ctx.blake3_batch_dev_call(rows)
-        call()
-        torch.cuda.synchronize()
-        with profile(activities=[ProfilerActivity.CUDA]) as prof:
-            for _ in range(calls):
-                call()
-        allev = sorted((e.start_ns(), e.duration_ns(), e.name())
-                       for e in prof.profiler.kineto_results.events()
-                       if e.device_type() == DeviceType.CUDA)
-        group = [d / 1e6 for _, d, n in allev if "blake3" in n and "group" in n]
-        reduce_ = [d / 1e6 for _, d, n in allev if "blake3" in n and "reduce" in n]
-        if len(group) < calls:
-            return {"error": f"trace holds {len(group)} group-kernel dispatches"}
-        # each call's device span: its descriptor upload (the HtoD copy before
-        # its group kernel) to the end of its last reduce kernel or download
-        starts = [t for t, _, n in allev if "blake3" in n and "group" in n]
-        spans, timeline = [], None
-        for j, g0 in enumerate(starts):
-            g1 = starts[j + 1] if j + 1 < len(starts) else float("inf")
-            mine = [(t, d, n) for t, d, n in allev
-                    if (g0 <= t < g1 and "HtoD" not in n)
-                    or ("HtoD" in n and t < g0 and (j == 0 or t >= starts[j - 1]))]
-            if "HtoD" not in " ".join(n for _, _, n in mine):
-                continue
-            t0 = min(t for t, _, _ in mine)
-            spans.append((max(t + d for t, d, _ in mine) - t0) / 1e6)
-            timeline = [(round((t - t0) / 1e3, 1), round(d / 1e3, 1), n[:60]) for t, d, n in mine]
-        out = {"group_kernel_ms": round(statistics.median(group), 4),
-               "reduce_kernels_ms_per_call": round(sum(reduce_) / calls, 4),
-               "reduce_launches_per_call": len(reduce_) // calls,
-               "how": f"torch.profiler over {calls} C-ABI calls in this process"}
-        if not spans:
-            out["event_names"] = sorted({n[:60] for _, _, n in allev})[:12]
-        if spans:
-            out["device_span_ms"] = round(min(spans), 4)
-            out["last_call_timeline_us"] = timeline  # (start, duration, name)
-        return out
-    except Exception as e:  # noqa: BLE001 - informative only
-        return {"error": f"{type(e).__name__}: {e}"}
 
 
 def host_pressure():
@@ -1247,7 +1383,7 @@ def rayon_fresh_process():
     generate_parity_all_blocks_threads`; cause not isolated)."""
     cmd = ["timeout", "-s", "KILL", "90", sys.executable,
            os.path.join(ROOT, "tools", "rayon_probe.py")]
-    env = dict(os.environ, PROBE_MODES="pinned", PROBE_REPS="3")
+    env = probe_env(PROBE_MODES="pinned", PROBE_REPS="3")
     try:
         r = subprocess.run(cmd, capture_output=True, text=True, env=env, cwd=ROOT)
     except OSError as e:
@@ -1428,8 +1564,7 @@ def _pmc_pass(counter, args, workdir):
            sys.executable, os.path.abspath(__file__), "--traffic-probe",
            "--segments", str(args.segments), "--segment-bytes", str(args.segment_bytes),
            "--pitch", str(args.pitch), "--layout", args.layout]
-    env = dict(os.environ, TMPDIR=workdir, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
-    env.pop("TORCHELASTIC_RUN_ID", None)  # the probe never joins a process group
+    env = probe_env(TMPDIR=workdir, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
     with open(os.path.join(workdir, f"{counter}.log"), "w") as log:
         rc = subprocess.call(cmd, stdout=log, stderr=subprocess.STDOUT, env=env, cwd=workdir)
     if rc != 0:
@@ -1483,56 +1618,55 @@ def live_pmc_traffic(args):
 TRACE_PASS_TIMEOUT_S = 150
 
 
-def same_process_trace(rt, step, stream, steps, profile_dir=None, settle_ms=300.0):
-    """A kernel trace of THIS process: K more steps on the timed region's own
-    buffers (same process, same HBM placement, right after the timed region),
-    recorded by the profiler built into torch (kineto over the ROCm tracer:
-    GPU start/end timestamps of every dispatch, ours included, since libbfrs
-    runs on torch's HIP runtime).  Returns the gf_apply C2 launches' mean /
-    median and the same loop's own HIP-event launch time, or {"error": ...}.
-    The rocprofv3 child pass (live_kernel_trace) runs in another process,
-    whose buffers may land in the other HBM placement mode."""
+def per_launch_events(rt, encode, decode, stream, sh, steps, settle_ms=300.0):
+    """Every launch's own duration in THIS process, without a profiler: after
+    `settle_ms` of settle steps on the timed region's buffers, K more steps
+    with a pair of HIP events on the launch stream around each launch (the
+    events sit between launches, so each pair brackets one gf_apply kernel).
+    Returns mean / median / min / max over the 2K launches, or {"error": ...}.
+    (Round 4 read the same figures from torch's profiler; a second profiler
+    session in one process is the prime suspect of round 4's SIGSEGV, so no
+    profiler runs in the bench process any more: DESIGN.md §5.)"""
     import statistics
     torch = rt.torch
     try:
-        from torch.autograd import DeviceType
-        from torch.profiler import ProfilerActivity, profile
-        if ProfilerActivity.CUDA not in torch.profiler.supported_activities():
-            return {"error": "torch profiler has no GPU activity on this build"}
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        rt.sync()
-        with profile(activities=[ProfilerActivity.CUDA]) as prof:
-            # the profiler's start idles the GPU, and the clock ramps after
-            # any idle gap (DESIGN.md §5): settle again inside the trace, then
-            # the K traced steps, whose 2K launches are the last in the trace
-            settle(rt, step, settle_ms)
-            ev0.record(stream)
-            for _ in range(steps):
-                step()
-            ev1.record(stream)
-            rt.sync()
-        kern = [(e.start_ns(), e.duration_ns(), e.name())
-                for e in prof.profiler.kineto_results.events()
-                if e.device_type() == DeviceType.CUDA and "gf_apply" in e.name()]
-        if len(kern) < 2 * steps:
-            return {"error": f"trace holds {len(kern)} gf_apply dispatches, expected {2 * steps}"}
-        d = [x[1] / 1e6 for x in sorted(kern)[-2 * steps:]]
-        out = {"how": "torch.profiler (kineto over the ROCm tracer: GPU timestamps of every "
-                      "dispatch) in the bench process itself, on the timed region's own "
-                      f"buffers right after it: {settle_ms:.0f} ms of settle steps, then K "
-                      "traced steps; the last 2K gf_apply dispatches",
-               "kernel": kern[-1][2].rsplit("(", 1)[0].replace("void ", ""),
-               "launches": len(d), "mean_ms": round(statistics.mean(d), 4),
-               "median_ms": round(statistics.median(d), 4), "min_ms": round(min(d), 4),
-               "max_ms": round(max(d), 4),
-               "loop_event_launch_ms": round(ev0.elapsed_time(ev1) / (2 * steps), 4)}
-        if profile_dir:
-            os.makedirs(profile_dir, exist_ok=True)
-            with open(os.path.join(profile_dir, "same_process_trace.json"), "w") as f:
-                json.dump(dict(out, durations_ms=[round(x, 5) for x in d]), f, indent=1)
-        return out
-    except Exception as e:  # noqa: BLE001 - a missing tracer is reported, never fatal
+        settle(rt, lambda: (encode(sh), decode(sh)), settle_ms)
+        pairs = []
+        for _ in range(steps):
+            for fn in (encode, decode):
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record(stream)
+                fn(sh)
+                b.record(stream)
+                pairs.append((a, b))
+        torch.cuda.synchronize()
+        d = [a.elapsed_time(b) for a, b in pairs]
+        return {"how": f"HIP event pair around each of {len(d)} launches (K steps after "
+                       f"{settle_ms:.0f} ms of settle steps, same process and buffers as the "
+                       "timed region)",
+                "launches": len(d), "mean_ms": round(statistics.mean(d), 4),
+                "median_ms": round(statistics.median(d), 4), "min_ms": round(min(d), 4),
+                "max_ms": round(max(d), 4)}
+    except Exception as e:  # noqa: BLE001 - informative only
         return {"error": f"{type(e).__name__}: {e}"}
+
+
+B3_PROBE_CALLS = 3
+
+
+def blake3_trace_figures(live_trace, nbytes):
+    """blake3_device.kernels: the device BLAKE3's kernel split from the
+    rocprofv3 child pass (trace_probe ends with B3_PROBE_CALLS calls over the
+    same 128 segments), so the call's wall time splits into device work and
+    the host side."""
+    b3 = (live_trace or {}).get("blake3")
+    if not b3:
+        return {"error": (live_trace or {}).get("error") or "no BLAKE3 dispatches in the trace pass"}
+    out = dict(b3)
+    if "group_kernel_ms" in out:
+        out["frac_group_kernel"] = round(
+            nbytes / (out["group_kernel_ms"] * 1e-3) / 1e9 / b3_ceiling_gbps(B3_VALU_PER_64B_ALG), 4)
+    return out
 
 
 def trace_probe(args):
@@ -1556,7 +1690,13 @@ def trace_probe(args):
         enc(sh)
         dec(sh)
     _, elapsed, launch_ms = device_loop(rt, step, stream, args)
-    emit({"launch_ms": launch_ms, "steps": args.steps, "ms_per_step": elapsed / args.steps * 1e3})
+    # then the device BLAKE3 of the 128 data segments, as blake3_device calls it
+    call, digests = ctx.blake3_batch_dev_call([sets.data[i] for i in range(sets.data.shape[0])])
+    for _ in range(B3_PROBE_CALLS):
+        call()
+    rt.sync()
+    emit({"launch_ms": launch_ms, "steps": args.steps, "ms_per_step": elapsed / args.steps * 1e3,
+          "blake3_calls": B3_PROBE_CALLS, "blake3_digest0": bytes(digests[0]).hex()})
     return 0
 
 
@@ -1583,6 +1723,31 @@ def summarize_kernel_trace(csv_path, steps):
             "span_ms_per_launch": round((timed[-1][1] - timed[0][0]) / 1e6 / len(d), 4)}
 
 
+def summarize_blake3_trace(csv_path, calls):
+    """The device BLAKE3 calls at the end of the trace pass: the group
+    kernel's median duration, the reduce kernels' time and count per call,
+    and each call's device span (first dispatch start to last dispatch end;
+    a call starts at its group kernel)."""
+    import csv
+    import statistics
+    rows = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"])
+                  for r in csv.DictReader(open(csv_path)) if "blake3" in r["Kernel_Name"])
+    group = [(t0, t1) for t0, t1, n in rows if "group" in n]
+    reduce_ = [(t0, t1) for t0, t1, n in rows if "reduce" in n]
+    if len(group) < calls:
+        return None
+    spans = []
+    for j, (g0, _) in enumerate(group):
+        g_next = group[j + 1][0] if j + 1 < len(group) else float("inf")
+        spans.append((max(t1 for t0, t1, _n in rows if g0 <= t0 < g_next) - g0) / 1e6)
+    return {"group_kernel_ms": round(statistics.median((t1 - t0) / 1e6 for t0, t1 in group), 4),
+            "reduce_kernels_ms_per_call": round(sum(t1 - t0 for t0, t1 in reduce_) / 1e6 / len(group), 4),
+            "reduce_launches_per_call": len(reduce_) // len(group),
+            "device_span_ms": round(min(spans), 4), "calls": len(group),
+            "how": "rocprofv3 --kernel-trace child pass (trace_probe's last "
+                   f"{len(group)} bfrs_blake3_batch_dev calls over C2's 128 segments)"}
+
+
 def live_kernel_trace(args, profile_dir=None):
     """roofline.trace measured in this run: one `rocprofv3 --kernel-trace
     --stats` child pass (the program right after `--`, no shell hop) over the
@@ -1606,8 +1771,7 @@ def live_kernel_trace(args, profile_dir=None):
            "--segments", str(args.segments), "--segment-bytes", str(args.segment_bytes),
            "--pitch", str(args.pitch), "--layout", args.layout, "--steps", str(args.steps),
            "--warmup", str(args.warmup), "--settle-ms", str(args.settle_ms)]
-    env = dict(os.environ, TMPDIR=workdir, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
-    env.pop("TORCHELASTIC_RUN_ID", None)
+    env = probe_env(TMPDIR=workdir, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
     try:
         log_path = os.path.join(workdir, "trace.log")
         with open(log_path, "w") as log:
@@ -1624,6 +1788,7 @@ def live_kernel_trace(args, profile_dir=None):
         if not traces:
             raise RuntimeError("no kernel_trace.csv in the rocprofv3 output")
         summ = summarize_kernel_trace(traces[0], args.steps)
+        summ["blake3"] = summarize_blake3_trace(traces[0], B3_PROBE_CALLS)
         top = []
         if stats:
             for r in list(csv.DictReader(open(stats[0])))[:4]:
@@ -1850,8 +2015,28 @@ def c5_cpu_baseline(adir, m, damaged, nbytes):
 
 
 # ---------------------------------------------------------------- main
+def stub_leg_standins():
+    """CPU stand-ins for the side legs (--stub-legs-builtin: the supervisor
+    and launcher tests run bench.py as a subprocess, where they cannot
+    monkeypatch); each reports a passing check and says it is a stand-in."""
+    return {
+        "check_config1": lambda ctx: {"match": True, "stub": True},
+        "blake3_device": lambda ctx, sets: {"bytes": 0, "parity_check": {"match": True},
+                                            "stub": True},
+        "pcie_inclusive": lambda ctx, sets: {"decode_match": True, "stub": True},
+        "crate_api": lambda ctx, sets: {"recover_match": True, "stub": True},
+        "cpu_baseline": lambda args, sets, info: {"self_check": True, "stub": True},
+        "run_c5": lambda args, ctx: {"blake3_match": True, "repair": {"match": True},
+                                     "stub": True},
+        "c4_one_process": lambda args, ctx, world, one: {"match": True, "contexts": world,
+                                                         "stub": True},
+    }
+
+
 def main(argv=None):
     args = parse(argv)
+    if args.stub_legs_builtin:
+        globals().update(stub_leg_standins())
     if args.workload == "c5":
         line = run_c5(args)
         line.update({"n_gpus": 1, "higher_is_better": True, "vs_baseline": None, "dtype": "u8",
@@ -1895,7 +2080,7 @@ def main(argv=None):
     sets = ShardSets(rt, shapes, S, args.layout, args.pitch)
     fill(rt, sets, seed, lo_b, S_full)
 
-    ctx = None
+    ctx = stream = None
     if not rt.stub:
         import bfrs
         # crate_api runs one codec object per C2 block on as many threads (as
@@ -1913,16 +2098,13 @@ def main(argv=None):
         encode(sh)
         decode(sh)
 
-    settle_steps, elapsed, launch_ms = device_loop(rt, step, stream if not rt.stub else None, args)
+    settle_steps, elapsed, launch_ms = device_loop(rt, step, stream, args)
     if rt.rank == 0:
         progress("timed region done")
     rank_ms = [round(x / args.steps * 1e3, 4) for x in rt.gather_over_ranks(elapsed)]
     elapsed = rt.max_over_ranks(elapsed)
 
-    enc_ms = dec_ms = copy_ms = None
-    sp_trace = None
-    if not rt.stub and args.trace == "auto" and not under_rocprof():
-        sp_trace = same_process_trace(rt, step, stream, args.steps, args.profile_dir)
+    enc_ms = dec_ms = copy_ms = events = None
     if not rt.stub:
         # Per-direction rates: short back-to-back loops after the timed region.
         def per_launch(fn, n=max(3, args.steps // 2)):
@@ -1934,6 +2116,8 @@ def main(argv=None):
             torch.cuda.synchronize()
             return a.elapsed_time(b) / n
         enc_ms, dec_ms = per_launch(encode), per_launch(decode)
+        # every launch's own duration in this process (HIP event pairs; no profiler)
+        events = per_launch_events(rt, encode, decode, stream, sh, args.steps)
         # reference point on this box: a plain device copy (torch copy_) moving the
         # same read + write bytes as one gf_apply launch (SURVEY 8(d) "achievable")
         alg_bytes_launch = sum(k + 3 for k in shapes) * S
@@ -1955,182 +2139,222 @@ def main(argv=None):
     job_bytes_step = 2 * sum(shapes) * (S_full if args.strong else S)
     value = parallel.throughput(job_bytes_step, rt.world, args.steps, elapsed, scaling)
 
+    n1 = rt.world == 1
+    real = not rt.stub or args.stub_legs  # --stub-legs: the CPU tests' stand-ins run the legs
+    solo_legs = n1 and real and not args.strong
+    golden_c2 = golden_covers("c2_128x32MiB", shapes, S, seed) and not rt.stub
+    golden_c4 = (golden_covers("c4_320x32MiB", synth.block_shapes(args.c4_segments), S_full, 0xB10C)
+                 and not rt.stub)
+    R = {}  # leg results by leg name
+
+    line = None
+    if rt.rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "GiB/s",
+            "n_gpus": rt.world,
+            "world_size_observed": rt.observed_world(),
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "settle": {"ms": args.settle_ms, "steps": settle_steps,
+                       "note": "untimed clock-settle steps before the warmup"},
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "rank_ms_per_step": rank_ms,
+            "higher_is_better": True,
+            "scaling": scaling,
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": ("STUB (CPU rehearsal of the launcher, not a measurement)" if rt.stub else
+                     "synthetic splitmix64 bytes (seed 0xB10C on every rank), resident in HBM"),
+            "config": {
+                "workload": ("BASELINE configs[3]: 10 GiB archive, 320 x 32 MiB segments = "
+                             "10xRS(30,3)+1xRS(20,3), column-striped over the GPUs"
+                             if args.strong else
+                             "BASELINE configs[1]+[2]: 128 x 32 MiB segments = 4xRS(30,3)+1xRS(8,3); "
+                             "step = encode batch + 3-erasure decode of every block"),
+                "segments": args.segments, "segment_bytes": S_full,
+                "shard_pitch": int(sets_pitch(S, args, rt)),
+                "layout": args.layout, "blocks": shapes, "parity_shards": 3,
+                "parallelism": (f"64-B column stripes x{rt.world}" if args.strong
+                                else f"independent batch per GPU x{rt.world}"),
+                "kernel_variant": os.environ.get("BFRS_KERNEL_VARIANT", "default"),
+            },
+        }
+        if not rt.stub:
+            line["encode_GiBps_per_gpu"] = round(data_bytes / 2**30 / (enc_ms * 1e-3), 2)
+            line["decode_GiBps_per_gpu"] = round(data_bytes / 2**30 / (dec_ms * 1e-3), 2)
+            line["roofline"] = roofline(alg_bytes, launch_ms, enc_ms, dec_ms, copy_ms,
+                                        live_traffic, live_trace, events)
+        STATE.line = line
+
+    def refresh():
+        """parity_check of the line from the checks and legs done so far."""
+        c4 = line.get("c4_strong")
+        c4_pc = (c4 or {}).get("parity_check") or {}
+        c1, b3, pcie, crate, cpu, c4_1p, c5 = (R.get(k) for k in (
+            "c1_rs13", "blake3_device", "pcie_inclusive", "crate_api", "cpu_baseline",
+            "c4_one_process", "c5"))
+        legs_enabled = {
+            "ranks_ok": (True, all(ranks_ok)),
+            "c2_encode": (golden_c2, leg_flag(my_check["encode"], "match")),
+            "c3_decode": (True, leg_flag(my_check["decode"], "match")),
+            "c1_rs13": (real, leg_flag(c1, "match")),
+            "c4_encode": (args.c4 == "auto" and not args.strong and golden_c4,
+                          leg_flag(c4_pc.get("encode"), "match")),
+            "c4_decode": (args.c4 == "auto" and not args.strong,
+                          leg_flag(c4_pc.get("decode"), "match")),
+            "c4_one_process": (real and args.c4 == "auto" and args.pcie == "auto" and not args.strong,
+                               leg_flag(c4_1p, "match")),
+            "c5_blake3": (solo_legs and args.c5 == "auto", leg_flag(c5, "blake3_match")),
+            "c5_repair": (solo_legs and args.c5 == "auto", leg_flag(c5, "repair", "match")),
+            "blake3_c2": (solo_legs and (golden_c2 or args.stub_legs),
+                          leg_flag(b3, "parity_check", "match")),
+            "blake3_device_ran": (solo_legs, isinstance(b3, dict) and "error" not in b3),
+            "pcie_decode": (solo_legs and args.pcie == "auto", leg_flag(pcie, "decode_match")),
+            "crate_recover": (solo_legs and args.crate == "auto", leg_flag(crate, "recover_match")),
+            "cpu_baseline_self_check": (solo_legs and args.cpu_baseline == "auto",
+                                        leg_flag(cpu, "self_check")),
+        }
+        line["parity_check"] = parity_summary(legs_enabled, {
+            "c1_rs13": c1, "c2_encode": my_check["encode"], "c3_decode": my_check["decode"],
+            "ranks_ok": [bool(x) for x in ranks_ok],
+            "c4_encode": c4_pc.get("encode"), "c4_decode": c4_pc.get("decode"),
+            "c5_blake3": None if c5 is None else c5.get("blake3_match"),
+            "c5_repair": ((c5 or {}).get("repair") or {}).get("match"),
+            "blake3_c2": ((b3 or {}).get("parity_check") or {}).get("match"),
+            "when": "after the timed region, on the buffers the timed launches wrote"})
+        if legs.aborted:
+            line["parity_check"]["aborted"] = legs.aborted
+
+    legs = Legs()
+    if line is not None:
+        refresh()
+        STATE.save()  # the headline survives anything that follows
+
     c4 = None
     if args.c4 == "auto" and not args.strong:
         c4 = run_c4_strong(rt, ctx, args, sh)  # collective inside: every rank runs it, no guard
-
     devices = rt.gather_objects(rt.device_info())  # collective: every rank, before rank 0 goes on
     if rt.rank != 0:
         rt.close()
         return 0 if ok_here else 3
+    line["c4_strong"] = c4
+    line["rank_devices"] = devices
+    line["host_budget"] = host_budget(args, rt.world)
+    refresh()
+    STATE.save()
 
-    n1 = rt.world == 1
+    def leg(name, key, fn, *a):
+        """One side leg, checkpointed before and after (the supervisor names
+        the leg if the process dies inside it)."""
+        STATE.save(running=name, key=key)
+        if args.stub_crash_leg == name:  # test hook: the process dies inside this leg
+            import signal
+            os.kill(os.getpid(), signal.SIGSEGV)
+        r = legs.run(name, fn, *a)
+        R[name] = r
+        if key:
+            line[key] = r
+        refresh()
+        STATE.save()
+        return r
+
     info = host_info()
-    legs = Legs()
-    real = not rt.stub or args.stub_legs  # --stub-legs: the CPU tests' stand-ins run the legs
-    solo_legs = n1 and real and not args.strong
-    c1 = legs.run("c1_rs13", check_config1, ctx) if real else None
-    b3 = legs.run("blake3_device", blake3_device, ctx, sets) if solo_legs else None
-    pcie = crate = cpu = c5 = None
+    if real:
+        leg("c1_rs13", None, check_config1, ctx)
+    if solo_legs:
+        b3 = leg("blake3_device", "blake3_device", blake3_device, ctx, sets)
+        if isinstance(b3, dict) and "error" not in b3 and live_trace:
+            b3["kernels"] = blake3_trace_figures(live_trace, b3["bytes"])
+            STATE.save()
     if solo_legs and args.pcie == "auto":
-        pcie = legs.run("pcie_inclusive", pcie_inclusive, ctx, sets)
+        leg("pcie_inclusive", "pcie_inclusive", pcie_inclusive, ctx, sets)
     if solo_legs and args.crate == "auto":
         host_pinned = pinned_host_state(rt)
-        if os.environ.get("BENCH_HOST_EMPTY_CACHE", "1") == "1" and not rt.stub:
+        if not rt.stub:
             # The earlier legs leave ~27 GB of pinned blocks in torch's caching
             # host allocator.  Held, they slowed the five concurrent blocks by
             # ~20% (r04ec: 85.4/87.4 ms emptied against 104.8/102.0 ms held, one
             # box, alternating; DESIGN.md §7c).  A BlockFrame process holds no
-            # such memory, so give it back first (BENCH_HOST_EMPTY_CACHE=0: keep it)
+            # such memory, so give it back first
             rt.torch._C._host_emptyCache()
             host_pinned["after_empty_cache"] = pinned_host_state(rt)
         load_before = host_pressure()
-        crate = legs.run("crate_api", crate_api, ctx, sets)
+        crate = leg("crate_api", "crate_api", crate_api, ctx, sets)
         if isinstance(crate, dict) and "error" not in crate:
             crate["pinned_host_before"] = host_pinned
             crate["host_pressure"] = {"before": load_before, "after": host_pressure()}
-        if rayon_child is not None and "error" not in crate:
-            crate["generate_parity_all_blocks_fresh_process"] = rayon_child
+            if rayon_child is not None:
+                crate["generate_parity_all_blocks_fresh_process"] = rayon_child
+            STATE.save()
     if solo_legs and args.cpu_baseline == "auto":
-        cpu = legs.run("cpu_baseline", cpu_baseline, args, sets, info)
+        leg("cpu_baseline", "cpu_baseline", cpu_baseline, args, sets, info)
     del sets
-    c4_1p = None
     if real and args.c4 == "auto" and args.pcie == "auto" and not args.strong:
-        c4_1p = legs.run("c4_one_process", c4_one_process, args, ctx, rt.world, args.one_device)
+        c4_1p = leg("c4_one_process", None, c4_one_process, args, ctx, rt.world, args.one_device)
         if c4 is not None:
             c4["pcie_inclusive_one_process"] = c4_1p
     if solo_legs and args.c5 == "auto":
-        c5 = legs.run("c5", run_c5, args, ctx)
-
-    line = {
-        "metric": METRIC,
-        "value": round(value, 2),
-        "unit": "GiB/s",
-        "n_gpus": rt.world,
-        "world_size_observed": rt.observed_world(),
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "settle": {"ms": args.settle_ms, "steps": settle_steps,
-                   "note": "untimed clock-settle steps before the warmup"},
-        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-        "rank_ms_per_step": rank_ms,
-        "higher_is_better": True,
-        "scaling": scaling,
-        "vs_baseline": None,
-        "dtype": "u8",
-        "data": ("STUB (CPU rehearsal of the launcher, not a measurement)" if rt.stub else
-                 "synthetic splitmix64 bytes (seed 0xB10C on every rank), resident in HBM"),
-        "config": {
-            "workload": ("BASELINE configs[3]: 10 GiB archive, 320 x 32 MiB segments = "
-                         "10xRS(30,3)+1xRS(20,3), column-striped over the GPUs"
-                         if args.strong else
-                         "BASELINE configs[1]+[2]: 128 x 32 MiB segments = 4xRS(30,3)+1xRS(8,3); "
-                         "step = encode batch + 3-erasure decode of every block"),
-            "segments": args.segments, "segment_bytes": S_full, "shard_pitch": int(sets_pitch(S, args, rt)),
-            "layout": args.layout, "blocks": shapes, "parity_shards": 3,
-            "parallelism": (f"64-B column stripes x{rt.world}" if args.strong
-                            else f"independent batch per GPU x{rt.world}"),
-            "kernel_variant": os.environ.get("BFRS_KERNEL_VARIANT", "default"),
-        },
-    }
+        leg("c5", "c5", run_c5, args, ctx)
     if not rt.stub:
-        achieved = alg_bytes / (launch_ms * 1e-3) / 1e9
-        traffic, traffic_src = live_traffic if live_traffic else (None, None)
-        if traffic is not None:
-            traffic_src["ratio_to_algorithmic"] = round(traffic / alg_bytes, 4)
-        else:
-            live_err = (traffic_src or {}).get("error")
-            traffic, traffic_src = pmc_traffic(alg_bytes)
-            live_note = live_err or ("skipped under rocprofv3" if under_rocprof() else "off")
-            traffic_src = dict(traffic_src or {}, live_pass=live_note)
-        line["encode_GiBps_per_gpu"] = round(data_bytes / 2**30 / (enc_ms * 1e-3), 2)
-        line["decode_GiBps_per_gpu"] = round(data_bytes / 2**30 / (dec_ms * 1e-3), 2)
-        line["roofline"] = {
-            "bound": "hbm",
-            "kernel": ("gf_apply_unrolled_kernel (variant 76: unrolled SDWA-addressed GF(2^8)-"
-                       "subfield pass, contiguous-line nt loads)"
-                       if os.environ.get("BFRS_KERNEL_VARIANT", "76") == "76" else
-                       f"gf_apply (variant {os.environ.get('BFRS_KERNEL_VARIANT')})"),
-            "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-            "traffic_source": traffic_src,
-            "alg_bytes_per_launch": alg_bytes,
-            "launch_ms": round(launch_ms, 4),
-            "launch_ms_by_direction": {"encode": round(enc_ms, 4), "decode": round(dec_ms, 4)},
-            "timing": "HIP events on the launch stream over the timed region / launches",
-            "device_copy_reference": {
-                "GBps": round(alg_bytes / (copy_ms * 1e-3) / 1e9, 1),
-                "ms": round(copy_ms, 4),
-                "what": "torch copy_ of alg_bytes/2 bytes (same read + write bytes as one launch), same box"},
-        }
-        trace = live_trace
-        if trace and "error" not in trace:
-            trace["ratio_mean_to_launch_ms"] = round(trace["mean_ms"] / launch_ms, 4)
-            trace["frac_at_trace_mean"] = round(
-                alg_bytes / (trace["mean_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
-        elif trace is None:
-            trace = {"live_pass": "skipped under rocprofv3" if under_rocprof() else "off"}
-        if trace and "error" not in trace:
-            trace["note"] = ("another process: its shard buffers land wherever the driver places "
-                             "them, in either HBM placement mode (DESIGN.md §9b), so its launch "
-                             "time can differ from this process's by the mode gap (~8%)")
-        if sp_trace and "error" not in sp_trace:
-            sp_trace["ratio_mean_to_launch_ms"] = round(sp_trace["mean_ms"] / launch_ms, 4)
-            sp_trace["ratio_median_to_launch_ms"] = round(sp_trace["median_ms"] / launch_ms, 4)
-            sp_trace["frac_at_trace_mean"] = round(
-                alg_bytes / (sp_trace["mean_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
-        # roofline.trace: a kernel trace of this very process (same buffers,
-        # same placement); the rocprofv3 child pass beside it
-        line["roofline"]["trace"] = sp_trace
-        line["roofline"]["trace_rocprofv3_child"] = trace
-        line["cpu_baseline"] = cpu
-        line["crate_api"] = crate
-        line["pcie_inclusive"] = pcie
-        line["c5"] = c5
-        line["blake3_device"] = b3
-    elif args.stub_legs:
-        line.update({"cpu_baseline": cpu, "crate_api": crate, "pcie_inclusive": pcie, "c5": c5,
-                     "blake3_device": b3})
-    line["c4_strong"] = c4
-    line["rank_devices"] = devices
-    line["host_budget"] = host_budget(args, rt.world)
-    golden_c2 = golden_covers("c2_128x32MiB", shapes, S, seed) and not rt.stub
-    golden_c4 = (golden_covers("c4_320x32MiB", synth.block_shapes(args.c4_segments), S_full, 0xB10C)
-                 and not rt.stub)
-    c4_pc = (c4 or {}).get("parity_check") or {}
-    legs_enabled = {
-        "ranks_ok": (True, all(ranks_ok)),
-        "c2_encode": (golden_c2, leg_flag(my_check["encode"], "match")),
-        "c3_decode": (True, leg_flag(my_check["decode"], "match")),
-        "c1_rs13": (real, leg_flag(c1, "match")),
-        "c4_encode": (args.c4 == "auto" and not args.strong and golden_c4,
-                      leg_flag(c4_pc.get("encode"), "match")),
-        "c4_decode": (args.c4 == "auto" and not args.strong, leg_flag(c4_pc.get("decode"), "match")),
-        "c4_one_process": (real and args.c4 == "auto" and args.pcie == "auto" and not args.strong,
-                           leg_flag(c4_1p, "match")),
-        "c5_blake3": (solo_legs and args.c5 == "auto", leg_flag(c5, "blake3_match")),
-        "c5_repair": (solo_legs and args.c5 == "auto", leg_flag(c5, "repair", "match")),
-        "blake3_c2": (solo_legs and (golden_c2 or args.stub_legs),
-                      leg_flag(b3, "parity_check", "match")),
-        "blake3_device_ran": (solo_legs, isinstance(b3, dict) and "error" not in b3),
-        "pcie_decode": (solo_legs and args.pcie == "auto", leg_flag(pcie, "decode_match")),
-        "crate_recover": (solo_legs and args.crate == "auto", leg_flag(crate, "recover_match")),
-        "cpu_baseline_self_check": (solo_legs and args.cpu_baseline == "auto",
-                                    leg_flag(cpu, "self_check")),
-    }
-    line["parity_check"] = parity_summary(legs_enabled, {
-        "c1_rs13": c1, "c2_encode": my_check["encode"], "c3_decode": my_check["decode"],
-        "ranks_ok": [bool(x) for x in ranks_ok],
-        "c4_encode": c4_pc.get("encode"), "c4_decode": c4_pc.get("decode"),
-        "c5_blake3": None if c5 is None else c5.get("blake3_match"),
-        "c5_repair": ((c5 or {}).get("repair") or {}).get("match"),
-        "blake3_c2": ((b3 or {}).get("parity_check") or {}).get("match"),
-        "when": "after the timed region, on the buffers the timed launches wrote"})
-    if legs.aborted:
-        line["parity_check"]["aborted"] = legs.aborted
+        for key in ("cpu_baseline", "crate_api", "pcie_inclusive", "c5", "blake3_device"):
+            line.setdefault(key, None)
+    refresh()
     emit(line)
     rt.close()
     return 0 if line["parity_check"]["all_ok"] else 1
+
+
+def roofline(alg_bytes, launch_ms, enc_ms, dec_ms, copy_ms, live_traffic, live_trace, events):
+    """The line's roofline object: achieved = algorithmic bytes per launch /
+    the launch time from HIP events over the timed region; traffic from the
+    live PMC passes (or the committed record); the rocprofv3 child pass's
+    kernel trace and this process's per-launch event pairs beside it."""
+    achieved = alg_bytes / (launch_ms * 1e-3) / 1e9
+    traffic, traffic_src = live_traffic if live_traffic else (None, None)
+    if traffic is not None:
+        traffic_src["ratio_to_algorithmic"] = round(traffic / alg_bytes, 4)
+    else:
+        live_err = (traffic_src or {}).get("error")
+        traffic, traffic_src = pmc_traffic(alg_bytes)
+        live_note = live_err or ("skipped under rocprofv3" if under_rocprof() else "off")
+        traffic_src = dict(traffic_src or {}, live_pass=live_note)
+    trace = live_trace
+    if trace and "error" not in trace:
+        trace = dict(trace)
+        trace.pop("blake3", None)
+        trace["ratio_mean_to_launch_ms"] = round(trace["mean_ms"] / launch_ms, 4)
+        trace["frac_at_trace_mean"] = round(
+            alg_bytes / (trace["mean_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
+        trace["note"] = ("another process: its shard buffers land wherever the driver places "
+                         "them, in either HBM placement mode (DESIGN.md §9b), so its launch "
+                         "time can differ from this process's by the mode gap (~8%)")
+    elif trace is None:
+        trace = {"live_pass": "skipped under rocprofv3" if under_rocprof() else "off"}
+    if events and "error" not in events:
+        events["ratio_mean_to_launch_ms"] = round(events["mean_ms"] / launch_ms, 4)
+        events["frac_at_mean"] = round(alg_bytes / (events["mean_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
+    return {
+        "bound": "hbm",
+        "kernel": ("gf_apply_unrolled_kernel (variant 76: unrolled SDWA-addressed GF(2^8)-"
+                   "subfield pass, contiguous-line nt loads)"
+                   if os.environ.get("BFRS_KERNEL_VARIANT", "76") == "76" else
+                   f"gf_apply (variant {os.environ.get('BFRS_KERNEL_VARIANT')})"),
+        "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+        "traffic_source": traffic_src,
+        "alg_bytes_per_launch": alg_bytes,
+        "launch_ms": round(launch_ms, 4),
+        "launch_ms_by_direction": {"encode": round(enc_ms, 4), "decode": round(dec_ms, 4)},
+        "timing": "HIP events on the launch stream over the timed region / launches",
+        "trace": trace,
+        "per_launch_events": events,
+        "device_copy_reference": {
+            "GBps": round(alg_bytes / (copy_ms * 1e-3) / 1e9, 1),
+            "ms": round(copy_ms, 4),
+            "what": "torch copy_ of alg_bytes/2 bytes (same read + write bytes as one launch), same box"},
+    }
 
 
 def sets_pitch(S, args, rt):
@@ -2141,5 +2365,16 @@ def sets_pitch(S, args, rt):
 
 
 if __name__ == "__main__":
+    faulthandler.enable(all_threads=True)  # a fault prints every thread's Python stack
     claim_stdout()
-    sys.exit(main())
+    if wants_supervisor(parse()):
+        sys.exit(supervise(sys.argv[1:]))
+    args = parse()
+    rc = main()
+    if STATE.path and not (args.traffic_probe or args.trace_probe or under_rocprof()):
+        # the measurement child: the line is in the state file; leave without
+        # the interpreter's and the runtimes' teardown (the supervisor prints)
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(rc)
+    sys.exit(rc)

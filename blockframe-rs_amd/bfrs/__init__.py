@@ -425,9 +425,10 @@ class Context:
         st = _stream_handle(stream, list(d_msgs))
         fn, h, out = lib().bfrs_blake3_batch_dev, self.handle, dig.ctypes.data
 
-        def call():
+        def call(_keep=(km, ls, dig)):
+            # _keep: the pointer arrays AND the digest array `out` points into
+            # stay alive as long as call does, whatever the caller keeps
             _check(fn(h, n, pm, ls, None, out, None, st))
-            return km, ls  # keeps the ctypes arrays referenced by the closure
         return call, dig[:n]
 
     # ---- host-memory batch API (host buffers: numpy arrays or CPU torch tensors)

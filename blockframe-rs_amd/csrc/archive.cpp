@@ -31,6 +31,7 @@
 #include <unordered_set>
 
 #include "archive_io.hpp"
+#include "knobs.hpp"
 #include "blake3.hpp"
 #include "gpu_block.hpp"
 #include "manifest.hpp"
@@ -1351,7 +1352,7 @@ int bfrs_archive_open(bfrs_ctx *ctx, const char *archive_dir, size_t cache_segme
   a->pool = std::make_shared<PinnedPool>(a->g.S);
   if (const char *e = std::getenv("BFRS_PREFETCH_DEPTH"))
     a->prefetch_depth = size_t(std::clamp(std::strtol(e, nullptr, 10), 1L, 256L));
-  if (const char *e = std::getenv("BFRS_PREFETCH_WORKERS"))
+  if (const char *e = BFRS_AB_KNOB("BFRS_PREFETCH_WORKERS"))
     a->prefetch_workers = size_t(std::clamp(std::strtol(e, nullptr, 10), 1L, 16L));
   a->prefetch = a->g.nseg > 1;
   if (a->prefetch) {

@@ -15,6 +15,7 @@
 #include <thread>
 
 #include "runtime.hpp"
+#include "knobs.hpp"
 
 using namespace bfrs;
 
@@ -62,7 +63,7 @@ bool overlaps(const uint8_t *a, size_t na, const uint8_t *b, size_t nb) {
 bool slab_wrapper_ok(bfrs_ctx *ctx, const uint8_t *const *segs, size_t n, size_t shard,
                      bool allow_missing = false) {
   static const bool on = [] {
-    const char *e = std::getenv("BFRS_WRAPPER_SLABS");
+    const char *e = BFRS_AB_KNOB("BFRS_WRAPPER_SLABS");
     return !(e && std::strcmp(e, "0") == 0);
   }();
   if (!on || shard < (size_t(16) << 20) || ctx->impl.codec_pool->staging != Staging::kPinned)
@@ -122,7 +123,7 @@ int bfrs_generate_parity(bfrs_ctx *ctx, const uint8_t *const *segments, const si
     }
     if ((rc = bfrs_encoder_add_original_shard(enc.p, src, max_len))) return rc;
   }
-  if (std::getenv("BFRS_TRACE"))  // measurement aid (tools/crate_probe.py)
+  if (BFRS_AB_KNOB("BFRS_TRACE"))  // measurement aid (tools/crate_probe.py)
     std::fprintf(stderr, "bfrs trace: generate_parity adds %.3f ms\n",
                  std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_add)
                      .count());

@@ -27,6 +27,7 @@
 #include <thread>
 
 #include "runtime.hpp"
+#include "knobs.hpp"
 
 using namespace bfrs;
 
@@ -36,7 +37,7 @@ namespace {
 // 1-8; 0 or unset: the call's default).  A/B knob.
 size_t prefault_parts(size_t dflt) {
   static const long v = [] {
-    const char *e = std::getenv("BFRS_PREFAULT_PARTS");
+    const char *e = BFRS_AB_KNOB("BFRS_PREFAULT_PARTS");
     return e ? std::strtol(e, nullptr, 10) : 0L;
   }();
   return v >= 1 && v <= 8 ? size_t(v) : dflt;
@@ -46,7 +47,7 @@ size_t prefault_parts(size_t dflt) {
 // buffers in while the device works (encoder_encode_to_host).
 bool prefault_outputs() {
   static const bool on = [] {
-    const char *e = std::getenv("BFRS_PREFAULT_OUTPUTS");
+    const char *e = BFRS_AB_KNOB("BFRS_PREFAULT_OUTPUTS");
     return !(e && std::strcmp(e, "0") == 0);
   }();
   return on;
@@ -250,7 +251,7 @@ int bfrs::encoder_encode_to_host(bfrs_encoder *e, uint8_t *const *outs) {
     wait_ms += std::chrono::duration<double, std::milli>(t1 - t0).count();
     copy_ms += std::chrono::duration<double, std::milli>(clk::now() - t1).count();
   }
-  if (std::getenv("BFRS_TRACE"))  // measurement aid (tools/crate_probe.py)
+  if (BFRS_AB_KNOB("BFRS_TRACE"))  // measurement aid (tools/crate_probe.py)
     std::fprintf(stderr, "bfrs trace: encode_to_host wait %.3f ms, copy-out %.3f ms\n", wait_ms,
                  copy_ms);
   // the pinned rows hold the recovery shards too, as after encode()

@@ -2,6 +2,7 @@
 // Host-only (no HIP): also linked into the ThreadSanitizer driver
 // (tools/tsan_host.cpp, make host-tsan).
 #include "host_copy.hpp"
+#include "knobs.hpp"
 
 #include <sched.h>
 #include <sys/mman.h>
@@ -9,6 +10,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cerrno>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -21,6 +23,10 @@ namespace {
 long env_long(const char *name, long dflt) {
   const char *e = std::getenv(name);
   return e && *e ? std::strtol(e, nullptr, 10) : dflt;
+}
+
+long ab_long(const char *value, long dflt) {  // a BFRS_AB_KNOB's value (knobs.hpp)
+  return value && *value ? std::strtol(value, nullptr, 10) : dflt;
 }
 
 // CPUs this process may use: the affinity mask, capped by a cgroup-v2 CPU
@@ -39,9 +45,10 @@ long cpu_share() {
   return std::max(1L, n);
 }
 
-// BFRS_HOST_COPY_THREADS (1..8, default 8) caps the threads of one call.
+// At most 8 threads per call (BFRS_HOST_COPY_THREADS, 1..8: measurement
+// build only).
 size_t max_parts() {
-  static const size_t v = size_t(std::clamp(env_long("BFRS_HOST_COPY_THREADS", 8), 1L, 8L));
+  static const size_t v = size_t(std::clamp(ab_long(BFRS_AB_KNOB("BFRS_HOST_COPY_THREADS"), 8), 1L, 8L));
   return v;
 }
 
@@ -121,7 +128,7 @@ void prefault_range(uint8_t *p, size_t n) {
 #endif
   static const uintptr_t page = uintptr_t(sysconf(_SC_PAGESIZE) > 0 ? sysconf(_SC_PAGESIZE) : 4096);
   static std::atomic<bool> populate_ok{[] {  // BFRS_PREFAULT_POPULATE=0: always touch (A/B)
-    const char *e = std::getenv("BFRS_PREFAULT_POPULATE");
+    const char *e = BFRS_AB_KNOB("BFRS_PREFAULT_POPULATE");
     return !(e && e[0] == '0');
   }()};
   const uintptr_t a = reinterpret_cast<uintptr_t>(p), e = a + n;
@@ -133,7 +140,10 @@ void prefault_range(uint8_t *p, size_t n) {
       q[n - 1] = 0;
       return;
     }
-    populate_ok.store(false, std::memory_order_relaxed);  // older kernel: touch instead
+    // EINVAL: a kernel without MADV_POPULATE_WRITE, so touch from now on.
+    // Anything else (EINTR, EAGAIN, or EFAULT / ENOMEM on an unusual mapping
+    // of this caller) falls back for this call only.
+    if (errno == EINVAL) populate_ok.store(false, std::memory_order_relaxed);
   }
   for (size_t o = 0; o < n; o += 4096) q[o] = 0;
   q[n - 1] = 0;

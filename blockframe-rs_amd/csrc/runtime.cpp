@@ -5,6 +5,7 @@
 // There is no CPU compute path: without a HIP device every codec entry point
 // fails with BFRS_E_NO_DEVICE.
 #include "runtime.hpp"
+#include "knobs.hpp"
 
 #include <algorithm>
 #include <thread>
@@ -259,16 +260,20 @@ int Context::init(int dev) {
   if (kernel_variant() < 0)
     return set_error(BFRS_E_INVALID_ARGUMENT,
                      std::string("BFRS_KERNEL_VARIANT=") + std::getenv("BFRS_KERNEL_VARIANT") +
-                         (ab_build() ? " is not a known kernel variant (probes need BFRS_ALLOW_PROBE=1)"
-                                     : " is not built into this library (product kernels: 76, 75, "
-                                       "73; A/B variants: make ab -> libbfrs_ab.so)"));
+#ifdef BFRS_AB_VARIANTS
+                         " is not a known kernel variant (probes need BFRS_ALLOW_PROBE=1)"
+#else
+                         " is not built into this library (product kernels: 76, 75, "
+                         "73; A/B variants: make ab -> libbfrs_ab.so)"
+#endif
+    );
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
     return set_error(BFRS_E_NO_DEVICE, "no HIP device available (no CPU fallback)");
   if (dev < 0 || dev >= n) return set_error(BFRS_E_NO_DEVICE, "HIP device id out of range");
   device = dev;
   if (const char *e = std::getenv("BFRS_PLAN_CACHE")) max_plans = std::max(1, atoi(e));
-  if (const char *e = std::getenv("BFRS_PIPE_SLOTS"))
+  if (const char *e = BFRS_AB_KNOB("BFRS_PIPE_SLOTS"))
     pipe_slots = std::min(kPipeSlotsMax, std::max(2, atoi(e)));
   codec_pool->device = dev;
   if (const char *e = std::getenv("BFRS_CODEC_SLOTS")) {
@@ -287,7 +292,7 @@ int Context::init(int dev) {
   // stream set and the FIFO copy streams are kept as options: neither was
   // consistently faster in the bench process
   size_t codec_streams = 0;
-  if (const char *e = std::getenv("BFRS_CODEC_STREAMS")) {
+  if (const char *e = BFRS_AB_KNOB("BFRS_CODEC_STREAMS")) {
     char *end = nullptr;
     const long v = std::strtol(e, &end, 10);
     if (end == e || v < 0 || v > 64)
@@ -296,7 +301,7 @@ int Context::init(int dev) {
     codec_streams = size_t(v);
   }
   bool copy_streams = false;
-  if (const char *e = std::getenv("BFRS_CODEC_COPIES")) {
+  if (const char *e = BFRS_AB_KNOB("BFRS_CODEC_COPIES")) {
     if (std::strcmp(e, "stream") == 0)
       copy_streams = true;
     else if (std::strcmp(e, "slot") != 0 && *e)
@@ -319,7 +324,7 @@ int Context::run_host(bool decode, size_t nblocks, const uint32_t *ks, size_t m,
   // Slab width: whole 64-byte chunks, ~8 MiB of columns per shard (env
   // BFRS_SLAB_BYTES overrides), the shard's tail chunk rides in the last slab.
   size_t slab = 8u << 20;
-  if (const char *e = std::getenv("BFRS_SLAB_BYTES")) slab = std::max<size_t>(64, atoll(e));
+  if (const char *e = BFRS_AB_KNOB("BFRS_SLAB_BYTES")) slab = std::max<size_t>(64, atoll(e));
   slab = std::max<size_t>(64, slab / 64 * 64);
   if (slab >= shard_bytes) slab = shard_bytes;
   size_t kmax = 0;
@@ -490,7 +495,7 @@ int Context::run_window(const std::vector<BlockIO> &blocks, size_t shard_bytes,
       // Workgroup sizing: one 8 KiB tile per workgroup unless the grid is huge.
       const uint64_t total_tiles = uint64_t(n_tiles) * (last - first);
       uint32_t tpw = uint32_t(std::max<uint64_t>(1, total_tiles / 65536));
-      if (const char *e = std::getenv("BFRS_TILES_PER_WG")) tpw = std::max(1, atoi(e));
+      if (const char *e = BFRS_AB_KNOB("BFRS_TILES_PER_WG")) tpw = std::max(1, atoi(e));
       const uint32_t wgs_per_pass = (n_tiles + tpw - 1) / tpw;
 
       KernArgs ka{};

@@ -20,7 +20,7 @@
  * how rayon's one-encoder-per-block use (src/chunker/commit.rs:391-466) maps
  * onto it.  Encoder/decoder objects and the batch calls may run concurrently
  * on one context: each codec object owns a pooled slot (device rows, pinned
- * rows, a HIP stream unless BFRS_CODEC_STREAMS shares a set), the plan cache
+ * rows, a HIP stream), the plan cache
  * and the slot pool are locked, the
  * host-batch pipeline and the BLAKE3 work area are serialised.  A single
  * encoder or decoder object is used by one thread at a time (as the crate's
@@ -35,34 +35,26 @@
  * its context (it shares the context's slot pool); every other call on it
  * needs the context open.  Free archive handles before bfrs_close.
  *
- * Environment, read by bfrs_open (BFRS_HOST_COPY_* on first use, once per
- * process):
- *   BFRS_CODEC_SLOTS    idle codec slots kept (default 2; 0 = none)
- *   BFRS_CODEC_STREAMS  0 (default): one HIP stream per codec slot; n > 0:
- *                       the codec objects of a context share n streams
- *                       created with it (an object takes the one with the
- *                       fewest live objects)
- *   BFRS_CODEC_COPIES   "slot" (default: an object's copies run on its own
- *                       stream) or "stream" (every codec object's H2D copies
- *                       go through one stream of the context and its D2H
- *                       copies through another, in FIFO order; kernels wait
- *                       on per-object events)
- *   BFRS_PREFAULT_OUTPUTS  1 (default): bfrs_generate_parity faults the caller's
- *                       output pages in on helper threads while the device
- *                       works; 0: the copy-out faults them
+ * Environment: libbfrs.so reads exactly these six knobs (tests/test_abi.py
+ * checks the BFRS_* strings in the binary against this list).  The knobs of
+ * concluded A/B studies (pipeline depth, slab width, stream layout, prefault
+ * modes, ...) exist only in the measurement build
+ * libbfrs_ab.so (csrc/knobs.hpp).
+ *   BFRS_CODEC_SLOTS    idle codec slots a context keeps (read by bfrs_open;
+ *                       default 2; 0 = none)
  *   BFRS_CODEC_STAGING  "pinned" (default: add_*_shard copies into a pinned
  *                       row on several threads and queues its H2D) or
  *                       "direct" (one DMA straight from the caller's buffer);
- *                       either way the buffer is free on return
- *   BFRS_HOST_COPY_THREADS  copy threads per staging call (1..8, default 8);
- *                       the copy threads of all concurrent calls share the
- *                       process's CPU share (cgroup quota), split evenly
+ *                       either way the buffer is free on return (bfrs_open)
+ *   BFRS_PLAN_CACHE     coefficient plans a context caches (bfrs_open;
+ *                       default 4096, at least 1)
+ *   BFRS_PREFETCH_DEPTH archive read handles: segments loaded ahead of the
+ *                       reader (default 16, at most half the cache; read by
+ *                       bfrs_archive_open)
+ *   BFRS_HOST_COPY_BUDGET  helper threads of all concurrent host copies
+ *                       together (default: the process's CPU share - 1, the
+ *                       cgroup quota; read once per process), split evenly
  *                       between the calls in flight
- *   BFRS_HOST_COPY_BUDGET   helper threads in total (default CPU share - 1)
- *   BFRS_PREFETCH_DEPTH / BFRS_PREFETCH_WORKERS  archive read handles: segments
- *                       loaded ahead of the reader (default 16, at most half
- *                       the cache) and the threads that load them (default 2);
- *                       read by bfrs_archive_open
  *   BFRS_KERNEL_VARIANT unset or 76 (default kernel); 75 / 73 force the looped
  *                       subfield / general kernels; anything else fails
  *                       bfrs_open with BFRS_E_INVALID_ARGUMENT (the A/B

@@ -87,6 +87,30 @@ def test_product_code_object_carries_only_product_kernels(bfrs):
         assert PRODUCT_KERNELS < set(code_objects.kernels(ab))
 
 
+PRODUCT_KNOBS = ["BFRS_CODEC_SLOTS", "BFRS_CODEC_STAGING", "BFRS_HOST_COPY_BUDGET",
+                 "BFRS_KERNEL_VARIANT", "BFRS_PLAN_CACHE", "BFRS_PREFETCH_DEPTH"]
+
+
+def _knob_strings(path):
+    data = open(path, "rb").read()
+    return sorted({m.decode() for m in re.findall(rb"BFRS_[A-Z0-9_]+", data)
+                   if not m.startswith(b"BFRS_E_")})
+
+
+def test_product_reads_only_the_documented_knobs():
+    """libbfrs.so has one soak-proven configuration.  The
+    only environment names in its binary are the six knobs include/bfrs.h
+    documents; the concluded A/B knobs (knobs.hpp) live in libbfrs_ab.so."""
+    product = os.path.join(ROOT, "blockframe-rs_amd", "libbfrs.so")
+    assert _knob_strings(product) == PRODUCT_KNOBS
+    doc = open(HEADER).read().split("#ifndef BFRS_H")[0]
+    documented = sorted(set(re.findall(r"^ \*   (BFRS_[A-Z0-9_]+)", doc, flags=re.M)))
+    assert documented == PRODUCT_KNOBS
+    ab = os.path.join(ROOT, "blockframe-rs_amd", "libbfrs_ab.so")
+    if os.path.exists(ab):
+        assert set(PRODUCT_KNOBS) < set(_knob_strings(ab))
+
+
 @pytest.mark.parametrize("value", ["44", "58", "77", "74", "abc", "76x", "-1"])
 def test_unknown_kernel_variant_is_refused(bfrs, monkeypatch, value):
     """A stray BFRS_KERNEL_VARIANT never silently changes the product's kernel:

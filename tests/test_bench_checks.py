@@ -352,3 +352,122 @@ def test_live_kernel_trace_child_pass(monkeypatch, tmp_path):
     assert os.path.exists(os.path.join(prof, "trace_c2_launch_summary.json"))
     monkeypatch.setattr(sp, "call", lambda cmd, **kw: 124)
     assert "exited 124" in bench.live_kernel_trace(args)["error"]
+
+
+# ---------------------------------------------------------------- supervisor
+def test_supervisor_keeps_the_line_when_the_child_segfaults():
+    """The measurement child dies by SIGSEGV inside a leg after the timed
+    region: the GPU-free parent still prints the line with the completed
+    legs, names the leg and the signal in parity_check.aborted, sets all_ok
+    false and exits non-zero (128 + 11); faulthandler printed the stack."""
+    import json
+    import subprocess
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--stub-legs-builtin",
+                        "--segments", "4", "--segment-bytes", "4096", "--steps", "2",
+                        "--warmup", "1", "--settle-ms", "0", "--c4", "off",
+                        "--stub-crash-leg", "pcie_inclusive"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 139, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    line = json.loads(lines[0])
+    pc = line["parity_check"]
+    assert pc["aborted"] == "pcie_inclusive: SIGSEGV" and pc["all_ok"] is False
+    assert "leg pcie_inclusive" in pc["failed"]
+    assert line["value"] > 0 and line["ms_per_step"] > 0  # the headline survived
+    assert line["blake3_device"]["stub"]                   # a leg done before the crash
+    assert "died in this leg" in line["pcie_inclusive"]["error"]
+    assert "crate_api" not in line                          # never started
+    assert "Fatal Python error: Segmentation fault" in r.stderr
+    assert "in leg" in r.stderr
+
+
+def test_supervisor_passes_a_complete_line_through():
+    import json
+    import subprocess
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--stub-legs-builtin",
+                        "--segments", "4", "--segment-bytes", "4096", "--steps", "2",
+                        "--warmup", "1", "--settle-ms", "0", "--c4", "off"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    pc = line["parity_check"]
+    assert pc["all_ok"] and "aborted" not in pc and pc["failed"] == []
+    for key in ("blake3_device", "pcie_inclusive", "crate_api", "cpu_baseline", "c5"):
+        assert line[key]["stub"], key
+
+
+def test_finish_supervised_rules(capsys):
+    import json
+    base = {"value": 4800.0, "parity_check": {"failed": [], "all_ok": True}}
+    # a final line: printed as written, with the child's own code
+    assert bench.finish_supervised({"line": dict(base), "final": True}, 0) == 0
+    assert json.loads(capsys.readouterr().out)["value"] == 4800.0
+    # a final line, then a crash in the teardown: flagged, non-zero
+    rc = bench.finish_supervised({"line": json.loads(json.dumps(base)), "final": True}, -11)
+    out = json.loads(capsys.readouterr().out)
+    assert rc == 139 and out["parity_check"]["aborted"] == "after the line: SIGSEGV"
+    assert out["parity_check"]["all_ok"] is False
+    # a checkpoint between legs, child killed
+    rc = bench.finish_supervised({"line": json.loads(json.dumps(base)), "final": False,
+                                  "running": None}, -9)
+    out = json.loads(capsys.readouterr().out)
+    assert rc == 137 and out["parity_check"]["aborted"] == "between legs: SIGKILL"
+    # an exit code instead of a signal, inside a leg
+    rc = bench.finish_supervised({"line": json.loads(json.dumps(base)), "final": False,
+                                  "running": "c5", "running_key": "c5"}, 3)
+    out = json.loads(capsys.readouterr().out)
+    assert rc == 3 and out["parity_check"]["aborted"] == "c5: exit 3" and "error" in out["c5"]
+    # no checkpoint at all: no line
+    assert bench.finish_supervised(None, -11) == 139
+    assert capsys.readouterr().out == ""
+
+
+def test_supervisor_not_used_where_it_must_not_be(monkeypatch):
+    for k in [k for k in os.environ if k.startswith("ROCPROF_")]:
+        monkeypatch.delenv(k)
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    assert bench.wants_supervisor(bench.parse([]))
+    assert not bench.wants_supervisor(bench.parse(["--no-supervisor"]))
+    assert not bench.wants_supervisor(bench.parse(["--trace-probe"]))
+    assert not bench.wants_supervisor(bench.parse(["--gpus", "2"]))  # the spawn launcher
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    assert bench.wants_supervisor(bench.parse(["--gpus", "2"]))  # a rank process
+    monkeypatch.setenv("ROCPROF_OUTPUT_PATH", "/tmp/x")
+    assert not bench.wants_supervisor(bench.parse([]))  # the profiled process measures
+
+
+def test_blake3_kernel_split_from_the_trace(tmp_path):
+    import csv
+    p = str(tmp_path / "t.csv")
+    with open(p, "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["Kind", "Dispatch_Id", "Kernel_Name", "Start_Timestamp", "End_Timestamp",
+                    "Grid_Size_X"])
+        t = 0
+        for call in range(3):
+            w.writerow(["K", 0, "void bfrs::blake3_group_kernel<3u, 0u>(...)", t, t + 1_400_000, 1])
+            w.writerow(["K", 0, "void bfrs::blake3_reduce_kernel<64u>(...)", t + 1_410_000,
+                        t + 1_430_000, 1])
+            w.writerow(["K", 0, "void bfrs::blake3_reduce_kernel<64u>(...)", t + 1_440_000,
+                        t + 1_450_000 + call, 1])
+            t += 5_000_000
+    s = bench.summarize_blake3_trace(p, 3)
+    assert s["group_kernel_ms"] == 1.4 and s["reduce_launches_per_call"] == 2
+    assert s["reduce_kernels_ms_per_call"] == pytest.approx(0.03, abs=1e-4)
+    assert s["device_span_ms"] == 1.45 and s["calls"] == 3
+    assert bench.summarize_blake3_trace(p, 4) is None
+    fig = bench.blake3_trace_figures({"blake3": s}, 128 * 32 * 2**20)
+    assert 0 < fig["frac_group_kernel"] < 2
+    assert "error" in bench.blake3_trace_figures({"error": "x"}, 1)
+
+
+def test_probe_children_never_see_the_state_file(monkeypatch):
+    """A probe child (PMC / trace pass, rayon probe) must neither write its
+    line into the supervisor's state file nor take the measurement child's
+    exit path (which skips rocprofv3's output at exit)."""
+    monkeypatch.setenv(bench.STATE_ENV, "/tmp/state.json")
+    monkeypatch.setenv("TORCHELASTIC_RUN_ID", "x")
+    env = bench.probe_env(WORLD_SIZE="1")
+    assert bench.STATE_ENV not in env and "TORCHELASTIC_RUN_ID" not in env
+    assert env["WORLD_SIZE"] == "1"

@@ -300,16 +300,15 @@ def test_archive_read_reconstructs_corrupt_segments(ctx, bfrs, tmp_path):
     assert np.array_equal(_read(os.path.join(b0, "segment_4.dat")), d[4 * SEG:5 * SEG])
 
 
-@pytest.mark.parametrize("depth,workers,cache", [(1, 1, 2), (16, 2, 64), (64, 4, 8)])
-def test_archive_read_prefetch_settings(ctx, bfrs, tmp_path, monkeypatch, depth, workers, cache):
-    """BFRS_PREFETCH_DEPTH / BFRS_PREFETCH_WORKERS (read at open; the depth is
-    capped at half the cache): every setting serves the original bytes of an
-    archive with damaged segments in two blocks, in FUSE-sized requests."""
+@pytest.mark.parametrize("depth,cache", [(1, 2), (16, 64), (64, 8)])
+def test_archive_read_prefetch_settings(ctx, bfrs, tmp_path, monkeypatch, depth, cache):
+    """BFRS_PREFETCH_DEPTH (read at open; capped at half the cache): every
+    setting serves the original bytes of an archive with damaged segments in
+    two blocks, in FUSE-sized requests."""
     adir, d = _tier3(ctx, bfrs, tmp_path)
     _flip(os.path.join(adir, "blocks", "block_0", "segments", "segment_7.dat"), 9)
     _flip(os.path.join(adir, "blocks", "block_1", "segments", "segment_29.dat"), 5)
     monkeypatch.setenv("BFRS_PREFETCH_DEPTH", str(depth))
-    monkeypatch.setenv("BFRS_PREFETCH_WORKERS", str(workers))
     with bfrs.Archive(ctx, adir, cache_segments=cache, write_back=False) as a:
         out = np.empty(d.size, np.uint8)
         step = 128 << 10

@@ -82,7 +82,11 @@ def test_bench_launcher_two_ranks_stub():
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--stub",
+    # --stub-legs-builtin: bench.py's own stand-ins run the legs, so rank 0's
+    # c4_one_process leg runs too (c4_strong and its
+    # pcie_inclusive_one_process print under the supervisor split at N > 1:
+    # launcher -> one supervisor per rank -> one measurement child per rank)
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--stub-legs-builtin",
            "--segments", "8", "--segment-bytes", "65536", "--steps", "3", "--warmup", "1",
            "--settle-ms", "5", "--c4-segments", "40"]
     env = dict(os.environ)
@@ -100,6 +104,9 @@ def test_bench_launcher_two_ranks_stub():
     c4 = line["c4_strong"]
     assert c4["scaling"] == "strong" and c4["stripe_bytes_per_gpu"] == 32768
     assert c4["blocks"] == [30, 10]
+    assert c4["pcie_inclusive_one_process"] == {"match": True, "contexts": 2, "stub": True}
+    pc = line["parity_check"]
+    assert pc["all_ok"] and "c4_one_process" in pc["expected"] and "aborted" not in pc
 
 
 def test_bench_refuses_mismatched_world(monkeypatch):
