@@ -348,6 +348,7 @@ int Commit::tier3(std::string *out_dir) {
     *shard = std::min(S, m.n - *s0 * S);  // the block's first segment is its longest
   };
   std::atomic<bool> write_ok{true};
+  std::atomic<bool> stop{false};  // a failed context stops the others before their next block
   // The pipeline of one context over its blocks `mine` (in file order): its
   // own staging arenas, stream, filler and writers; `thr` host threads for
   // the copies.  Every result lands in a per-block slot (seg_cvs ranges,
@@ -446,6 +447,7 @@ int Commit::tier3(std::string *out_dir) {
     fill(0);
     BgTask writer[2];  // after the lambdas: joined first on every exit path
     for (size_t i = 0; i < mine.size() && rc == BFRS_OK; ++i) {
+      if (stop.load(std::memory_order_relaxed)) break;  // another context failed
       // arena[(i+1) % 2] was last used by block i-1's GPU work, which is done
       BgTask filler;
       if (i + 1 < mine.size()) filler.start([&fill, i] { fill(i + 1); });
@@ -471,7 +473,10 @@ int Commit::tier3(std::string *out_dir) {
     } catch (const std::exception &e) {
       rcs[d] = set_error(BFRS_E_WRAPPER, std::string("internal error: ") + e.what());
     }
-    if (rcs[d]) errs[d] = bfrs_last_error();  // thread-local: carried back below
+    if (rcs[d]) {
+      errs[d] = bfrs_last_error();  // thread-local: carried back below
+      stop = true;
+    }
   };
   {
     std::vector<BgTask> others(n - 1);  // joined on every exit path
@@ -927,8 +932,11 @@ int bfrs_commit_multi(bfrs_ctx *const *ctxs, size_t n_ctx, const char *file_path
 namespace {
 // repair_blocked (health.rs:642-765), intended semantics, over the blocks
 // `mine` of a tier-3 archive on one context; counts land in *rep.
+// `stop`: set when another context's repair failed (repair_tier3); the
+// loop ends before its next block, so a failing call writes no more files
+// than the blocks already in progress.
 int repair_blocks(bfrs_ctx *ctx, const Geometry &g, const std::vector<size_t> &mine,
-                  bfrs_repair_report *rep) {
+                  bfrs_repair_report *rep, const std::atomic<bool> *stop = nullptr) {
   if (hipSetDevice(ctx->impl.device) != hipSuccess)
     return set_error(BFRS_E_HIP, "repair: hipSetDevice failed");
   StagingCache &sc = staging(ctx);
@@ -936,6 +944,7 @@ int repair_blocks(bfrs_ctx *ctx, const Geometry &g, const std::vector<size_t> &m
   Arena &a = sc.a[0];
   int rc;
   for (const size_t b : mine) {
+    if (stop && stop->load(std::memory_order_relaxed)) break;
     BlockState bs;
     if ((rc = load_block(ctx, g, b, a, &bs))) return rc;
     ++rep->blocks_checked;
@@ -977,15 +986,19 @@ int repair_tier3(const std::vector<bfrs_ctx *> &ctxs, const Geometry &g, bfrs_re
   std::vector<bfrs_repair_report> reps(n, bfrs_repair_report{});
   std::vector<int> rcs(n, BFRS_OK);
   std::vector<std::string> errs(n);
+  std::atomic<bool> stop{false};  // a failed context stops the others' next block
   auto run = [&](size_t d) {
     try {
-      rcs[d] = repair_blocks(ctxs[d], g, mine[d], &reps[d]);
+      rcs[d] = repair_blocks(ctxs[d], g, mine[d], &reps[d], &stop);
     } catch (const std::bad_alloc &) {
       rcs[d] = set_error(BFRS_E_NOMEM, "host memory allocation failed");
     } catch (const std::exception &e) {
       rcs[d] = set_error(BFRS_E_WRAPPER, std::string("internal error: ") + e.what());
     }
-    if (rcs[d]) errs[d] = bfrs_last_error();
+    if (rcs[d]) {
+      errs[d] = bfrs_last_error();
+      stop = true;
+    }
   };
   {
     std::vector<BgTask> others(n - 1);  // joined on every exit path

@@ -314,12 +314,39 @@ struct SlabH2D {
   static void row_done(void *p, size_t i) {
     auto *h = static_cast<SlabH2D *>(p);
     const size_t r = h->rows.empty() ? i : h->rows[i];
-    const hipError_t e = hipMemcpyAsync(h->obj->d_row(r) + h->off, h->obj->h_row(r) + h->off,
-                                        h->len, hipMemcpyHostToDevice, h->st);
+    // a host_copy helper thread: make the pool's device current on it, so
+    // the copy never depends on which device the thread last used
+    hipError_t e = hipSetDevice(h->obj->pool->device);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(h->obj->d_row(r) + h->off, h->obj->h_row(r) + h->off, h->len,
+                         hipMemcpyHostToDevice, h->st);
     int expect = 0;
     if (e != hipSuccess && h->err_.compare_exchange_strong(expect, 1)) h->err = e;
   }
 };
+
+// Every exit of a slab wrapper, an error included: the slot's events cover
+// all the work it queued on both streams, so release() and the slot's next
+// user wait for it (an early return used to leave slab copies and
+// kernels in flight behind events of an earlier call).
+struct SlabFence {
+  CodecSlot &sl;
+  hipStream_t st, ax;
+  ~SlabFence() {
+    (void)hipEventRecord(sl.ev_h2d, st);
+    (void)hipEventRecord(sl.ev_d2h, ax);
+  }
+};
+
+// Measurement build only (knobs.hpp): BFRS_FAIL_SLAB=q fails a slab wrapper
+// after it queued slab q, read on every call (tests/test_gpu_parity.py: a
+// failed call leaves its slot safe to reuse).
+int injected_slab_failure(size_t q) {
+  const char *e = BFRS_AB_KNOB("BFRS_FAIL_SLAB");
+  if (e && *e && std::strtol(e, nullptr, 10) == long(q))
+    return set_error(BFRS_E_HIP, "injected slab failure (BFRS_FAIL_SLAB)");
+  return BFRS_OK;
+}
 
 struct EventList {
   std::vector<hipEvent_t> v;
@@ -347,6 +374,7 @@ int bfrs::encoder_encode_slabs(bfrs_encoder *e, const uint8_t *const *segs, cons
   CodecSlot &sl = *e->slot;
   if (!sl.aux) HIP_TRY(hipStreamCreateWithFlags(&sl.aux, hipStreamNonBlocking));
   hipStream_t st = sl.stream, ax = sl.aux;
+  SlabFence fence{sl, st, ax};
   const std::vector<size_t> off = slab_offsets(S);
   const size_t nslab = off.size() - 1;
   EventList ev;
@@ -378,9 +406,8 @@ int bfrs::encoder_encode_slabs(bfrs_encoder *e, const uint8_t *const *segs, cons
       HIP_TRY(hipMemcpyAsync(e->h_row(k + j) + o, e->d_row(k + j) + o, len,
                              hipMemcpyDeviceToHost, ax));
     if ((rc = ev.add(ax, &done[q]))) return rc;
+    if ((rc = injected_slab_failure(q))) return rc;
   }
-  HIP_TRY(hipEventRecord(sl.ev_h2d, st));
-  HIP_TRY(hipEventRecord(sl.ev_d2h, ax));
   // the caller's fresh outputs fault in while the last slabs transfer, 4
   // threads per output (from the start of the call, beside the input copies,
   // they cost more: r04n; 1 thread per output: r04v)
@@ -605,6 +632,7 @@ int bfrs::decoder_restore_slabs(bfrs_decoder *d, const uint8_t *const *segs,
   CodecSlot &sl = *d->slot;
   if (!sl.aux) HIP_TRY(hipStreamCreateWithFlags(&sl.aux, hipStreamNonBlocking));
   hipStream_t st = sl.stream, ax = sl.aux;
+  SlabFence fence{sl, st, ax};
   for (size_t i = 0; i < k; ++i) d->orig_present[i] = segs[i] != nullptr;
   for (size_t j = 0; j < m; ++j) d->rec_present[j] = par[j] != nullptr;
   const std::vector<size_t> off = slab_offsets(S);
@@ -642,9 +670,8 @@ int bfrs::decoder_restore_slabs(bfrs_decoder *d, const uint8_t *const *segs,
     HIP_TRY(hipMemcpyAsync(d->h_row(target) + o, d->d_row(target) + o, len, hipMemcpyDeviceToHost,
                            ax));
     if ((rc = ev.add(ax, &done[q]))) return rc;
+    if ((rc = injected_slab_failure(q))) return rc;
   }
-  HIP_TRY(hipEventRecord(sl.ev_h2d, st));
-  HIP_TRY(hipEventRecord(sl.ev_d2h, ax));
   if (prefault_outputs()) touch.start(outs, 1, S, prefault_parts(4));
   touch.join();
   for (size_t q = 0; q < nslab; ++q) {

@@ -200,6 +200,10 @@ void CodecPool::release(std::unique_ptr<CodecSlot> slot) {
   if (!slot) return;
   DeviceScope scope(device);  // a slot dropped below is freed on its own device
   (void)slot->sync();
+  // and whatever else the slot's own streams still hold (the slab wrappers'
+  // second stream): the next user must find the rows idle
+  if (slot->aux) (void)hipStreamSynchronize(slot->aux);
+  if (slot->own_stream && slot->stream) (void)hipStreamSynchronize(slot->stream);
   std::unique_ptr<CodecSlot> drop;  // freed after the lock is released
   {
     std::lock_guard<std::mutex> g(mu);

@@ -7,6 +7,10 @@ bfrs_decode_host_batch_multi spread a host-memory batch over several contexts
 file's blocks over them.  The boxes have one GPU, so the tests open two or
 three contexts on device 0: each has its own streams, HBM staging and host
 thread, which is the multi-device code path; only the device ordinal differs.
+Every test also has a "spread" form that puts context d on device
+d % device_count: it runs wherever two or more GPUs are visible
+and is skipped on the one-GPU boxes, so cross-device use stays untested until
+a multi-GPU box runs the suite (README).
 """
 import hashlib
 import json
@@ -19,9 +23,22 @@ import torch
 pytestmark = pytest.mark.gpu
 
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+PLACEMENTS = ["device0", "spread"]
 
 
-def test_config4_host_batch_multi_golden(bfrs):
+def _devices(bfrs, n, placement):
+    """Device of each of n contexts: all on device 0, or spread over the
+    visible GPUs (skipped with fewer than two)."""
+    if placement == "spread":
+        nd = bfrs.device_count()
+        if nd < 2:
+            pytest.skip("cross-device form: needs >= 2 visible GPUs (this box has one)")
+        return [d % nd for d in range(n)]
+    return [0] * n
+
+
+@pytest.mark.parametrize("placement", PLACEMENTS)
+def test_config4_host_batch_multi_golden(bfrs, placement):
     """BASELINE configs[3] (320 x 32 MiB = 10 x RS(30,3) + RS(20,3)) from
     pinned host memory through two contexts in this one process: parity equal
     to the golden digests of the unsplit oracle encode, and a 3-erasure decode
@@ -38,7 +55,7 @@ def test_config4_host_batch_multi_golden(bfrs):
         host[s].copy_(row)
     del row
     par = torch.full((3 * len(shapes), S), 0xA5, dtype=torch.uint8, pin_memory=True)
-    ctxs = [bfrs.Context(0), bfrs.Context(0)]
+    ctxs = [bfrs.Context(d) for d in _devices(bfrs, 2, placement)]
     try:
         bfrs.encode_host_batch_multi(ctxs, shapes, 3, S, [host[s] for s in range(nseg)],
                                      [par[i] for i in range(par.shape[0])])
@@ -66,14 +83,15 @@ def test_config4_host_batch_multi_golden(bfrs):
             c.close()
 
 
+@pytest.mark.parametrize("placement", PLACEMENTS)
 @pytest.mark.parametrize("n_ctx", [1, 2, 3, 5])
-def test_host_batch_multi_stripes_vs_oracle(bfrs, oracle, n_ctx):
+def test_host_batch_multi_stripes_vs_oracle(bfrs, oracle, n_ctx, placement):
     """Ragged shards (a tail chunk in the last stripe), more contexts than a
     narrow shard has chunks (idle contexts), mixed block sizes; every byte
     against the oracle."""
     rng = np.random.default_rng(n_ctx)
     ks = [30, 8, 1, 20]
-    ctxs = [bfrs.Context(0) for _ in range(n_ctx)]
+    ctxs = [bfrs.Context(d) for d in _devices(bfrs, n_ctx, placement)]
     try:
         for n in (64 * 3 + 38, 8192 * 5 + 64 * 7 + 2, (1 << 20) + 6):
             host = [[rng.integers(0, 256, n, dtype=np.uint8) for _ in range(k)] for k in ks]
@@ -126,12 +144,13 @@ def _tree(d):
     return out
 
 
+@pytest.mark.parametrize("placement", PLACEMENTS)
 @pytest.mark.parametrize("n_ctx,seg,size", [
     (2, 1 << 20, 200 * (1 << 20) + 12346),   # 7 blocks (last one 20 segments + a tail)
     (3, 1 << 20, 61 * (1 << 20)),            # 3 blocks, the last one segment
     (8, 64 << 10, 2 * 30 * (64 << 10)),      # more contexts than blocks
 ])
-def test_commit_multi_equals_commit(bfrs, tmp_path, n_ctx, seg, size):
+def test_commit_multi_equals_commit(bfrs, tmp_path, n_ctx, seg, size, placement):
     """bfrs_commit_multi over several contexts writes the same archive as
     bfrs_commit: every segment and parity file byte for byte, and the
     manifest except time_of_creation; the archive then reads back, checks
@@ -140,7 +159,7 @@ def test_commit_multi_equals_commit(bfrs, tmp_path, n_ctx, seg, size):
     src = tmp_path / "big.bin"
     src.write_bytes(synth.segment_np(7, 0, size).tobytes())
     one = bfrs.Context(0)
-    ctxs = [bfrs.Context(0) for _ in range(n_ctx)]
+    ctxs = [bfrs.Context(d) for d in _devices(bfrs, n_ctx, placement)]
     try:
         a = bfrs.commit(one, str(src), str(tmp_path / "single"), segment_size=seg, tier=3)
         b = bfrs.commit(ctxs, str(src), str(tmp_path / "multi"), segment_size=seg, tier=3)
