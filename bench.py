@@ -1651,7 +1651,7 @@ def per_launch_events(rt, encode, decode, stream, sh, steps, settle_ms=300.0):
         return {"error": f"{type(e).__name__}: {e}"}
 
 
-B3_PROBE_CALLS = 3
+B3_PROBE_CALLS = 10
 
 
 def blake3_trace_figures(live_trace, nbytes):

@@ -41,6 +41,12 @@ def main():
     ctx = bfrs.Context(0)
     stats = {"cases": 0, "bytes": 0, "by_api": {}, "failures": []}
     lock = threading.Lock()
+    # What every thread is running right now (case number, API, shape, start
+    # time): snapshotted at the first failure, so a sticky, asynchronously
+    # reported HIP error is recorded with everything that was in flight on
+    # the context when it surfaced (DESIGN.md §7c, round 4's fault)
+    inflight = {}
+    t_zero = time.perf_counter()
     stop = time.perf_counter() + a.seconds
 
     def one_block(rng):
@@ -83,6 +89,9 @@ def main():
                     rec_in[j][int(rng.integers(0, n))] ^= 0x5A  # corrupted, non-codeword input
                 orig_in = [None if i in er else data[i] for i in range(k)]
                 blocks.append((data, rec, orig_in, rec_in, er))
+            with lock:
+                inflight[tid] = {"case": stats["cases"], "api": api, "k": k, "m": m, "n": n,
+                                 "nblocks": nblocks, "t_s": round(time.perf_counter() - t_zero, 3)}
             try:
                 # encode check for every block, decode check (vs the oracle's decode of the
                 # same, possibly corrupted, inputs) for blocks with erasures
@@ -184,9 +193,15 @@ def main():
                 stats["cases"] += 1
                 stats["bytes"] += nblocks * (k + m) * n
                 stats["by_api"][api] = stats["by_api"].get(api, 0) + 1
+                if not ok and not stats["failures"]:
+                    stats["in_flight_at_first_failure"] = {
+                        "thread": tid, "t_s": round(time.perf_counter() - t_zero, 3),
+                        "threads": {str(t): dict(v) for t, v in sorted(inflight.items())}}
                 if not ok and len(stats["failures"]) < 20:
                     stats["failures"].append({"api": api, "k": k, "m": m, "n": n, "nblocks": nblocks,
-                                              "erasures": [b[4] for b in blocks], "error": err})
+                                              "erasures": [b[4] for b in blocks], "error": err,
+                                              "thread": tid})
+                inflight.pop(tid, None)
 
     th = [threading.Thread(target=worker, args=(t,)) for t in range(a.threads)]
     for t in th:
