@@ -958,10 +958,13 @@ def cpu_baseline(args, sets, info):
     }
 
 
-def pcie_link(S, k):
+def pcie_link(S, k, dec_in=None):
     """Host link rates on this box (torch copies of k x S bytes, best of 3) and
     the PCIe floor they put under one crate-shaped RS(k,3) block: encode moves
-    k shards in and 3 out, a one-target decode k shards in and 1 out."""
+    k shards in and 3 out; a one-target decode moves every present shard in
+    (`dec_in`, default k: the crate's decoder combines all the shards it was
+    given, so a bit-exact decode of possibly inconsistent inputs reads them
+    all; with one erasure that is k - 1 segments + 3 parity) and 1 out."""
     import numpy as np
     import torch
     n = k * S
@@ -988,7 +991,8 @@ def pcie_link(S, k):
     h2d = max(r["h2d_pageable_GBps"], r["h2d_pinned_GBps"]) * 1e9
     d2h = max(r["d2h_pageable_GBps"], r["d2h_pinned_GBps"]) * 1e9
     r["floor_generate_parity_ms"] = (k * S / h2d + 3 * S / d2h) * 1e3
-    r["floor_recover_one_target_ms"] = (k * S / h2d + S / d2h) * 1e3
+    r["floor_recover_one_target_ms"] = ((dec_in or k) * S / h2d + S / d2h) * 1e3
+    r["recover_shards_in"] = dec_in or k
     del dev, pageable, pinned
     return {key: (round(v, 2) if isinstance(v, float) else v) for key, v in r.items()}
 
@@ -1195,7 +1199,7 @@ def crate_api(ctx, sets, reps=7, staging_ab=True):
                                 "through ctypes, fresh output buffers, best of reps (median_ms "
                                 "beside it), wall clock, after 400 ms of untimed calls",
     }
-    res["link"] = pcie_link(S, k)
+    res["link"] = pcie_link(S, k, dec_in=sum(x is not None for x in slots) + len(par))
     lk = res["link"]
     ref = reference_copies(segs, S, reps)
     res["reference_copies"] = ref

@@ -197,3 +197,32 @@ def test_torchrun_rank_failure_ends_the_job():
     assert r.returncode != 0
     assert time.time() - t0 < 120
     assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+
+
+def test_torchrun_two_ranks_supervised_line():
+    """The driver's N>1 launch form (torch.distributed.run, world 2, gloo,
+    stubbed codec and legs): every rank process is a GPU-free supervisor of
+    its own measurement child (round 5); exactly one line reaches stdout,
+    with both ranks observed, c4_strong and its one-process figure."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(root, "bench.py"), "--gpus", "2", "--stub-legs-builtin", "--segments", "8",
+           "--segment-bytes", "65536", "--steps", "3", "--warmup", "1", "--settle-ms", "5",
+           "--c4-segments", "40"]
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["world_size_observed"] == 2
+    assert line["parity_check"]["all_ok"] and len(line["rank_ms_per_step"]) == 2
+    assert line["c4_strong"]["pcie_inclusive_one_process"]["match"] is True
