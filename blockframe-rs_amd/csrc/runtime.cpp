@@ -25,6 +25,72 @@ constexpr size_t kMaxOriginal = 1024;
 constexpr size_t kMaxRecovery = 1024;
 
 size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// One slab's piece of each row of a host batch: `len` bytes from src to dst.
+struct RowCopy {
+  uint8_t *dst;
+  const uint8_t *src;
+};
+
+// The HIP allocation holding host pointer p, if HIP knows it (pinned host
+// memory: hipHostMalloc'd or registered); false for pageable memory.
+bool pinned_range(const void *p, uintptr_t *lo, uintptr_t *hi) {
+  void *start = nullptr;
+  size_t size = 0;
+  if (hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR,
+                             reinterpret_cast<hipDeviceptr_t>(const_cast<void *>(p))) != hipSuccess ||
+      hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE,
+                             reinterpret_cast<hipDeviceptr_t>(const_cast<void *>(p))) != hipSuccess ||
+      !start || !size) {
+    (void)hipGetLastError();  // a pageable pointer is not an error here
+    return false;
+  }
+  *lo = reinterpret_cast<uintptr_t>(start);
+  *hi = *lo + size;
+  return true;
+}
+
+// Queues the row copies on `st`.  Consecutive rows whose source and
+// destination both advance by one constant pitch (>= len) go as ONE
+// hipMemcpy2DAsync when the host side of the whole run lies inside one
+// pinned allocation: the rows of a pinned tensor into the pipeline's device
+// rows `stride` apart.  With the D2H of the previous slab running beside it,
+// one 2-D copy of 30 rows moved 55.3 GB/s against 52.5 GB/s for 30 separate
+// copies (tools/copy2d_probe.py, profiles/r05/copy2d_r05.json; DESIGN.md
+// §7).  Pageable rows, and rows of different allocations, stay one copy each.
+int copy_rows(const std::vector<RowCopy> &rows, size_t len, hipMemcpyKind kind, hipStream_t st) {
+  auto at = [](const void *p) { return reinterpret_cast<uintptr_t>(p); };
+  auto host = [&](const RowCopy &r) {
+    return kind == hipMemcpyHostToDevice ? at(r.src) : at(r.dst);
+  };
+  size_t i = 0;
+  while (i < rows.size()) {
+    size_t j = i + 1;  // end of the run starting at row i
+    intptr_t dp = 0, sp = 0;
+    if (j < rows.size()) {
+      dp = intptr_t(at(rows[j].dst) - at(rows[i].dst));
+      sp = intptr_t(at(rows[j].src) - at(rows[i].src));
+      if (dp >= intptr_t(len) && sp >= intptr_t(len)) {
+        while (j + 1 < rows.size() && intptr_t(at(rows[j + 1].dst) - at(rows[j].dst)) == dp &&
+               intptr_t(at(rows[j + 1].src) - at(rows[j].src)) == sp)
+          ++j;
+        ++j;
+        uintptr_t lo = 0, hi = 0;
+        if (!pinned_range(reinterpret_cast<const void *>(host(rows[i])), &lo, &hi) ||
+            host(rows[i]) < lo || host(rows[j - 1]) + len > hi)
+          j = i + 1;  // not one pinned allocation: row by row
+      }
+    }
+    if (j - i == 1) {
+      HIP_TRY(hipMemcpyAsync(rows[i].dst, rows[i].src, len, kind, st));
+    } else {
+      HIP_TRY(hipMemcpy2DAsync(rows[i].dst, size_t(dp), rows[i].src, size_t(sp), len, j - i, kind,
+                               st));
+    }
+    i = j;
+  }
+  return BFRS_OK;
+}
 }  // namespace
 
 int set_error(int code, const std::string &msg) {
@@ -346,6 +412,7 @@ int Context::run_host(bool decode, size_t nblocks, const uint32_t *ks, size_t m,
   }
   int slot = 0;
   size_t oi = 0;
+  std::vector<RowCopy> h2d, d2h;
   for (size_t b = 0; b < nblocks; ++b) {
     const size_t k = ks[b];
     const uint8_t *const *bo = orig + oi;
@@ -359,32 +426,36 @@ int Context::run_host(bool decode, size_t nblocks, const uint32_t *ks, size_t m,
       uint8_t *base = static_cast<uint8_t *>(pipe_buf) + size_t(slot) * pipe_cap;
       std::vector<const uint8_t *> din(k, nullptr), drec(m, nullptr);
       std::vector<uint8_t *> dout(decode ? k : m, nullptr);
+      h2d.clear();
       for (size_t i = 0; i < k; ++i) {
         if (!bo[i]) {
           if (decode) dout[i] = base + i * stride;
           continue;
         }
         din[i] = base + i * stride;
-        HIP_TRY(hipMemcpyAsync(base + i * stride, bo[i] + off, len, hipMemcpyHostToDevice, st));
+        h2d.push_back({base + i * stride, bo[i] + off});
       }
       for (size_t j = 0; j < m; ++j) {
         uint8_t *d = base + (kmax + j) * stride;
         if (decode) {
           if (!br[j]) continue;
           drec[j] = d;
-          HIP_TRY(hipMemcpyAsync(d, br[j] + off, len, hipMemcpyHostToDevice, st));
+          h2d.push_back({d, br[j] + off});
         } else {
           dout[j] = d;
         }
       }
+      if (int rc = copy_rows(h2d, len, hipMemcpyHostToDevice, st)) return rc;
       uint32_t kk = uint32_t(k);
       bfrs_ctx *self = reinterpret_cast<bfrs_ctx *>(this);
       int rc = decode ? decode_batch_on(self, 1, &kk, m, len, din.data(), drec.data(),
                                         dout.data(), st)
                       : encode_batch_on(self, 1, &kk, m, len, din.data(), dout.data(), st);
       if (rc) return rc;
+      d2h.clear();
       for (size_t t = 0; t < dout.size(); ++t)
-        if (dout[t]) HIP_TRY(hipMemcpyAsync(bout[t] + off, dout[t], len, hipMemcpyDeviceToHost, st));
+        if (dout[t]) d2h.push_back({bout[t] + off, dout[t]});
+      if ((rc = copy_rows(d2h, len, hipMemcpyDeviceToHost, st))) return rc;
       slot = (slot + 1) % pipe_slots;
       off += len;
     }

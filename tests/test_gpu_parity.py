@@ -951,3 +951,56 @@ def test_failed_slab_call_leaves_its_slot_reusable():
     r = subprocess.run([sys.executable, "-c", _SLAB_FAILURE_SCRIPT], capture_output=True,
                        text=True, timeout=180, env=env)
     assert r.returncode == 0 and "reuse ok" in r.stdout, (r.stdout[-1000:], r.stderr[-2000:])
+
+
+@pytest.mark.parametrize("n", [64 * 150 + 38, (16 << 20) + 64 * 5 + 38])
+def test_host_batch_pinned_strided_rows_vs_oracle(ctx, oracle, n):
+    """Pinned shard rows at a constant pitch (one pinned tensor, as the bench
+    and config 4's host batches hand them over) go through the pipeline as
+    2-D row copies (runtime.cpp copy_rows): every parity byte against the
+    oracle, decodes whose erasures split the rows into runs, rows handed over
+    in reverse order (a negative pitch: row by row), and recovery rows of
+    another pinned tensor."""
+    rng = np.random.default_rng(77)
+    ks = [30, 8, 20]
+    nseg = sum(ks)
+    host = torch.empty(nseg, n, dtype=torch.uint8, pin_memory=True)
+    host.copy_(torch.from_numpy(rng.integers(0, 256, (nseg, n), dtype=np.uint8)))
+    par = torch.empty(3 * len(ks), n, dtype=torch.uint8, pin_memory=True)
+    rows = [host[s] for s in range(nseg)]
+    ctx.encode_host_batch(ks, 3, n, rows, [par[i] for i in range(par.shape[0])])
+    big = n > (1 << 20) and oracle.lib().oracle_have_avx2()
+    eng = oracle.ENGINE_AVX2 if big else oracle.ENGINE_SCALAR
+    blocks, off = [], 0
+    for k in ks:
+        blocks.append([host[off + i].numpy() for i in range(k)])
+        off += k
+    want = [oracle.encode(blk, 3, eng) for blk in blocks]
+    for b in range(len(ks)):
+        for j in range(3):
+            assert np.array_equal(par[3 * b + j].numpy(), want[b][j]), (n, b, j)
+    # reversed row order within each block: pitch -n, not merged
+    par2 = torch.zeros_like(par)
+    rev, off = [], 0
+    for k in ks:
+        rev += [host[off + i] for i in range(k)][::-1]
+        off += k
+    ctx.encode_host_batch(ks, 3, n, rev, [par2[i] for i in range(par2.shape[0])])
+    for b, blk in enumerate(blocks):
+        w = oracle.encode(blk[::-1], 3, eng)
+        for j in range(3):
+            assert np.array_equal(par2[3 * b + j].numpy(), w[j]), ("reversed", b, j)
+    # decodes: erasures in the middle and at the ends of each block
+    rest = torch.empty(3 * len(ks), n, dtype=torch.uint8, pin_memory=True)
+    orig, outs, want_rows, off = [], [], [], 0
+    for b, k in enumerate(ks):
+        er = [0, k // 2, k - 1]
+        for i in range(k):
+            orig.append(None if i in er else host[off + i])
+            outs.append(rest[3 * b + er.index(i)] if i in er else None)
+            if i in er:
+                want_rows.append((3 * b + er.index(i), off + i))
+        off += k
+    ctx.decode_host_batch(ks, 3, n, orig, [par[i] for i in range(par.shape[0])], outs)
+    for r, s in want_rows:
+        assert torch.equal(rest[r], host[s]), (n, r, s)
