@@ -1004,3 +1004,47 @@ def test_host_batch_pinned_strided_rows_vs_oracle(ctx, oracle, n):
     ctx.decode_host_batch(ks, 3, n, orig, [par[i] for i in range(par.shape[0])], outs)
     for r, s in want_rows:
         assert torch.equal(rest[r], host[s]), (n, r, s)
+
+
+@pytest.mark.parametrize("k", [30, 20, 8])
+def test_every_three_erasure_pattern(ctx, oracle, k):
+    """All C(k + 3, 3) ways to lose 3 of an RS(k,3) block's k + 3 shards (data
+    and parity alike; 5,456 for k = 30), for the three block shapes the
+    unrolled kernel has code for (a full block, config 4's last block of 20,
+    C2's last block of 8), decoded on the GPU in device batches of up to 496
+    blocks that share one set of shards: every restored data shard equals the
+    original (MDS decoding of a codeword is unique, so this is bit-exact with
+    the crate by construction).  The shard size is ragged (tail kernel
+    included)."""
+    import itertools
+    from math import comb
+    rng = np.random.default_rng(0x3E3 + k)
+    n = 64 * 70 + 38
+    data = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(k)]
+    par = oracle.encode(data, 3)
+    d_data = [torch.from_numpy(x).cuda() for x in data]
+    d_par = [torch.from_numpy(np.ascontiguousarray(p)).cuda() for p in par]
+    patterns = list(itertools.combinations(range(k + 3), 3))
+    checked = 0
+    for c0 in range(0, len(patterns), 496):
+        chunk = patterns[c0:c0 + 496]
+        orig, rec, outs, want = [], [], [], []
+        for er in chunk:
+            for i in range(k):
+                orig.append(None if i in er else d_data[i])
+            for j in range(3):
+                rec.append(None if k + j in er else d_par[j])
+            for i in range(k):
+                if i in er:
+                    outs.append(torch.empty(n, dtype=torch.uint8, device="cuda"))
+                    want.append(i)
+                else:
+                    outs.append(None)
+        ctx.decode_batch_dev([k] * len(chunk), 3, n, orig, rec, outs)
+        got = torch.stack([o for o in outs if o is not None])
+        ref = torch.stack([d_data[i] for i in want])
+        bad = (got != ref).any(dim=1).nonzero().flatten().tolist()
+        assert not bad, f"RS({k},3): {len(bad)} restored shards differ in patterns {c0}.."
+        checked += got.shape[0]
+    # patterns erasing e data shards (and 3 - e parity) restore e shards each
+    assert checked == sum(e * comb(k, e) * comb(3, 3 - e) for e in range(4))
