@@ -67,18 +67,17 @@ int copy_rows(const std::vector<RowCopy> &rows, size_t len, hipMemcpyKind kind, 
   while (i < rows.size()) {
     size_t j = i + 1;  // end of the run starting at row i
     intptr_t dp = 0, sp = 0;
+    uintptr_t lo = 0, hi = 0;
     if (j < rows.size()) {
       dp = intptr_t(at(rows[j].dst) - at(rows[i].dst));
       sp = intptr_t(at(rows[j].src) - at(rows[i].src));
-      if (dp >= intptr_t(len) && sp >= intptr_t(len)) {
-        while (j + 1 < rows.size() && intptr_t(at(rows[j + 1].dst) - at(rows[j].dst)) == dp &&
-               intptr_t(at(rows[j + 1].src) - at(rows[j].src)) == sp)
+      // a run: constant pitches, the host side inside row i's pinned allocation
+      if (dp >= intptr_t(len) && sp >= intptr_t(len) &&
+          pinned_range(reinterpret_cast<const void *>(host(rows[i])), &lo, &hi) &&
+          host(rows[i]) >= lo) {
+        while (j < rows.size() && intptr_t(at(rows[j].dst) - at(rows[j - 1].dst)) == dp &&
+               intptr_t(at(rows[j].src) - at(rows[j - 1].src)) == sp && host(rows[j]) + len <= hi)
           ++j;
-        ++j;
-        uintptr_t lo = 0, hi = 0;
-        if (!pinned_range(reinterpret_cast<const void *>(host(rows[i])), &lo, &hi) ||
-            host(rows[i]) < lo || host(rows[j - 1]) + len > hi)
-          j = i + 1;  // not one pinned allocation: row by row
       }
     }
     if (j - i == 1) {
