@@ -32,22 +32,29 @@ struct RowCopy {
   const uint8_t *src;
 };
 
-// The HIP allocation holding host pointer p, if HIP knows it (pinned host
-// memory: hipHostMalloc'd or registered); false for pageable memory.
+// The HIP allocation holding host pointer p, if it is pinned host memory
+// that the device sees at the same address (hipHostMalloc'd, as a pinned
+// tensor's storage), so its range is in host addresses; false for pageable
+// memory and for registered memory mapped elsewhere.
 bool pinned_range(const void *p, uintptr_t *lo, uintptr_t *hi) {
-  void *start = nullptr;
+  auto dp = reinterpret_cast<hipDeviceptr_t>(const_cast<void *>(p));
+  unsigned type = 0;
+  void *hostp = nullptr, *devp = nullptr, *start = nullptr;
   size_t size = 0;
-  if (hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR,
-                             reinterpret_cast<hipDeviceptr_t>(const_cast<void *>(p))) != hipSuccess ||
-      hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE,
-                             reinterpret_cast<hipDeviceptr_t>(const_cast<void *>(p))) != hipSuccess ||
+  if (hipPointerGetAttribute(&type, HIP_POINTER_ATTRIBUTE_MEMORY_TYPE, dp) != hipSuccess ||
+      type != unsigned(hipMemoryTypeHost) ||
+      hipPointerGetAttribute(&hostp, HIP_POINTER_ATTRIBUTE_HOST_POINTER, dp) != hipSuccess ||
+      hipPointerGetAttribute(&devp, HIP_POINTER_ATTRIBUTE_DEVICE_POINTER, dp) != hipSuccess ||
+      hostp != p || devp != p ||
+      hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, dp) != hipSuccess ||
+      hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, dp) != hipSuccess ||
       !start || !size) {
     (void)hipGetLastError();  // a pageable pointer is not an error here
     return false;
   }
   *lo = reinterpret_cast<uintptr_t>(start);
   *hi = *lo + size;
-  return true;
+  return *lo <= reinterpret_cast<uintptr_t>(p) && reinterpret_cast<uintptr_t>(p) < *hi;
 }
 
 // Queues the row copies on `st`.  Consecutive rows whose source and
