@@ -153,12 +153,35 @@ def main():
                     ks = [k] * nblocks
                     origs = [x for b in blocks for x in b[0]]
                     outs = [np.empty(n, np.uint8) for _ in range(m * nblocks)]
-                    ctx.encode_host_batch(ks, m, n, origs, outs)
-                    ok = all(np.array_equal(outs[b * m + j], blocks[b][1][j])
-                             for b in range(nblocks) for j in range(m))
                     oi = [x for b in blocks for x in b[2]]
                     ri = [x for b in blocks for x in b[3]]
                     ro = [np.empty(n, np.uint8) if x is None else None for x in oi]
+                    if rng.random() < 0.5:
+                        # rows of pinned tensors at a constant pitch: the 2-D row
+                        # copies of runtime.cpp copy_rows (outputs pinned too)
+                        pin = torch.empty(len(origs) + len(outs) + len(oi) + len(ri) + len(ro), n,
+                                          dtype=torch.uint8, pin_memory=True).numpy()
+                        r0 = 0
+
+                        def pinned(xs, fill=True):
+                            nonlocal r0
+                            out = []
+                            for x in xs:
+                                if x is None:
+                                    out.append(None)
+                                else:
+                                    if fill:
+                                        pin[r0][:] = x
+                                    out.append(pin[r0])
+                                r0 += 1
+                            return out
+                        origs = pinned(origs)
+                        outs = pinned(outs, fill=False)
+                        oi, ri = pinned(oi), pinned(ri)
+                        ro = pinned(ro, fill=False)
+                    ctx.encode_host_batch(ks, m, n, origs, outs)
+                    ok = all(np.array_equal(outs[b * m + j], blocks[b][1][j])
+                             for b in range(nblocks) for j in range(m))
                     ctx.decode_host_batch(ks, m, n, oi, ri, ro)
                     for b, blk in enumerate(blocks):
                         if blk[4]:
