@@ -1006,15 +1006,16 @@ def test_host_batch_pinned_strided_rows_vs_oracle(ctx, oracle, n):
         assert torch.equal(rest[r], host[s]), (n, r, s)
 
 
-@pytest.mark.parametrize("k", [30, 20, 8])
+@pytest.mark.parametrize("k", list(range(1, 31)))
 def test_every_three_erasure_pattern(ctx, oracle, k):
-    """All C(k + 3, 3) ways to lose 3 of an RS(k,3) block's k + 3 shards (data
-    and parity alike; 5,456 for k = 30), for the three block shapes the
-    unrolled kernel has code for (a full block, config 4's last block of 20,
-    C2's last block of 8), decoded on the GPU in device batches of up to 496
-    blocks that share one set of shards: every restored data shard equals the
-    original (MDS decoding of a codeword is unique, so this is bit-exact with
-    the crate by construction).  The shard size is ragged (tail kernel
+    """Every RS(k,3) shape a tier-3 block can have (k = 1..30: a full block or
+    any last block) and all C(k + 3, 3) ways to lose 3 of its k + 3 shards
+    (data and parity alike; 5,456 for k = 30, 46,375 in all), decoded on the
+    GPU in device batches of up to 496 blocks that share one set of shards:
+    every restored data shard equals the original (MDS decoding of a codeword
+    is unique, so this is bit-exact with the crate by construction).  k = 30,
+    20, 8 run the unrolled kernel, the others the looped subfield kernel;
+    k <= 2 and k = 4 take LowRate.  The shard size is ragged (tail kernel
     included)."""
     import itertools
     from math import comb
