@@ -1049,3 +1049,40 @@ def test_every_three_erasure_pattern(ctx, oracle, k):
         checked += got.shape[0]
     # patterns erasing e data shards (and 3 - e parity) restore e shards each
     assert checked == sum(e * comb(k, e) * comb(3, 3 - e) for e in range(4))
+
+
+@pytest.mark.parametrize("k", list(range(1, 31)))
+def test_inconsistent_inputs_follow_the_crates_decoder(ctx, oracle, k):
+    """Decodes whose inputs are NOT a codeword (one present recovery shard
+    corrupted): MDS uniqueness no longer fixes the output, so here the bytes
+    are the crate decoder's own linear map of every shard it was given.  For
+    every tier-3 block shape (k = 1..30) and 24 sampled erasure patterns (1-3
+    erased data shards, the rest of the recovery present, one of those
+    corrupted), one device batch per k against the oracle's restatement of
+    the crate's decoder, byte for byte."""
+    rng = np.random.default_rng(0xBAD0 + k)
+    n = 64 * 70 + 38
+    data = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(k)]
+    par = [np.ascontiguousarray(p) for p in oracle.encode(data, 3)]
+    cases = []
+    for _ in range(24):
+        e = int(rng.integers(1, min(3, k) + 1))
+        er = sorted(rng.choice(k, e, replace=False).tolist())
+        rec = [p.copy() for p in par]
+        # drop recovery shards beyond what the erasures need, keep >= 1 to corrupt
+        keep = sorted(rng.choice(3, int(rng.integers(e, 4)), replace=False).tolist())
+        rec = [rec[j] if j in keep else None for j in range(3)]
+        j = keep[int(rng.integers(0, len(keep)))]
+        rec[j][int(rng.integers(0, n))] ^= int(rng.integers(1, 256))
+        orig = [None if i in er else data[i] for i in range(k)]
+        cases.append((orig, rec, er))
+    d = lambda x: None if x is None else torch.from_numpy(np.ascontiguousarray(x)).cuda()
+    outs = [[torch.empty(n, dtype=torch.uint8, device="cuda") if o is None else None for o in orig]
+            for orig, _, _ in cases]
+    ctx.decode_batch_dev([k] * len(cases), 3, n, [d(x) for c in cases for x in c[0]],
+                         [d(x) for c in cases for x in c[1]], [o for oo in outs for o in oo])
+    torch.cuda.synchronize()
+    for (orig, rec, er), oo in zip(cases, outs):
+        want = oracle.decode(orig, rec)
+        for i in er:
+            assert np.array_equal(oo[i].cpu().numpy(), want[i]), (k, er, i)
