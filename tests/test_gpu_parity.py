@@ -1086,3 +1086,30 @@ def test_inconsistent_inputs_follow_the_crates_decoder(ctx, oracle, k):
         want = oracle.decode(orig, rec)
         for i in er:
             assert np.array_equal(oo[i].cpu().numpy(), want[i]), (k, er, i)
+
+
+@pytest.mark.parametrize("k", [30, 8, 1])
+def test_every_tail_length(ctx, oracle, k):
+    """Every even tail length the crate allows (shard_bytes % 64 = 2, 4, ...,
+    62) with whole chunks before it, in one device batch per k: encode against
+    the oracle, and a decode of min(3, k) erased data shards against the
+    originals.  The tail chunk's lo/hi split is the oracle's
+    reading; the kernel must agree at every length."""
+    rng = np.random.default_rng(0x7A11 + k)
+    sizes = [64 * 9 + t for t in range(2, 64, 2)]
+    for n in sizes:  # one launch per size (a batch shares its shard size)
+        data = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(k)]
+        d_data = [torch.from_numpy(x).cuda() for x in data]
+        d_rec = [torch.empty(n, dtype=torch.uint8, device="cuda") for _ in range(3)]
+        ctx.encode_batch_dev([k], 3, n, d_data, d_rec)
+        want = oracle.encode(data, 3)
+        for j in range(3):
+            assert np.array_equal(d_rec[j].cpu().numpy(), want[j]), (k, n, j)
+        er = list(range(min(3, k)))
+        outs = [torch.empty(n, dtype=torch.uint8, device="cuda") if i in er else None
+                for i in range(k)]
+        ctx.decode_batch_dev([k], 3, n, [None if i in er else d_data[i] for i in range(k)],
+                             d_rec, outs)
+        torch.cuda.synchronize()
+        for i in er:
+            assert torch.equal(outs[i], d_data[i]), (k, n, i)
