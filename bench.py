@@ -2306,7 +2306,10 @@ def main(argv=None):
             line.setdefault(key, None)
     refresh()
     emit(line)
-    rt.close()
+    if not STATE.path:
+        # (the measurement child leaves through os._exit right after its final
+        # line: no process-group teardown that could hang after the line)
+        rt.close()
     return 0 if line["parity_check"]["all_ok"] else 1
 
 

@@ -55,7 +55,7 @@ def main():
     print(json.dumps({
         "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) of the "
                   f"driver's bench command (python3 bench.py --gpus 1 --steps 20 --warmup 5), "
-                  f"{tag} (scripts/r0{tag[2]}_profile.sh)",
+                  f"{tag}",
         "round": tag, "box": box,
         "kernel": kernel.replace("void ", "").split("(bfrs::KernArgs)")[0],
         "grid": C2_GRID,
