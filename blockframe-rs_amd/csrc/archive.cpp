@@ -710,10 +710,10 @@ int bfrs_archive::load_clean(size_t gi, SegPtr *out, bool *ok) {
   auto seg = std::make_shared<Seg>(pool, buf, len);
   if (read_file_into(seg_path(gi), buf, pool->slot, 8) != (long long)len) return BFRS_OK;
   std::lock_guard<std::mutex> lg(gpu_mu);
+  Context &c = ctx->impl;
+  HIP_TRY(hipSetDevice(c.device));  // before the arena's HBM: a prefetch thread starts on device 0
   int rc = arena.reserve(pool->slot, kBlockSegments + kParity);
   if (rc) return rc;
-  Context &c = ctx->impl;
-  HIP_TRY(hipSetDevice(c.device));
   HIP_TRY(hipMemcpyAsync(arena.ds(0), buf, len, hipMemcpyHostToDevice, c.stream));
   std::vector<std::string> hex;
   if ((rc = gpu_hash_hex(ctx, {arena.ds(0)}, {len}, &hex))) return rc;

@@ -77,6 +77,10 @@ int load_block(bfrs_ctx *ctx, const Geometry &g, size_t b, Arena &a, BlockState 
   const size_t k = st->k, shard = st->shard;
   st->lens.resize(k);
   for (size_t s = 0; s < k; ++s) st->lens[s] = g.seg_len(b * kBlockSegments + s);
+  Context &c = ctx->impl;
+  // the arena's HBM must be on this context's device: the caller may be a
+  // read handle's prefetch thread or an API thread bound to another GPU
+  HIP_TRY(hipSetDevice(c.device));
   int rc = a.reserve(shard, k + kParity);
   if (rc) return rc;
   std::vector<uint8_t> readable(k + kParity, 0);
@@ -90,8 +94,6 @@ int load_block(bfrs_ctx *ctx, const Geometry &g, size_t b, Arena &a, BlockState 
       readable[i] = read_file_into(t3_par(g.dir, b, i - k), a.hs(i), a.slot) == (long long)shard;
     }
   });
-  Context &c = ctx->impl;
-  HIP_TRY(hipSetDevice(c.device));
   HIP_TRY(hipMemcpyAsync(a.d, a.h, a.slot * (k + kParity), hipMemcpyHostToDevice, c.stream));
   std::vector<const uint8_t *> msgs;
   std::vector<size_t> lens, idx;
