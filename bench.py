@@ -1885,8 +1885,8 @@ def run_c5(args, ctx=None):
         m = json.load(open(os.path.join(adir, "manifest.json")))
         want = m["original_hash"]
 
-        def sweep():
-            with bfrs.Archive(ctx, adir, cache_segments=64) as a:
+        def sweep(c):
+            with bfrs.Archive(c, adir, cache_segments=64) as a:
                 out = np.empty(n, np.uint8)
                 out[::4096] = 0  # fault the destination in before timing
                 rb = args.c5_read_bytes
@@ -1898,7 +1898,7 @@ def run_c5(args, ctx=None):
                     off += read(off, base + off, min(rb, n - off))
                 return time.perf_counter() - t, a.stats(), out
 
-        clean_s, clean_st, out = sweep()
+        clean_s, clean_st, out = sweep(ctx)
         clean_ok = bfrs.blake3_hex(out, threads=16) == want
         del out
         rng = np.random.default_rng(6)
@@ -1913,8 +1913,17 @@ def run_c5(args, ctx=None):
                     f.seek(-1, 1)
                     f.write(bytes([c[0] ^ 0xFF]))
                 damaged.append((int(b), s))
-        dirty_s, dirty_st, out = sweep()
+        dirty_s, dirty_st, out = sweep(ctx)
         ok = clean_ok and bfrs.blake3_hex(out, threads=16) == want
+        del out
+        # the same read on a context of its own: its segment pool is pinned
+        # during the read (the handles above share the first one's pool)
+        cold_ctx = bfrs.Context(ctx.device)
+        try:
+            cold_s, _, out = sweep(cold_ctx)
+        finally:
+            cold_ctx.close()
+        ok = ok and bfrs.blake3_hex(out, threads=16) == want
         del out
         res = {
             "metric": "MB/s end-to-end read of a corrupted tier-3 file (BASELINE configs[4])",
@@ -1924,6 +1933,11 @@ def run_c5(args, ctx=None):
             "bytes": n, "segment_bytes": args.segment_bytes, "read_bytes": args.c5_read_bytes,
             "blocks": len(m["merkle_tree"]["blocks"]), "damaged_segments": len(damaged),
             "clean_read_MBps": round(n / clean_s / 1e6, 1),
+            "corrupted_read_fresh_context_MBps": round(n / cold_s / 1e6, 1),
+            "handles": "clean sweep = the context's first read handle (pins the segment pool); "
+                       "value = a second handle on that context, as a long-lived mount serves "
+                       "its reads; corrupted_read_fresh_context_MBps = the value's read on a "
+                       "new context",
             "commit_MBps": round(n / commit_s / 1e6, 1),
             "stats_corrupted": dirty_st, "stats_clean": clean_st, "blake3_match": ok,
         }

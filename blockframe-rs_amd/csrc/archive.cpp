@@ -18,8 +18,10 @@
 #include <algorithm>
 #include <array>
 #include <atomic>
+#include <chrono>
 #include <cctype>
 #include <condition_variable>
+#include <cstdio>
 #include <cstring>
 #include <deque>
 #include <list>
@@ -560,6 +562,46 @@ struct PinnedPool {
   }
 };
 
+// The context's pool for buffers of `bytes` (StagingCache::seg_pools).
+std::shared_ptr<PinnedPool> segment_pool(bfrs_ctx *ctx, size_t bytes) {
+  StagingCache &sc = staging(ctx);
+  auto pool = std::make_shared<PinnedPool>(bytes);
+  std::lock_guard<std::mutex> l(sc.pools_mu);
+  std::shared_ptr<void> &slot = sc.seg_pools[pool->slot];
+  if (slot) return std::static_pointer_cast<PinnedPool>(slot);
+  slot = pool;
+  return pool;
+}
+
+// A clean segment's verification lane: one HBM segment buffer and a stream
+// of its own, so prefetch workers verify segments side by side and beside a
+// block reconstruction (which uses the handle's arena and the context's
+// stream); only the hash itself is serialised (the context's hash_mu).
+struct CleanLane {
+  std::mutex mu;
+  uint8_t *d = nullptr;
+  size_t cap = 0;
+  hipStream_t st = nullptr;
+  CleanLane() = default;
+  CleanLane(const CleanLane &) = delete;
+  CleanLane &operator=(const CleanLane &) = delete;
+  ~CleanLane() {
+    if (st) (void)hipStreamDestroy(st);
+    if (d) (void)hipFree(d);
+  }
+  int ready(size_t bytes) {  // under mu, on the context's device
+    if (!st) HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    if (d && cap >= bytes) return BFRS_OK;
+    if (d) {
+      HIP_TRY(hipFree(d));
+      d = nullptr;
+    }
+    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d), bytes));
+    cap = bytes;
+    return BFRS_OK;
+  }
+};
+
 struct Seg {
   uint8_t *p = nullptr;
   size_t n = 0;
@@ -570,6 +612,44 @@ struct Seg {
   }
 };
 using SegPtr = std::shared_ptr<Seg>;
+
+// Read-path timeline, measurement build only (BFRS_TRACE): what the reader
+// waits for and how long loads and block reconstructions take, one line on
+// stderr when the handle closes.  Off (one branch) in libbfrs.so.
+struct ReadTrace {
+  bool on = false;
+  std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+  std::mutex mu;
+  std::vector<std::string> events;
+  std::atomic<long long> reader_wait_ns{0}, reader_miss_ns{0}, gpu_lock_wait_ns{0},
+      clean_read_ns{0}, clean_gpu_ns{0}, rec_load_ns{0}, rec_restore_ns{0}, rec_copy_ns{0};
+  std::atomic<long long> reader_waits{0}, cleans{0};
+  long long ns() const {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0)
+        .count();
+  }
+  void event(const char *what, size_t gi, long long start, long long end) {
+    if (!on) return;
+    std::lock_guard<std::mutex> l(mu);
+    std::ostringstream os;
+    os << "[\"" << what << "\"," << gi << "," << start / 1000 << "," << (end - start) / 1000 << "]";
+    events.push_back(os.str());
+  }
+  void print() {
+    if (!on) return;
+    std::ostringstream os;
+    os << "bfrs_read_trace {\"reader_waits\":" << reader_waits << ",\"reader_wait_ms\":"
+       << reader_wait_ns / 1e6 << ",\"reader_miss_ms\":" << reader_miss_ns / 1e6
+       << ",\"cleans\":" << cleans << ",\"clean_read_ms\":" << clean_read_ns / 1e6
+       << ",\"clean_gpu_ms\":" << clean_gpu_ns / 1e6 << ",\"gpu_lock_wait_ms\":"
+       << gpu_lock_wait_ns / 1e6 << ",\"rec_load_ms\":" << rec_load_ns / 1e6
+       << ",\"rec_restore_ms\":" << rec_restore_ns / 1e6 << ",\"rec_copy_ms\":"
+       << rec_copy_ns / 1e6 << ",\"events_us\":[";
+    for (size_t i = 0; i < events.size(); ++i) os << (i ? "," : "") << events[i];
+    os << "]}\n";
+    std::fputs(os.str().c_str(), stderr);
+  }
+};
 
 }  // namespace
 
@@ -607,8 +687,28 @@ struct bfrs_archive {
   bool stop = false;
   std::vector<std::thread> workers;
 
-  std::mutex gpu_mu;  // the context and the arena (one user at a time)
+  std::mutex gpu_mu;  // the arena (block reconstructions, one at a time)
   Arena arena;
+  std::vector<std::unique_ptr<CleanLane>> lanes;  // clean-segment verification
+  ReadTrace trace;
+
+  bfrs_archive() { add_lanes(1); }
+  void add_lanes(size_t n) {
+    for (size_t i = 0; i < n; ++i) lanes.emplace_back(new CleanLane);
+  }
+  // a free lane, else the lane for gi (blocking); lanes are never resized
+  // once prefetch workers run
+  std::unique_lock<std::mutex> take_lane(size_t gi, CleanLane **out) {
+    for (auto &ln : lanes) {
+      std::unique_lock<std::mutex> l(ln->mu, std::try_to_lock);
+      if (l.owns_lock()) {
+        *out = ln.get();
+        return l;
+      }
+    }
+    *out = lanes[gi % lanes.size()].get();
+    return std::unique_lock<std::mutex>((*out)->mu);
+  }
 
   ~bfrs_archive() {
     {
@@ -619,6 +719,7 @@ struct bfrs_archive {
     for (auto &w : workers)
       if (w.joinable()) w.join();
     cache.clear();
+    trace.print();
   }
 
   SegPtr lookup(size_t gi) {  // under mu
@@ -651,7 +752,7 @@ struct bfrs_archive {
   // nobody to catch it).  *verified: the file was clean; *restored: rebuilt.
   int load_inflight(std::unique_lock<std::mutex> &l, size_t gi, SegPtr *seg, bool *verified,
                     bool *restored);
-  void prefetch_loop();
+  void prefetch_loop(size_t worker);
 };
 
 int bfrs_archive::load_inflight(std::unique_lock<std::mutex> &l, size_t gi, SegPtr *seg,
@@ -708,15 +809,34 @@ int bfrs_archive::load_clean(size_t gi, SegPtr *out, bool *ok) {
   uint8_t *buf = pool->get();
   if (!buf) return set_error(BFRS_E_NOMEM, "pinned segment buffer allocation failed");
   auto seg = std::make_shared<Seg>(pool, buf, len);
+  const long long t_read = trace.on ? trace.ns() : 0;
   if (read_file_into(seg_path(gi), buf, pool->slot, 8) != (long long)len) return BFRS_OK;
-  std::lock_guard<std::mutex> lg(gpu_mu);
+  const long long t_lock = trace.on ? trace.ns() : 0;
+  CleanLane *ln = nullptr;
+  std::unique_lock<std::mutex> lane_lock = take_lane(gi, &ln);
+  const long long t_gpu = trace.on ? trace.ns() : 0;
+  struct Done {  // trace only
+    bfrs_archive *a;
+    size_t gi;
+    long long t_read, t_lock, t_gpu;
+    ~Done() {
+      if (!a->trace.on) return;
+      const long long t_end = a->trace.ns();
+      a->trace.clean_read_ns += t_lock - t_read;
+      a->trace.gpu_lock_wait_ns += t_gpu - t_lock;
+      a->trace.clean_gpu_ns += t_end - t_gpu;
+      ++a->trace.cleans;
+      a->trace.event("clean", gi, t_read, t_end);
+    }
+  } done{this, gi, t_read, t_lock, t_gpu};
   Context &c = ctx->impl;
-  HIP_TRY(hipSetDevice(c.device));  // before the arena's HBM: a prefetch thread starts on device 0
-  int rc = arena.reserve(pool->slot, kBlockSegments + kParity);
+  HIP_TRY(hipSetDevice(c.device));  // before the lane's HBM: a prefetch thread starts on device 0
+  int rc = ln->ready(pool->slot);
   if (rc) return rc;
-  HIP_TRY(hipMemcpyAsync(arena.ds(0), buf, len, hipMemcpyHostToDevice, c.stream));
+  HIP_TRY(hipMemcpyAsync(ln->d, buf, len, hipMemcpyHostToDevice, ln->st));
+  HIP_TRY(hipStreamSynchronize(ln->st));  // before the hash takes hash_mu
   std::vector<std::string> hex;
-  if ((rc = gpu_hash_hex(ctx, {arena.ds(0)}, {len}, &hex))) return rc;
+  if ((rc = gpu_hash_hex(ctx, {ln->d}, {len}, &hex, nullptr, nullptr, ln->st))) return rc;
   if (hex[0] == expected_hash(gi)) {
     *ok = true;
     *out = std::move(seg);
@@ -731,7 +851,10 @@ int bfrs_archive::recover(size_t gi, SegPtr *out) {
   if (mf.tier == 3) {
     std::vector<std::pair<size_t, SegPtr>> restored;
     {
+      const long long t_lock = trace.on ? trace.ns() : 0;
       std::lock_guard<std::mutex> lg(gpu_mu);
+      const long long t_gpu = trace.on ? trace.ns() : 0;
+      if (trace.on) trace.gpu_lock_wait_ns += t_gpu - t_lock;
       {  // another thread's reconstruction of this block may have restored it meanwhile
         std::lock_guard<std::mutex> l(mu);
         if (SegPtr c = lookup(gi)) {
@@ -743,9 +866,10 @@ int bfrs_archive::recover(size_t gi, SegPtr *out) {
       BlockState bs;
       int rc = load_block(ctx, g, b, arena, &bs);
       if (rc) return rc;
+      const long long t_loaded = trace.on ? trace.ns() : 0;
       const std::vector<uint8_t> was_ok = bs.seg_ok;
-      rc = restore_block(ctx, g, arena, bs);
-      if (rc < 0) return rc;
+      // the restored segments go from HBM straight into their cache buffers
+      std::vector<uint8_t *> dst(bs.k, nullptr);
       for (size_t s = 0; s < bs.k; ++s) {
         const bool need = !was_ok[s] || b * kBlockSegments + s == gi;
         if (!need) continue;
@@ -753,9 +877,25 @@ int bfrs_archive::recover(size_t gi, SegPtr *out) {
         if (!buf) return set_error(BFRS_E_NOMEM, "pinned segment buffer allocation failed");
         // owned by a Seg before anything can fail, so every path returns it to the pool
         restored.emplace_back(b * kBlockSegments + s, std::make_shared<Seg>(pool, buf, bs.lens[s]));
-        std::memcpy(buf, arena.hs(s), bs.lens[s]);
-        if (!was_ok[s] && write_back && !write_file(t3_seg(g.dir, b, s), buf, bs.lens[s]))
+        dst[s] = buf;
+      }
+      rc = restore_block(ctx, g, arena, bs, &dst);
+      if (rc < 0) return rc;
+      const long long t_restored = trace.on ? trace.ns() : 0;
+      for (auto &r : restored) {
+        const size_t s = r.first - b * kBlockSegments;
+        if (was_ok[s]) {  // the target itself was clean (another reader's view was stale)
+          std::memcpy(r.second->p, arena.hs(s), bs.lens[s]);
+        } else if (write_back && !write_file(t3_seg(g.dir, b, s), r.second->p, bs.lens[s])) {
           return io_error("write back segment");
+        }
+      }
+      if (trace.on) {
+        const long long t_end = trace.ns();
+        trace.rec_load_ns += t_loaded - t_gpu;
+        trace.rec_restore_ns += t_restored - t_loaded;
+        trace.rec_copy_ns += t_end - t_restored;
+        trace.event("recover", gi, t_gpu, t_end);
       }
       std::lock_guard<std::mutex> l(mu);
       ++st.recoveries;
@@ -798,7 +938,15 @@ int bfrs_archive::recover(size_t gi, SegPtr *out) {
   return BFRS_OK;
 }
 
-void bfrs_archive::prefetch_loop() {
+void bfrs_archive::prefetch_loop(size_t worker) {
+  if (worker == 0 && g.mf.tier == 3) {
+    // the block arena (~1.1 GiB pinned + HBM at 32 MiB segments), allocated
+    // here rather than when the first damaged block is found and the reader
+    // is about to need it; a failure is left to that reconstruction
+    std::lock_guard<std::mutex> lg(gpu_mu);
+    if (hipSetDevice(ctx->impl.device) == hipSuccess)
+      (void)arena.reserve(pool->slot, kBlockSegments + kParity);
+  }
   std::unique_lock<std::mutex> l(mu);
   for (;;) {
     cv.wait(l, [&] { return stop || !wantq.empty(); });
@@ -1038,7 +1186,7 @@ int repair_impl(const std::vector<bfrs_ctx *> &ctxs, const char *archive_dir,
   a.ctx = ctx;
   a.g = g;
   a.write_back = true;
-  a.pool = std::make_shared<PinnedPool>(g.S);
+  a.pool = segment_pool(ctx, g.S);
   for (size_t i = 0; i < g.nseg; ++i) {
     ++report->segments_checked;
     ++report->blocks_checked;
@@ -1155,7 +1303,7 @@ int health_report(bfrs_ctx *ctx, const char *archive_dir, Json *out) {
     bfrs_archive ar;
     ar.ctx = ctx;
     ar.g = g;
-    ar.pool = std::make_shared<PinnedPool>(g.S);
+    ar.pool = segment_pool(ctx, g.S);
     for (size_t i = 0; i < g.nseg; ++i) {
       SegPtr v;
       bool ok = false;
@@ -1362,16 +1510,18 @@ int bfrs_archive_open(bfrs_ctx *ctx, const char *archive_dir, size_t cache_segme
   a->write_back = write_back != 0;
   int rc = load_geometry(archive_dir, &a->g);
   if (rc) return rc;
-  a->pool = std::make_shared<PinnedPool>(a->g.S);
+  a->pool = segment_pool(ctx, a->g.S);
+  a->trace.on = BFRS_AB_KNOB("BFRS_TRACE") != nullptr;
   if (const char *e = std::getenv("BFRS_PREFETCH_DEPTH"))
     a->prefetch_depth = size_t(std::clamp(std::strtol(e, nullptr, 10), 1L, 256L));
   if (const char *e = BFRS_AB_KNOB("BFRS_PREFETCH_WORKERS"))
     a->prefetch_workers = size_t(std::clamp(std::strtol(e, nullptr, 10), 1L, 16L));
   a->prefetch = a->g.nseg > 1;
+  if (a->prefetch) a->add_lanes(a->prefetch_workers);  // one per worker + the reader's
   if (a->prefetch) {
     try {
       for (size_t w = 0; w < a->prefetch_workers; ++w)
-        a->workers.emplace_back(&bfrs_archive::prefetch_loop, a.get());
+        a->workers.emplace_back(&bfrs_archive::prefetch_loop, a.get(), w);
     } catch (const std::system_error &) {  // no thread: fewer prefetch workers, or none
     }
     a->prefetch = !a->workers.empty();
@@ -1422,14 +1572,27 @@ int bfrs_archive_read(bfrs_archive *a, uint64_t offset, size_t len, uint8_t *out
     if (seg) {
       ++a->st.hits;
     } else if (a->inflight.count(gi)) {  // a prefetch worker or another reader is loading it
+      const long long t = a->trace.on ? a->trace.ns() : 0;
       a->cv.wait(l, [&] { return !a->inflight.count(gi); });
+      if (a->trace.on) {
+        const long long e = a->trace.ns();
+        a->trace.reader_wait_ns += e - t;
+        ++a->trace.reader_waits;
+        a->trace.event("reader_wait", gi, t, e);
+      }
       continue;
     } else {
       ++a->st.misses;
       // queued but not started: load it here instead
       a->wantq.erase(std::remove(a->wantq.begin(), a->wantq.end(), gi), a->wantq.end());
       bool ok = false, restored = false;
+      const long long t = a->trace.on ? a->trace.ns() : 0;
       const int rc = a->load_inflight(l, gi, &seg, &ok, &restored);
+      if (a->trace.on) {
+        const long long e = a->trace.ns();
+        a->trace.reader_miss_ns += e - t;
+        a->trace.event("reader_miss", gi, t, e);
+      }
       if (rc) return rc;
       if (ok) ++a->st.verified;
       a->put(gi, seg);
@@ -1449,7 +1612,11 @@ int bfrs_archive_read(bfrs_archive *a, uint64_t offset, size_t len, uint8_t *out
     }
     if (in_seg >= seg->n) return set_error(BFRS_E_WRAPPER, "segment shorter than manifest size");
     const size_t n = std::min(len - *nread, seg->n - in_seg);
+    // the copy runs unlocked (seg keeps the buffer alive): a reader that held
+    // mu through its copies starved the prefetch workers of it
+    l.unlock();
     std::memcpy(out + *nread, seg->p + in_seg, n);
+    l.lock();
     *nread += n;
   }
   a->st.bytes_served += *nread;

@@ -4,6 +4,7 @@
 #include "blake3.hpp"
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <sstream>
 
@@ -43,12 +44,12 @@ StagingCache &staging(bfrs_ctx *ctx) {
 
 int gpu_hash_hex(bfrs_ctx *ctx, const std::vector<const uint8_t *> &d_msgs,
                  const std::vector<size_t> &lens, std::vector<std::string> *hex,
-                 const uint64_t *chunk_offsets, std::vector<uint8_t> *cvs) {
+                 const uint64_t *chunk_offsets, std::vector<uint8_t> *cvs, hipStream_t stream) {
   const size_t n = d_msgs.size();
   std::vector<uint8_t> dig(n * 32);
   if (cvs) cvs->assign(n * 32, 0);
   int rc = ctx->impl.blake3_dev(n, d_msgs.data(), lens.data(), chunk_offsets, dig.data(),
-                                cvs ? cvs->data() : nullptr, ctx->impl.stream);
+                                cvs ? cvs->data() : nullptr, stream ? stream : ctx->impl.stream);
   if (rc) return rc;
   hex->resize(n);
   for (size_t i = 0; i < n; ++i) (*hex)[i] = to_hex(dig.data() + 32 * i, 32);
@@ -84,6 +85,7 @@ int load_block(bfrs_ctx *ctx, const Geometry &g, size_t b, Arena &a, BlockState 
   int rc = a.reserve(shard, k + kParity);
   if (rc) return rc;
   std::vector<uint8_t> readable(k + kParity, 0);
+  std::atomic<int> hip_rc{int(hipSuccess)};
   parallel_for(k + kParity, hw_threads(), [&](size_t i) {
     if (i < k) {
       const long long n = read_file_into(t3_seg(g.dir, b, i), a.hs(i), a.slot);
@@ -93,8 +95,18 @@ int load_block(bfrs_ctx *ctx, const Geometry &g, size_t b, Arena &a, BlockState 
     } else {
       readable[i] = read_file_into(t3_par(g.dir, b, i - k), a.hs(i), a.slot) == (long long)shard;
     }
+    if (!readable[i]) return;  // excluded from the hash and the decode: no copy
+    // this shard's H2D now, while the other files are still being read
+    hipError_t e = hipSetDevice(c.device);
+    if (e == hipSuccess) e = hipMemcpyAsync(a.ds(i), a.hs(i), shard, hipMemcpyHostToDevice, c.stream);
+    int ok = int(hipSuccess);
+    if (e != hipSuccess) hip_rc.compare_exchange_strong(ok, int(e));
   });
-  HIP_TRY(hipMemcpyAsync(a.d, a.h, a.slot * (k + kParity), hipMemcpyHostToDevice, c.stream));
+  if (hip_rc.load() != int(hipSuccess)) {
+    (void)hipStreamSynchronize(c.stream);
+    return hip_error(hipError_t(hip_rc.load()), "hipMemcpyAsync (block shard H2D)");
+  }
+  HIP_TRY(hipStreamSynchronize(c.stream));  // the copies land before the hash takes hash_mu
   std::vector<const uint8_t *> msgs;
   std::vector<size_t> lens, idx;
   for (size_t i = 0; i < k + kParity; ++i)
@@ -117,7 +129,8 @@ int load_block(bfrs_ctx *ctx, const Geometry &g, size_t b, Arena &a, BlockState 
   return BFRS_OK;
 }
 
-int restore_block(bfrs_ctx *ctx, const Geometry &g, Arena &a, BlockState &st) {
+int restore_block(bfrs_ctx *ctx, const Geometry &g, Arena &a, BlockState &st,
+                  const std::vector<uint8_t *> *host_out) {
   const size_t k = st.k, erased = st.damaged_segments(), present = st.valid_parity();
   if (erased == 0) return 0;
   if (erased > present) {
@@ -156,8 +169,11 @@ int restore_block(bfrs_ctx *ctx, const Geometry &g, Arena &a, BlockState &st) {
       os << "block " << st.b << " segment " << idx[j] << ": restored bytes fail the manifest hash";
       return set_error(BFRS_E_WRAPPER, os.str());
     }
-  for (size_t s : idx)
-    HIP_TRY(hipMemcpyAsync(a.hs(s), a.ds(s), st.shard, hipMemcpyDeviceToHost, c.stream));
+  for (size_t s : idx) {
+    uint8_t *dst = host_out ? (*host_out)[s] : nullptr;
+    HIP_TRY(hipMemcpyAsync(dst ? dst : a.hs(s), a.ds(s), dst ? st.lens[s] : st.shard,
+                           hipMemcpyDeviceToHost, c.stream));
+  }
   HIP_TRY(hipStreamSynchronize(c.stream));
   for (size_t s : idx) st.seg_ok[s] = 1;
   return int(idx.size());

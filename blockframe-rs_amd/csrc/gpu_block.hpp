@@ -12,6 +12,8 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -34,10 +36,13 @@ struct Arena {
   uint8_t *ds(size_t i) const { return d + i * slot; }
 };
 
-// Device BLAKE3 -> lowercase hex digests (ctx stream; synchronises).
+// Device BLAKE3 -> lowercase hex digests (on `stream`, default the context's;
+// synchronises it).  The context's hash_mu is held throughout, so callers
+// synchronise their own copies first rather than make it wait behind them.
 int gpu_hash_hex(bfrs_ctx *ctx, const std::vector<const uint8_t *> &d_msgs,
                  const std::vector<size_t> &lens, std::vector<std::string> *hex,
-                 const uint64_t *chunk_offsets = nullptr, std::vector<uint8_t> *cvs = nullptr);
+                 const uint64_t *chunk_offsets = nullptr, std::vector<uint8_t> *cvs = nullptr,
+                 hipStream_t stream = nullptr);
 
 // The context's staging arenas (Context::staging): archive calls on one
 // context take `mu` for their duration and use a[0..1] as block arenas and
@@ -45,6 +50,12 @@ int gpu_hash_hex(bfrs_ctx *ctx, const std::vector<const uint8_t *> &d_msgs,
 struct StagingCache {
   std::mutex mu;
   Arena a[4];
+  // Pinned segment buffers of the read handles (archive.cpp PinnedPool,
+  // type-erased, keyed by buffer size), shared by every handle of the
+  // context and kept until bfrs_close: pinning a 32 MiB buffer costs about
+  // as much as reading and verifying the segment it holds.  pools_mu only.
+  std::mutex pools_mu;
+  std::map<size_t, std::shared_ptr<void>> seg_pools;
 };
 StagingCache &staging(bfrs_ctx *ctx);
 
@@ -59,13 +70,16 @@ struct BlockState {
 
 // Reads block b's files into the arena's pinned slots (segments zero-padded
 // to the shard size), copies the block to HBM and verifies every shard
-// against the manifest with the device BLAKE3.
+// against the manifest with the device BLAKE3.  Each shard's H2D copy is
+// queued as soon as its file is read, so the copies overlap the other reads.
 int load_block(bfrs_ctx *ctx, const Geometry &g, size_t b, Arena &a, BlockState *st);
 // RS(k,3)-decodes every damaged segment into its own device slot, re-verifies
-// the restored bytes on the device and copies them to the pinned slots.
+// the restored bytes on the device and copies them to the pinned slots, or,
+// where host_out[s] is given (pinned, >= lens[s] bytes), straight there.
 // Returns the number restored, BFRS_E_NOT_ENOUGH_SHARDS if the block has more
 // damage than valid parity, or another error.
-int restore_block(bfrs_ctx *ctx, const Geometry &g, Arena &a, BlockState &st);
+int restore_block(bfrs_ctx *ctx, const Geometry &g, Arena &a, BlockState &st,
+                  const std::vector<uint8_t *> *host_out = nullptr);
 // Re-encodes the 3 parity shards from the (whole) data on the device,
 // verifies them against the manifest and copies them to the pinned slots.
 int reencode_parity(bfrs_ctx *ctx, const Geometry &g, Arena &a, BlockState &st);
