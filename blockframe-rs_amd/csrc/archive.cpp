@@ -351,6 +351,23 @@ int Commit::tier3(std::string *out_dir) {
   };
   std::atomic<bool> write_ok{true};
   std::atomic<bool> stop{false};  // a failed context stops the others before their next block
+  // pipeline timeline, measurement build only (BFRS_TRACE): one line on stderr
+  const bool trace = BFRS_AB_KNOB("BFRS_TRACE") != nullptr;
+  const auto t_origin = std::chrono::steady_clock::now();
+  std::mutex trace_mu;
+  std::vector<std::string> trace_ev;
+  auto now_us = [&] {
+    return (long long)std::chrono::duration_cast<std::chrono::microseconds>(
+               std::chrono::steady_clock::now() - t_origin)
+        .count();
+  };
+  auto event = [&](const char *what, size_t b, long long t0) {
+    if (!trace) return;
+    const long long t1 = now_us();
+    std::lock_guard<std::mutex> l(trace_mu);
+    trace_ev.push_back(std::string("[\"") + what + "\"," + std::to_string(b) + "," +
+                       std::to_string(t0) + "," + std::to_string(t1 - t0) + "]");
+  };
   // The pipeline of one context over its blocks `mine` (in file order): its
   // own staging arenas, stream, filler and writers; `thr` host threads for
   // the copies.  Every result lands in a per-block slot (seg_cvs ranges,
@@ -360,45 +377,79 @@ int Commit::tier3(std::string *out_dir) {
     if (hipSetDevice(c.device) != hipSuccess) return set_error(BFRS_E_HIP, "commit: hipSetDevice");
     StagingCache &sc = staging(cx);
     std::lock_guard<std::mutex> staging_lock(sc.mu);
-    Arena *arena = sc.a, *pbuf = sc.a + 2;  // pbuf: pinned parity of the block being written
-    for (int i = 0; i < 2; ++i) {
-      int rc = arena[i].reserve(S, kBlockSegments + kParity);
-      if (rc) return rc;
-      if ((rc = pbuf[i].reserve(S, kParity))) return rc;
-    }
-    auto fill = [&](size_t i) {
+    // Segments reach HBM through a ring of pinned slots: filler thread w
+    // copies segments w, w + nfill, ... of a block from the mmap into its two
+    // slots in turn and queues each one's H2D on the ring's stream, so copies
+    // and DMA overlap and only 2 x nfill segments (not two whole blocks) are
+    // pinned.
+    const size_t nfill = std::min<size_t>(kRingThreads, size_t(std::max(1, thr)));
+    BlockArena &ba = sc.blk;
+    int rc = ba.reserve(S);
+    if (!rc) rc = sc.blk2.reserve(S, kBlockSegments + kParity, kArenaDevice);
+    if (!rc) rc = sc.commit_events();
+    if (rc) return rc;
+    Arena *blk[2] = {&ba.dev, &sc.blk2};
+    // the pinned parity of the block being written: out slots [3 (i % 2), +3)
+    auto pbuf = [&](size_t i, size_t p) { return ba.out.hs(kParity * (i % 2) + p); };
+    // block i's segments -> blk[i % 2]; sc.filled[i % 2] marks the last H2D.
+    // blk[i % 2] was last read by block i - 2's GPU work, finished before
+    // block i - 1's began; a ring slot is rewritten once its H2D is done.
+    auto fill = [&](size_t i) -> int {
+      const long long t0 = trace ? now_us() : 0;
       size_t s0, k, shard;
       geom(mine[i], &s0, &k, &shard);
-      Arena &a = arena[i % 2];
-      parallel_for(k, thr, [&](size_t s) {
-        const size_t len = std::min(S, m.n - (s0 + s) * S);
-        std::memcpy(a.hs(s), m.p + (s0 + s) * S, len);
-        if (len < shard) std::memset(a.hs(s) + len, 0, shard - len);
+      Arena &a = *blk[i % 2];
+      std::atomic<int> hip_rc{int(hipSuccess)};
+      auto hip_ok = [&](hipError_t e) {
+        int ok = int(hipSuccess);
+        if (e != hipSuccess) hip_rc.compare_exchange_strong(ok, int(e));
+        return e == hipSuccess;
+      };
+      parallel_for(nfill, int(nfill), [&](size_t w) {
+        if (!hip_ok(hipSetDevice(c.device))) return;
+        size_t turn = 0;
+        for (size_t s = w; s < k && hip_rc.load() == int(hipSuccess); s += nfill, ++turn) {
+          const size_t r = 2 * w + (turn & 1);
+          if (!hip_ok(hipEventSynchronize(ba.ring_ev[r]))) return;
+          const size_t len = std::min(S, m.n - (s0 + s) * S);
+          uint8_t *h = ba.ring.hs(r);
+          std::memcpy(h, m.p + (s0 + s) * S, len);
+          if (len < shard) std::memset(h + len, 0, shard - len);  // generate.rs:75-82
+          if (!hip_ok(hipMemcpyAsync(a.ds(s), h, shard, hipMemcpyHostToDevice, ba.h2d))) return;
+          if (!hip_ok(hipEventRecord(ba.ring_ev[r], ba.h2d))) return;
+        }
       });
+      if (hip_rc.load() == int(hipSuccess)) hip_ok(hipEventRecord(sc.filled[i % 2], ba.h2d));
+      event("fill", mine[i], t0);
+      return hip_rc.load() == int(hipSuccess)
+                 ? BFRS_OK
+                 : hip_error(hipError_t(hip_rc.load()), "commit: segment H2D through the ring");
     };
     auto write_block = [&](size_t i) {  // segments from the mmap, parity from pbuf
       const size_t b = mine[i];
       size_t s0, k, shard;
       geom(b, &s0, &k, &shard);
-      const Arena &pb = pbuf[i % 2];
+      const long long t0 = trace ? now_us() : 0;
       parallel_for(k + kParity, thr, [&](size_t j) {
         bool ok;
         if (j < k)
           ok = write_file(t3_seg(dir, b, j), m.p + (s0 + j) * S, std::min(S, m.n - (s0 + j) * S));
         else
-          ok = write_file(t3_par(dir, b, j - k), pb.hs(j - k), shard);
+          ok = write_file(t3_par(dir, b, j - k), pbuf(i, j - k), shard);
         if (!ok) write_ok = false;
       });
+      event("write", b, t0);
     };
-    // one block on the GPU: H2D, encode, hashes, D2H parity into pbuf[i % 2].
+    // one block on the GPU: encode, hashes, D2H parity into pbuf[i % 2].
     // `wait_writer` is the writer of block i - 2, which still owns pbuf[i % 2]
     auto gpu_block = [&](size_t i, BgTask &wait_writer) -> int {
       const size_t b = mine[i];
       size_t s0, k, shard;
       geom(b, &s0, &k, &shard);
-      Arena &a = arena[i % 2];
-      if (hipMemcpyAsync(a.d, a.h, a.slot * k, hipMemcpyHostToDevice, c.stream) != hipSuccess)
-        return set_error(BFRS_E_HIP, "commit: H2D copy failed");
+      Arena &a = *blk[i % 2];
+      const long long t1 = trace ? now_us() : 0;
+      if (hipStreamWaitEvent(c.stream, sc.filled[i % 2], 0) != hipSuccess)
+        return set_error(BFRS_E_HIP, "commit: wait for the block's H2D failed");
       std::vector<const uint8_t *> orig(k);
       std::vector<uint8_t *> rec(kParity);
       for (size_t s = 0; s < k; ++s) orig[s] = a.ds(s);
@@ -406,6 +457,11 @@ int Commit::tier3(std::string *out_dir) {
       const uint32_t kk = uint32_t(k);
       int rc = encode_batch_on(cx, 1, &kk, kParity, shard, orig.data(), rec.data(), c.stream);
       if (rc) return rc;
+      // the block's H2D and encode land before the hash takes hash_mu
+      if (hipStreamSynchronize(c.stream) != hipSuccess)
+        return set_error(BFRS_E_HIP, "commit: stream synchronize failed");
+      event("h2d_encode", b, t1);
+      const long long t2 = trace ? now_us() : 0;
       std::vector<const uint8_t *> msgs;
       std::vector<size_t> lens;
       for (size_t s = 0; s < k; ++s) {
@@ -428,14 +484,18 @@ int Commit::tier3(std::string *out_dir) {
         if ((rc = gpu_hash_hex(cx, sm, sl, &unused, offs.data(), &cvs))) return rc;
         std::memcpy(seg_cvs.data() + s0 * 32, cvs.data(), k * 32);
       }
+      event("hash", b, t2);
+      const long long t3 = trace ? now_us() : 0;
       wait_writer.join();
-      Arena &pb = pbuf[i % 2];
+      event("wait_writer", b, t3);
+      const long long t4 = trace ? now_us() : 0;
       for (size_t p = 0; p < kParity; ++p)
-        if (hipMemcpyAsync(pb.hs(p), a.ds(k + p), shard, hipMemcpyDeviceToHost, c.stream) !=
+        if (hipMemcpyAsync(pbuf(i, p), a.ds(k + p), shard, hipMemcpyDeviceToHost, c.stream) !=
             hipSuccess)
           return set_error(BFRS_E_HIP, "commit: D2H copy failed");
       if (hipStreamSynchronize(c.stream) != hipSuccess)
         return set_error(BFRS_E_HIP, "commit: stream synchronize failed");
+      event("d2h", b, t4);
       BlockHashes &bh = block_hashes[b];
       bh.segments.assign(hex.begin(), hex.begin() + k);
       bh.parity.assign(hex.begin() + k, hex.end());
@@ -444,20 +504,32 @@ int Commit::tier3(std::string *out_dir) {
       block_roots[b] = merkle_root_hex(leaves);
       return BFRS_OK;
     };
-    int rc = BFRS_OK;
     if (mine.empty()) return rc;
-    fill(0);
-    BgTask writer[2];  // after the lambdas: joined first on every exit path
-    for (size_t i = 0; i < mine.size() && rc == BFRS_OK; ++i) {
-      if (stop.load(std::memory_order_relaxed)) break;  // another context failed
-      // arena[(i+1) % 2] was last used by block i-1's GPU work, which is done
-      BgTask filler;
-      if (i + 1 < mine.size()) filler.start([&fill, i] { fill(i + 1); });
-      rc = gpu_block(i, writer[i % 2]);
-      filler.join();
-      if (rc == BFRS_OK) writer[i % 2].start([&write_block, i] { write_block(i); });
+    rc = fill(0);
+    {
+      BgTask writer[2];  // after the lambdas: joined first on every exit path
+      for (size_t i = 0; i < mine.size() && rc == BFRS_OK; ++i) {
+        if (stop.load(std::memory_order_relaxed)) break;  // another context failed
+        int fill_rc = BFRS_OK;
+        std::string fill_err;
+        {
+          BgTask filler;
+          if (i + 1 < mine.size())
+            filler.start([&fill, &fill_rc, &fill_err, i] {
+              fill_rc = fill(i + 1);
+              if (fill_rc) fill_err = bfrs_last_error();  // thread-local: carried back
+            });
+          rc = gpu_block(i, writer[i % 2]);
+          filler.join();
+        }
+        if (rc == BFRS_OK && fill_rc) rc = set_error(fill_rc, fill_err);
+        if (rc == BFRS_OK) writer[i % 2].start([&write_block, i] { write_block(i); });
+      }
+      for (auto &w : writer) w.join();
     }
-    for (auto &w : writer) w.join();
+    // nothing of this call may still be copying into the ring or the blocks
+    if (hipStreamSynchronize(ba.h2d) != hipSuccess && rc == BFRS_OK)
+      rc = set_error(BFRS_E_HIP, "commit: ring stream synchronize failed");
     return rc;
   };
   // blocks dealt round-robin over the contexts (block b to context b % n)
@@ -485,6 +557,12 @@ int Commit::tier3(std::string *out_dir) {
     for (size_t d = 1; d < n; ++d) others[d - 1].start([&run, d] { run(d); });
     run(0);
     for (auto &t : others) t.join();
+  }
+  if (trace) {
+    std::string line = "bfrs_commit_trace {\"thr\":" + std::to_string(threads) + ",\"events_us\":[";
+    for (size_t i = 0; i < trace_ev.size(); ++i) line += (i ? "," : "") + trace_ev[i];
+    line += "],\"total_us\":" + std::to_string(now_us()) + "}\n";
+    std::fputs(line.c_str(), stderr);
   }
   for (size_t d = 0; d < n; ++d)
     if (rcs[d]) return set_error(rcs[d], n == 1 ? errs[d] : "context " + std::to_string(d) + ": " + errs[d]);
@@ -688,7 +766,7 @@ struct bfrs_archive {
   std::vector<std::thread> workers;
 
   std::mutex gpu_mu;  // the arena (block reconstructions, one at a time)
-  Arena arena;
+  BlockArena arena;
   std::vector<std::unique_ptr<CleanLane>> lanes;  // clean-segment verification
   ReadTrace trace;
 
@@ -885,7 +963,7 @@ int bfrs_archive::recover(size_t gi, SegPtr *out) {
       for (auto &r : restored) {
         const size_t s = r.first - b * kBlockSegments;
         if (was_ok[s]) {  // the target itself was clean (another reader's view was stale)
-          std::memcpy(r.second->p, arena.hs(s), bs.lens[s]);
+          HIP_TRY(hipMemcpy(r.second->p, arena.dev.ds(s), bs.lens[s], hipMemcpyDeviceToHost));
         } else if (write_back && !write_file(t3_seg(g.dir, b, s), r.second->p, bs.lens[s])) {
           return io_error("write back segment");
         }
@@ -940,12 +1018,12 @@ int bfrs_archive::recover(size_t gi, SegPtr *out) {
 
 void bfrs_archive::prefetch_loop(size_t worker) {
   if (worker == 0 && g.mf.tier == 3) {
-    // the block arena (~1.1 GiB pinned + HBM at 32 MiB segments), allocated
+    // the block arena (~1.1 GiB HBM + 22 pinned slots at 32 MiB segments), allocated
     // here rather than when the first damaged block is found and the reader
     // is about to need it; a failure is left to that reconstruction
     std::lock_guard<std::mutex> lg(gpu_mu);
     if (hipSetDevice(ctx->impl.device) == hipSuccess)
-      (void)arena.reserve(pool->slot, kBlockSegments + kParity);
+      (void)arena.reserve(pool->slot);
   }
   std::unique_lock<std::mutex> l(mu);
   for (;;) {
@@ -1089,7 +1167,7 @@ int repair_blocks(bfrs_ctx *ctx, const Geometry &g, const std::vector<size_t> &m
     return set_error(BFRS_E_HIP, "repair: hipSetDevice failed");
   StagingCache &sc = staging(ctx);
   std::lock_guard<std::mutex> staging_lock(sc.mu);
-  Arena &a = sc.a[0];
+  BlockArena &a = sc.blk;
   int rc;
   for (const size_t b : mine) {
     if (stop && stop->load(std::memory_order_relaxed)) break;
@@ -1105,17 +1183,16 @@ int repair_blocks(bfrs_ctx *ctx, const Geometry &g, const std::vector<size_t> &m
       continue;
     }
     if (restored < 0) return restored;
-    for (size_t s = 0; s < bs.k; ++s)
-      if (!was_ok[s]) {
-        if (!write_file(t3_seg(g.dir, b, s), a.hs(s), bs.lens[s]))
-          return io_error("write restored segment");
-        ++rep->segments_repaired;
-      }
+    for (const auto &r : bs.restored) {  // exactly the segments that were damaged
+      if (!write_file(t3_seg(g.dir, b, r.first), r.second, bs.lens[r.first]))
+        return io_error("write restored segment");
+      ++rep->segments_repaired;
+    }
     if (parity_bad) {
       const std::vector<uint8_t> par_was = bs.par_ok;
       if ((rc = reencode_parity(ctx, g, a, bs))) return rc;
       for (size_t p = 0; p < kParity; ++p)
-        if (!par_was[p] && !write_file(t3_par(g.dir, b, p), a.hs(bs.k + p), bs.shard))
+        if (!par_was[p] && !write_file(t3_par(g.dir, b, p), bs.parity_host[p], bs.shard))
           return io_error("write parity");
       rep->parity_repaired += parity_bad;
     }
@@ -1281,7 +1358,7 @@ int health_report(bfrs_ctx *ctx, const char *archive_dir, Json *out) {
   if (g.mf.tier == 3) {
     StagingCache &sc = staging(ctx);
     std::lock_guard<std::mutex> staging_lock(sc.mu);
-    Arena &a = sc.a[0];
+    BlockArena &a = sc.blk;
     for (const auto &kv : g.mf.blocks) {
       const size_t b = size_t(kv.first);
       BlockState bs;

@@ -15,12 +15,14 @@ Arena::~Arena() {
   if (d) (void)hipFree(d);
 }
 
-int Arena::reserve(size_t slot_bytes, size_t n) {
+int Arena::reserve(size_t slot_bytes, size_t n, unsigned parts) {
   slot_bytes = std::max<size_t>(256, shard_pitch(slot_bytes));
   n = std::max<size_t>(1, n);
-  if (h && slot_bytes <= slot && n <= nslots) return BFRS_OK;
+  const bool have = (!(parts & kArenaHost) || h) && (!(parts & kArenaDevice) || d);
+  if (have && slot_bytes <= slot && n <= nslots) return BFRS_OK;
+  parts |= (h ? kArenaHost : 0u) | (d ? kArenaDevice : 0u);
+  if (h || d) HIP_TRY(hipDeviceSynchronize());
   if (h) {
-    HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipHostFree(h));
     h = nullptr;
   }
@@ -30,9 +32,41 @@ int Arena::reserve(size_t slot_bytes, size_t n) {
   }
   slot = std::max(slot, slot_bytes);
   nslots = std::max(nslots, n);
-  HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&h), slot * nslots, hipHostMallocDefault));
-  HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d), slot * nslots));
+  if (parts & kArenaHost)
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&h), slot * nslots, hipHostMallocDefault));
+  if (parts & kArenaDevice) HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d), slot * nslots));
   return BFRS_OK;
+}
+
+int BlockArena::reserve(size_t slot_bytes) {
+  int rc = dev.reserve(slot_bytes, kBlockSegments + kParity, kArenaDevice);
+  if (!rc) rc = ring.reserve(slot_bytes, 2 * kRingThreads, kArenaHost);
+  if (!rc) rc = out.reserve(slot_bytes, kOutSlots, kArenaHost);
+  if (rc) return rc;
+  if (!h2d) HIP_TRY(hipStreamCreateWithFlags(&h2d, hipStreamNonBlocking));
+  while (ring_ev.size() < 2 * kRingThreads) {
+    hipEvent_t e = nullptr;
+    HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    ring_ev.push_back(e);
+  }
+  return BFRS_OK;
+}
+
+BlockArena::~BlockArena() {
+  if (h2d) (void)hipStreamSynchronize(h2d);
+  for (hipEvent_t e : ring_ev) (void)hipEventDestroy(e);
+  if (h2d) (void)hipStreamDestroy(h2d);
+}
+
+int StagingCache::commit_events() {
+  for (auto &e : filled)
+    if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  return BFRS_OK;
+}
+
+StagingCache::~StagingCache() {
+  for (hipEvent_t e : filled)
+    if (e) (void)hipEventDestroy(e);
 }
 
 StagingCache &staging(bfrs_ctx *ctx) {
@@ -68,13 +102,15 @@ size_t BlockState::valid_parity() const {
   return n;
 }
 
-int load_block(bfrs_ctx *ctx, const Geometry &g, size_t b, Arena &a, BlockState *st) {
+int load_block(bfrs_ctx *ctx, const Geometry &g, size_t b, BlockArena &a, BlockState *st) {
   auto it = g.mf.blocks.find(int64_t(b));
   if (it == g.mf.blocks.end()) return set_error(BFRS_E_WRAPPER, "manifest has no block " + std::to_string(b));
   const BlockHashes &bh = it->second;
   st->b = b;
   st->k = bh.segments.size();
   st->shard = g.block_shard(b);
+  st->restored.clear();
+  for (auto &p : st->parity_host) p = nullptr;
   const size_t k = st->k, shard = st->shard;
   st->lens.resize(k);
   for (size_t s = 0; s < k; ++s) st->lens[s] = g.seg_len(b * kBlockSegments + s);
@@ -82,36 +118,50 @@ int load_block(bfrs_ctx *ctx, const Geometry &g, size_t b, Arena &a, BlockState 
   // the arena's HBM must be on this context's device: the caller may be a
   // read handle's prefetch thread or an API thread bound to another GPU
   HIP_TRY(hipSetDevice(c.device));
-  int rc = a.reserve(shard, k + kParity);
+  int rc = a.reserve(shard);
   if (rc) return rc;
-  std::vector<uint8_t> readable(k + kParity, 0);
+  // thread w reads shards w, w + nthr, ... into its two ring slots in turn;
+  // each shard's H2D goes as soon as its read ends
+  const size_t n = k + kParity;
+  const size_t nthr = std::min<size_t>(kRingThreads, size_t(std::max(1, hw_threads())));
+  std::vector<uint8_t> readable(n, 0);
   std::atomic<int> hip_rc{int(hipSuccess)};
-  parallel_for(k + kParity, hw_threads(), [&](size_t i) {
-    if (i < k) {
-      const long long n = read_file_into(t3_seg(g.dir, b, i), a.hs(i), a.slot);
-      readable[i] = n == (long long)st->lens[i];
-      if (readable[i] && st->lens[i] < shard)  // generate.rs:75-82 zero padding
-        std::memset(a.hs(i) + st->lens[i], 0, shard - st->lens[i]);
-    } else {
-      readable[i] = read_file_into(t3_par(g.dir, b, i - k), a.hs(i), a.slot) == (long long)shard;
-    }
-    if (!readable[i]) return;  // excluded from the hash and the decode: no copy
-    // this shard's H2D now, while the other files are still being read
-    hipError_t e = hipSetDevice(c.device);
-    if (e == hipSuccess) e = hipMemcpyAsync(a.ds(i), a.hs(i), shard, hipMemcpyHostToDevice, c.stream);
+  auto hip_ok = [&](hipError_t e) {
     int ok = int(hipSuccess);
     if (e != hipSuccess) hip_rc.compare_exchange_strong(ok, int(e));
+    return e == hipSuccess;
+  };
+  parallel_for(nthr, int(nthr), [&](size_t w) {
+    if (!hip_ok(hipSetDevice(c.device))) return;
+    size_t turn = 0;
+    for (size_t i = w; i < n && hip_rc.load() == int(hipSuccess); i += nthr, ++turn) {
+      const size_t r = 2 * w + (turn & 1);
+      if (!hip_ok(hipEventSynchronize(a.ring_ev[r]))) return;  // slot r's last copy is done
+      uint8_t *h = a.ring.hs(r);
+      if (i < k) {
+        const long long got = read_file_into(t3_seg(g.dir, b, i), h, a.ring.slot);
+        readable[i] = got == (long long)st->lens[i];
+        if (readable[i] && st->lens[i] < shard)  // generate.rs:75-82 zero padding
+          std::memset(h + st->lens[i], 0, shard - st->lens[i]);
+      } else {
+        readable[i] = read_file_into(t3_par(g.dir, b, i - k), h, a.ring.slot) == (long long)shard;
+      }
+      if (!readable[i]) continue;  // excluded from the hash and the decode: no copy
+      if (!hip_ok(hipMemcpyAsync(a.dev.ds(i), h, shard, hipMemcpyHostToDevice, a.h2d))) return;
+      if (!hip_ok(hipEventRecord(a.ring_ev[r], a.h2d))) return;
+    }
   });
-  if (hip_rc.load() != int(hipSuccess)) {
-    (void)hipStreamSynchronize(c.stream);
-    return hip_error(hipError_t(hip_rc.load()), "hipMemcpyAsync (block shard H2D)");
-  }
-  HIP_TRY(hipStreamSynchronize(c.stream));  // the copies land before the hash takes hash_mu
+  // the copies land before the hash takes hash_mu (and before any error
+  // return: nothing may still be reading the ring)
+  const hipError_t sync = hipStreamSynchronize(a.h2d);
+  if (hip_rc.load() != int(hipSuccess))
+    return hip_error(hipError_t(hip_rc.load()), "block shard H2D through the ring");
+  if (sync != hipSuccess) return hip_error(sync, "hipStreamSynchronize (block ring)");
   std::vector<const uint8_t *> msgs;
   std::vector<size_t> lens, idx;
-  for (size_t i = 0; i < k + kParity; ++i)
+  for (size_t i = 0; i < n; ++i)
     if (readable[i]) {
-      msgs.push_back(a.ds(i));
+      msgs.push_back(a.dev.ds(i));
       lens.push_back(i < k ? st->lens[i] : shard);
       idx.push_back(i);
     }
@@ -129,9 +179,10 @@ int load_block(bfrs_ctx *ctx, const Geometry &g, size_t b, Arena &a, BlockState 
   return BFRS_OK;
 }
 
-int restore_block(bfrs_ctx *ctx, const Geometry &g, Arena &a, BlockState &st,
+int restore_block(bfrs_ctx *ctx, const Geometry &g, BlockArena &a, BlockState &st,
                   const std::vector<uint8_t *> *host_out) {
   const size_t k = st.k, erased = st.damaged_segments(), present = st.valid_parity();
+  st.restored.clear();
   if (erased == 0) return 0;
   if (erased > present) {
     std::ostringstream os;
@@ -142,10 +193,10 @@ int restore_block(bfrs_ctx *ctx, const Geometry &g, Arena &a, BlockState &st,
   std::vector<const uint8_t *> orig(k), rec(kParity);
   std::vector<uint8_t *> out(k);
   for (size_t s = 0; s < k; ++s) {
-    orig[s] = st.seg_ok[s] ? a.ds(s) : nullptr;
-    out[s] = a.ds(s);  // written only where erased: the restored segment lands in its own slot
+    orig[s] = st.seg_ok[s] ? a.dev.ds(s) : nullptr;
+    out[s] = a.dev.ds(s);  // written only where erased: the restored segment lands in its own slot
   }
-  for (size_t p = 0; p < kParity; ++p) rec[p] = st.par_ok[p] ? a.ds(k + p) : nullptr;
+  for (size_t p = 0; p < kParity; ++p) rec[p] = st.par_ok[p] ? a.dev.ds(k + p) : nullptr;
   Context &c = ctx->impl;
   const uint32_t kk = uint32_t(k);
   int rc = decode_batch_on(ctx, 1, &kk, kParity, st.shard, orig.data(), rec.data(), out.data(),
@@ -156,7 +207,7 @@ int restore_block(bfrs_ctx *ctx, const Geometry &g, Arena &a, BlockState &st,
   std::vector<size_t> lens, idx;
   for (size_t s = 0; s < k; ++s)
     if (!st.seg_ok[s]) {
-      msgs.push_back(a.ds(s));
+      msgs.push_back(a.dev.ds(s));
       lens.push_back(st.lens[s]);
       idx.push_back(s);
     }
@@ -169,23 +220,25 @@ int restore_block(bfrs_ctx *ctx, const Geometry &g, Arena &a, BlockState &st,
       os << "block " << st.b << " segment " << idx[j] << ": restored bytes fail the manifest hash";
       return set_error(BFRS_E_WRAPPER, os.str());
     }
-  for (size_t s : idx) {
-    uint8_t *dst = host_out ? (*host_out)[s] : nullptr;
-    HIP_TRY(hipMemcpyAsync(dst ? dst : a.hs(s), a.ds(s), dst ? st.lens[s] : st.shard,
-                           hipMemcpyDeviceToHost, c.stream));
+  // erased <= kParity, so the out slots [0, kParity) hold every one of them
+  for (size_t j = 0; j < idx.size(); ++j) {
+    const size_t s = idx[j];
+    uint8_t *dst = host_out && (*host_out)[s] ? (*host_out)[s] : a.out.hs(j);
+    HIP_TRY(hipMemcpyAsync(dst, a.dev.ds(s), st.lens[s], hipMemcpyDeviceToHost, c.stream));
+    st.restored.emplace_back(s, dst);
   }
   HIP_TRY(hipStreamSynchronize(c.stream));
   for (size_t s : idx) st.seg_ok[s] = 1;
   return int(idx.size());
 }
 
-int reencode_parity(bfrs_ctx *ctx, const Geometry &g, Arena &a, BlockState &st) {
+int reencode_parity(bfrs_ctx *ctx, const Geometry &g, BlockArena &a, BlockState &st) {
   const size_t k = st.k;
   if (st.damaged_segments()) return set_error(BFRS_E_WRAPPER, "re-encode needs whole data");
   std::vector<const uint8_t *> orig(k);
   std::vector<uint8_t *> rec(kParity);
-  for (size_t s = 0; s < k; ++s) orig[s] = a.ds(s);
-  for (size_t p = 0; p < kParity; ++p) rec[p] = a.ds(k + p);
+  for (size_t s = 0; s < k; ++s) orig[s] = a.dev.ds(s);
+  for (size_t p = 0; p < kParity; ++p) rec[p] = a.dev.ds(k + p);
   Context &c = ctx->impl;
   const uint32_t kk = uint32_t(k);
   int rc = encode_batch_on(ctx, 1, &kk, kParity, st.shard, orig.data(), rec.data(), c.stream);
@@ -198,7 +251,11 @@ int reencode_parity(bfrs_ctx *ctx, const Geometry &g, Arena &a, BlockState &st) 
   for (size_t p = 0; p < kParity; ++p)
     if (hex[p] != bh.parity[p])
       return set_error(BFRS_E_WRAPPER, "re-encoded parity fails the manifest hash");
-  HIP_TRY(hipMemcpyAsync(a.hs(k), a.ds(k), a.slot * kParity, hipMemcpyDeviceToHost, c.stream));
+  for (size_t p = 0; p < kParity; ++p) {
+    HIP_TRY(hipMemcpyAsync(a.out.hs(kParity + p), a.dev.ds(k + p), st.shard, hipMemcpyDeviceToHost,
+                           c.stream));
+    st.parity_host[p] = a.out.hs(kParity + p);
+  }
   HIP_TRY(hipStreamSynchronize(c.stream));
   for (size_t p = 0; p < kParity; ++p) st.par_ok[p] = 1;
   return BFRS_OK;

@@ -4,8 +4,8 @@
 // The reference reads a block's shards into Vec<u8>s, hashes each on the CPU
 // and calls reed-solomon-simd (health.rs:642-765, recovery.rs:118-173).  Here
 // a block of k segments + 3 parity shards occupies k+3 equal slots of an
-// Arena: the files are read straight into pinned slots (one H2D copy of the
-// whole block), every shard is hashed in one device BLAKE3 call, the decode
+// Arena: the files are read straight into pinned slots (each shard's H2D
+// queued as its read ends), every shard is hashed in one device BLAKE3 call, the decode
 // writes restored segments over their own (erased) device slots, and the
 // restored bytes are re-hashed on the device before anything reaches disk.
 #pragma once
@@ -23,7 +23,9 @@
 
 namespace bfrs {
 
-// Pinned host slots and device slots of equal size (grow-only).
+// Pinned host slots and device slots of equal size (grow-only); `parts`
+// picks which of the two an arena holds (a regrow keeps what it had).
+enum : unsigned { kArenaHost = 1, kArenaDevice = 2, kArenaBoth = 3 };
 struct Arena {
   size_t slot = 0, nslots = 0;
   uint8_t *h = nullptr, *d = nullptr;
@@ -31,9 +33,29 @@ struct Arena {
   Arena(const Arena &) = delete;
   Arena &operator=(const Arena &) = delete;
   ~Arena();
-  int reserve(size_t slot_bytes, size_t n);
+  int reserve(size_t slot_bytes, size_t n, unsigned parts = kArenaBoth);
   uint8_t *hs(size_t i) const { return h + i * slot; }
   uint8_t *ds(size_t i) const { return d + i * slot; }
+};
+
+// A tier-3 block's staging: HBM slots for the whole block (k segments + 3
+// parity) and the pinned memory the block passes through — a ring the shard
+// files are read (or copied) into on their way to HBM, two slots per staging
+// thread, and kOutSlots slots for what comes back (restored segments,
+// re-encoded parity).  The ring's H2D copies run on its own stream; ring_ev[r]
+// marks slot r's last copy.  Pinned: (2 x kRingThreads + kOutSlots) slots,
+// not the whole block.
+constexpr size_t kRingThreads = 8;
+constexpr size_t kOutSlots = 2 * kParity;
+struct BlockArena {
+  Arena dev, ring, out;
+  hipStream_t h2d = nullptr;
+  std::vector<hipEvent_t> ring_ev;
+  BlockArena() = default;
+  BlockArena(const BlockArena &) = delete;
+  BlockArena &operator=(const BlockArena &) = delete;
+  ~BlockArena();
+  int reserve(size_t slot_bytes);  // on the context's device
 };
 
 // Device BLAKE3 -> lowercase hex digests (on `stream`, default the context's;
@@ -45,11 +67,23 @@ int gpu_hash_hex(bfrs_ctx *ctx, const std::vector<const uint8_t *> &d_msgs,
                  hipStream_t stream = nullptr);
 
 // The context's staging arenas (Context::staging): archive calls on one
-// context take `mu` for their duration and use a[0..1] as block arenas and
-// a[2..3] as parity buffers.  Arenas grow and are never shrunk.
+// context take `mu` for their duration.  The RS(1,3) tiers' commit uses
+// a[0..1] as round arenas and a[2..3] as parity buffers.  Tier 3: repair and
+// health check use `blk`; the commit uses blk.dev and blk2 as its two device
+// block buffers, blk's ring to fill them, blk.out slots [0,3) / [3,6) as the
+// pinned parity of the blocks being written, and `filled[i]` to mark a
+// block's last H2D.  Arenas grow and are never shrunk.
 struct StagingCache {
   std::mutex mu;
   Arena a[4];
+  BlockArena blk;
+  Arena blk2;
+  hipEvent_t filled[2] = {nullptr, nullptr};
+  int commit_events();  // under mu, on the context's device
+  StagingCache() = default;
+  StagingCache(const StagingCache &) = delete;
+  StagingCache &operator=(const StagingCache &) = delete;
+  ~StagingCache();
   // Pinned segment buffers of the read handles (archive.cpp PinnedPool,
   // type-erased, keyed by buffer size), shared by every handle of the
   // context and kept until bfrs_close: pinning a 32 MiB buffer costs about
@@ -64,24 +98,30 @@ struct BlockState {
   size_t b = 0, k = 0, shard = 0;
   std::vector<size_t> lens;            // unpadded segment lengths
   std::vector<uint8_t> seg_ok, par_ok;  // present and matching the manifest
+  // where restore_block / reencode_parity left host copies: segment index ->
+  // bytes (lens[s]), parity p -> bytes (shard)
+  std::vector<std::pair<size_t, const uint8_t *>> restored;
+  const uint8_t *parity_host[kParity] = {};
   size_t damaged_segments() const;
   size_t valid_parity() const;
 };
 
-// Reads block b's files into the arena's pinned slots (segments zero-padded
-// to the shard size), copies the block to HBM and verifies every shard
-// against the manifest with the device BLAKE3.  Each shard's H2D copy is
-// queued as soon as its file is read, so the copies overlap the other reads.
-int load_block(bfrs_ctx *ctx, const Geometry &g, size_t b, Arena &a, BlockState *st);
+// Reads block b's files through the arena's ring (segments zero-padded to
+// the shard size) into its HBM slots and verifies every shard against the
+// manifest with the device BLAKE3.  Each shard's H2D is queued as soon as
+// its file is read, so the copies overlap the other reads.
+int load_block(bfrs_ctx *ctx, const Geometry &g, size_t b, BlockArena &a, BlockState *st);
 // RS(k,3)-decodes every damaged segment into its own device slot, re-verifies
-// the restored bytes on the device and copies them to the pinned slots, or,
-// where host_out[s] is given (pinned, >= lens[s] bytes), straight there.
-// Returns the number restored, BFRS_E_NOT_ENOUGH_SHARDS if the block has more
-// damage than valid parity, or another error.
-int restore_block(bfrs_ctx *ctx, const Geometry &g, Arena &a, BlockState &st,
+// the restored bytes on the device and copies them to host memory: to
+// host_out[s] where given (pinned, >= lens[s] bytes), else to the arena's out
+// slots; st.restored lists where each one landed.  Returns the number
+// restored, BFRS_E_NOT_ENOUGH_SHARDS if the block has more damage than valid
+// parity, or another error.
+int restore_block(bfrs_ctx *ctx, const Geometry &g, BlockArena &a, BlockState &st,
                   const std::vector<uint8_t *> *host_out = nullptr);
 // Re-encodes the 3 parity shards from the (whole) data on the device,
-// verifies them against the manifest and copies them to the pinned slots.
-int reencode_parity(bfrs_ctx *ctx, const Geometry &g, Arena &a, BlockState &st);
+// verifies them against the manifest and copies them to the arena's out
+// slots [kParity, 2 kParity) (st.parity_host).
+int reencode_parity(bfrs_ctx *ctx, const Geometry &g, BlockArena &a, BlockState &st);
 
 }  // namespace bfrs

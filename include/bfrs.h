@@ -376,7 +376,7 @@ typedef struct {
  * context keeps per segment size and shares between its handles (they stay
  * pinned until bfrs_close: about cache_segments + 8 buffers per handle open
  * at the same time); a tier-3 handle with prefetch also allocates a
- * block arena of 33 segment slots (pinned + HBM) at open, on a prefetch
+ * block arena (33 HBM segment slots, 22 pinned) at open, on a prefetch
  * thread, and one HBM segment buffer per verification lane (prefetch workers
  * + 1).  Both are freed by bfrs_archive_close. */
 int bfrs_archive_open(bfrs_ctx *ctx, const char *archive_dir, size_t cache_segments,
