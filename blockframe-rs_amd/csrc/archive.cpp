@@ -64,6 +64,35 @@ struct Mapped {
   }
 };
 
+// Pipeline timeline, measurement build only (BFRS_TRACE): [what, unit,
+// start us, duration us] events, one line on stderr at the end.  `on` is
+// false in libbfrs.so (one branch per event).
+struct PipeTrace {
+  const bool on = BFRS_AB_KNOB("BFRS_TRACE") != nullptr;
+  const std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+  std::mutex mu;
+  std::vector<std::string> ev;
+  long long now_us() const {
+    return (long long)std::chrono::duration_cast<std::chrono::microseconds>(
+               std::chrono::steady_clock::now() - t0)
+        .count();
+  }
+  void event(const char *what, size_t unit, long long start) {
+    if (!on) return;
+    const long long end = now_us();
+    std::lock_guard<std::mutex> l(mu);
+    ev.push_back(std::string("[\"") + what + "\"," + std::to_string(unit) + "," +
+                 std::to_string(start) + "," + std::to_string(end - start) + "]");
+  }
+  void print(const char *name, int threads) {
+    if (!on) return;
+    std::string line = std::string(name) + " {\"thr\":" + std::to_string(threads) + ",\"events_us\":[";
+    for (size_t i = 0; i < ev.size(); ++i) line += (i ? "," : "") + ev[i];
+    line += "],\"total_us\":" + std::to_string(now_us()) + "}\n";
+    std::fputs(line.c_str(), stderr);
+  }
+};
+
 struct Commit {
   bfrs_ctx *ctx;
   std::string root, name;
@@ -77,7 +106,7 @@ struct Commit {
   int tier3(std::string *out_dir);
   int rs13_segments(size_t nseg, bool cv_hash, std::vector<uint8_t> *seg_cvs,
                     std::vector<struct Rs13Hashes> *hashes,
-                    const std::function<bool(size_t, const uint8_t *const *, size_t)> &write);
+                    const std::function<bool(size_t, size_t, const uint8_t *const *, size_t)> &write);
   int finish(const std::string &computing, const std::string &file_hash, Manifest &mf,
              std::string *out_dir);
 };
@@ -115,11 +144,13 @@ struct Rs13Hashes {
   std::string data;
   std::string parity[3];
 };
-using Rs13Writer = std::function<bool(size_t seg, const uint8_t *const par[3], size_t shard)>;
+// writes file `file` of segment `seg`: 0 = the data, 1 + p = parity copy p
+using Rs13Writer =
+    std::function<bool(size_t seg, size_t file, const uint8_t *const par[3], size_t shard)>;
 
 int Commit::rs13_segments(size_t nseg, bool cv_hash, std::vector<uint8_t> *seg_cvs,
                           std::vector<Rs13Hashes> *hashes, const Rs13Writer &write) {
-  constexpr size_t kRound = 8;
+  constexpr size_t kRound = 4;
   auto seg_len = [&](size_t j) { return std::min(S, m.n - j * S); };
   auto padded = [&](size_t j) { return (seg_len(j) + 63) / 64 * 64; };
   // rounds: consecutive segments with the same padded size, <= kRound each
@@ -133,42 +164,80 @@ int Commit::rs13_segments(size_t nseg, bool cv_hash, std::vector<uint8_t> *seg_c
   hashes->assign(nseg, {});
   if (cv_hash) seg_cvs->assign(nseg * 32, 0);
   const size_t slot = (std::min(S, m.n) + 63) / 64 * 64;
+  PipeTrace pt;
   StagingCache &sc = staging(ctx);
   std::lock_guard<std::mutex> staging_lock(sc.mu);
+  // device round buffers (4 slots per segment: data + 3 parity), filled
+  // through the pinned ring of sc.blk like the tier-3 commit; only the
+  // rounds' parity (3 slots per segment, two rounds) is pinned besides
   Arena *arena = sc.a, *pbuf = sc.a + 2;
-  for (int i = 0; i < 2; ++i) {
-    int rc = arena[i].reserve(slot, 4 * std::min(kRound, nseg));
-    if (rc) return rc;
-    if ((rc = pbuf[i].reserve(slot, 3 * std::min(kRound, nseg)))) return rc;
+  BlockArena &ba = sc.blk;
+  Context &c = ctx->impl;
+  if (hipSetDevice(c.device) != hipSuccess) return set_error(BFRS_E_HIP, "commit: hipSetDevice");
+  const long long t_res = pt.on ? pt.now_us() : 0;
+  const size_t nfill = std::min({kRingThreads, size_t(std::max(1, threads)), std::min(kRound, nseg)});
+  int rc = ba.reserve_ring(slot, 2 * nfill);
+  if (!rc) rc = sc.commit_events();
+  for (int i = 0; i < 2 && !rc; ++i) {
+    rc = arena[i].reserve(slot, 4 * std::min(kRound, nseg), kArenaDevice);
+    if (!rc) rc = pbuf[i].reserve(slot, 3 * std::min(kRound, nseg), kArenaHost);
   }
-  auto fill = [&](size_t r) {
+  if (rc) return rc;
+  pt.event("reserve", 0, t_res);
+  // round r's segments -> arena[r % 2] (slots 4j); sc.filled[r % 2] marks
+  // the last H2D.  arena[r % 2] was last read by round r - 2's GPU work,
+  // finished before round r - 1's began; a ring slot is rewritten once its
+  // H2D is done.
+  auto fill = [&](size_t r) -> int {
+    const long long t0 = pt.on ? pt.now_us() : 0;
     const size_t first = rounds[r].first, cnt = rounds[r].second;
     Arena &a = arena[r % 2];
-    parallel_for(cnt, threads, [&](size_t j) {
-      const size_t len = seg_len(first + j), pad = padded(first + j);
-      std::memcpy(a.hs(4 * j), m.p + (first + j) * S, len);
-      if (pad > len) std::memset(a.hs(4 * j) + len, 0, pad - len);
+    std::atomic<int> hip_rc{int(hipSuccess)};
+    auto hip_ok = [&](hipError_t e) {
+      int ok = int(hipSuccess);
+      if (e != hipSuccess) hip_rc.compare_exchange_strong(ok, int(e));
+      return e == hipSuccess;
+    };
+    parallel_for(nfill, int(nfill), [&](size_t w) {
+      if (!hip_ok(hipSetDevice(c.device))) return;
+      size_t turn = 0;
+      for (size_t j = w; j < cnt && hip_rc.load() == int(hipSuccess); j += nfill, ++turn) {
+        const size_t rs = 2 * w + (turn & 1);
+        if (!hip_ok(hipEventSynchronize(ba.ring_ev[rs]))) return;
+        const size_t len = seg_len(first + j), pad = padded(first + j);
+        uint8_t *h = ba.ring.hs(rs);
+        std::memcpy(h, m.p + (first + j) * S, len);
+        if (pad > len) std::memset(h + len, 0, pad - len);  // generate.rs:34-46
+        if (!hip_ok(hipMemcpyAsync(a.ds(4 * j), h, pad, hipMemcpyHostToDevice, ba.h2d))) return;
+        if (!hip_ok(hipEventRecord(ba.ring_ev[rs], ba.h2d))) return;
+      }
     });
+    if (hip_rc.load() == int(hipSuccess)) hip_ok(hipEventRecord(sc.filled[r % 2], ba.h2d));
+    pt.event("fill", r, t0);
+    return hip_rc.load() == int(hipSuccess)
+               ? BFRS_OK
+               : hip_error(hipError_t(hip_rc.load()), "commit: segment H2D through the ring");
   };
   std::atomic<bool> write_ok{true};
   auto write_round = [&](size_t r) {
     const size_t first = rounds[r].first, cnt = rounds[r].second;
     const Arena &pb = pbuf[r % 2];
-    parallel_for(cnt, threads, [&](size_t j) {
+    const long long t0 = pt.on ? pt.now_us() : 0;
+    parallel_for(cnt * (1 + kParity), threads, [&](size_t item) {  // one file per item
+      const size_t j = item / (1 + kParity), file = item % (1 + kParity);
       const uint8_t *par[3] = {pb.hs(3 * j), pb.hs(3 * j + 1), pb.hs(3 * j + 2)};
-      if (!write(first + j, par, padded(first + j))) write_ok = false;
+      if (!write(first + j, file, par, padded(first + j))) write_ok = false;
     });
+    pt.event("write", r, t0);
   };
-  Context &c = ctx->impl;
   // `wait_writer` is the writer of round r - 2, which still owns pbuf[r % 2]
   auto gpu_round = [&](size_t r, BgTask &wait_writer) -> int {
     const size_t first = rounds[r].first, cnt = rounds[r].second;
     const size_t shard = padded(first);
     Arena &a = arena[r % 2];
-    if (hipSetDevice(c.device) != hipSuccess) return set_error(BFRS_E_HIP, "commit: hipSetDevice");
-    for (size_t j = 0; j < cnt; ++j)
-      if (hipMemcpyAsync(a.ds(4 * j), a.hs(4 * j), shard, hipMemcpyHostToDevice, c.stream) != hipSuccess)
-        return set_error(BFRS_E_HIP, "commit: H2D copy failed");
+    const long long t0 = pt.on ? pt.now_us() : 0;
+    if (hipStreamWaitEvent(c.stream, sc.filled[r % 2], 0) != hipSuccess)
+      return set_error(BFRS_E_HIP, "commit: wait for the round's H2D failed");
     std::vector<uint32_t> ks(cnt, 1);
     std::vector<const uint8_t *> orig(cnt);
     std::vector<uint8_t *> rec(3 * cnt);
@@ -209,7 +278,11 @@ int Commit::rs13_segments(size_t nseg, bool cv_hash, std::vector<uint8_t> *seg_c
       if ((rc = gpu_hash_hex(ctx, sm, sl, &unused, offs.data(), &cvs))) return rc;
       std::memcpy(seg_cvs->data() + first * 32, cvs.data(), cnt * 32);
     }
+    pt.event("h2d_encode_hash", r, t0);
+    const long long t1 = pt.on ? pt.now_us() : 0;
     wait_writer.join();
+    pt.event("wait_writer", r, t1);
+    const long long t2 = pt.on ? pt.now_us() : 0;
     Arena &pb = pbuf[r % 2];
     for (size_t j = 0; j < cnt; ++j)
       for (size_t p = 0; p < kParity; ++p)
@@ -218,19 +291,34 @@ int Commit::rs13_segments(size_t nseg, bool cv_hash, std::vector<uint8_t> *seg_c
           return set_error(BFRS_E_HIP, "commit: D2H copy failed");
     if (hipStreamSynchronize(c.stream) != hipSuccess)
       return set_error(BFRS_E_HIP, "commit: stream synchronize failed");
+    pt.event("d2h", r, t2);
     return BFRS_OK;
   };
-  int rc = BFRS_OK;
-  fill(0);
-  BgTask writer[2];  // after the lambdas: joined first on every exit path
-  for (size_t r = 0; r < rounds.size() && rc == BFRS_OK; ++r) {
-    BgTask filler;
-    if (r + 1 < rounds.size()) filler.start([&fill, r] { fill(r + 1); });
-    rc = gpu_round(r, writer[r % 2]);
-    filler.join();
-    if (rc == BFRS_OK) writer[r % 2].start([&write_round, r] { write_round(r); });
+  rc = fill(0);
+  {
+    BgTask writer[2];  // after the lambdas: joined first on every exit path
+    for (size_t r = 0; r < rounds.size() && rc == BFRS_OK; ++r) {
+      int fill_rc = BFRS_OK;
+      std::string fill_err;
+      {
+        BgTask filler;
+        if (r + 1 < rounds.size())
+          filler.start([&fill, &fill_rc, &fill_err, r] {
+            fill_rc = fill(r + 1);
+            if (fill_rc) fill_err = bfrs_last_error();  // thread-local: carried back
+          });
+        rc = gpu_round(r, writer[r % 2]);
+        filler.join();
+      }
+      if (rc == BFRS_OK && fill_rc) rc = set_error(fill_rc, fill_err);
+      if (rc == BFRS_OK) writer[r % 2].start([&write_round, r] { write_round(r); });
+    }
+    for (auto &w : writer) w.join();
   }
-  for (auto &w : writer) w.join();
+  // nothing of this call may still be copying into the ring or the rounds
+  if (hipStreamSynchronize(ba.h2d) != hipSuccess && rc == BFRS_OK)
+    rc = set_error(BFRS_E_HIP, "commit: ring stream synchronize failed");
+  pt.print("bfrs_rs13_trace", threads);
   if (rc) return rc;
   return write_ok ? BFRS_OK : io_error("write RS(1,3) shards");
 }
@@ -245,9 +333,10 @@ int Commit::tier1(std::string *out_dir) {
   // and encode into memory first (the writer runs after the pass completes)
   std::vector<std::vector<uint8_t>> par(kParity);
   size_t shard = 0;
-  auto keep = [&](size_t, const uint8_t *const p[3], size_t sh) {
+  auto keep = [&](size_t, size_t file, const uint8_t *const p[3], size_t sh) {
+    if (file == 0) return true;  // the data is written from the mapping below
     shard = sh;
-    for (size_t i = 0; i < kParity; ++i) par[i].assign(p[i], p[i] + sh);
+    par[file - 1].assign(p[file - 1], p[file - 1] + sh);
     return true;
   };
   int rc = rs13_segments(1, false, nullptr, &hs, keep);
@@ -278,10 +367,9 @@ int Commit::tier2(std::string *out_dir) {
   const bool cv_hash = pow2_kib(S) && nseg >= 2;
   std::vector<Rs13Hashes> hs;
   std::vector<uint8_t> seg_cvs;
-  auto write = [&](size_t j, const uint8_t *const par[3], size_t shard) {
-    bool ok = write_file(t2_seg(dir, j), m.p + j * S, std::min(S, m.n - j * S));
-    for (size_t p = 0; p < kParity; ++p) ok = ok && write_file(t2_par(dir, j, p), par[p], shard);
-    return ok;
+  auto write = [&](size_t j, size_t file, const uint8_t *const par[3], size_t shard) {
+    if (file == 0) return write_file(t2_seg(dir, j), m.p + j * S, std::min(S, m.n - j * S));
+    return write_file(t2_par(dir, j, file - 1), par[file - 1], shard);
   };
   int rc = rs13_segments(nseg, cv_hash, &seg_cvs, &hs, write);
   if (rc) return rc;
@@ -351,23 +439,10 @@ int Commit::tier3(std::string *out_dir) {
   };
   std::atomic<bool> write_ok{true};
   std::atomic<bool> stop{false};  // a failed context stops the others before their next block
-  // pipeline timeline, measurement build only (BFRS_TRACE): one line on stderr
-  const bool trace = BFRS_AB_KNOB("BFRS_TRACE") != nullptr;
-  const auto t_origin = std::chrono::steady_clock::now();
-  std::mutex trace_mu;
-  std::vector<std::string> trace_ev;
-  auto now_us = [&] {
-    return (long long)std::chrono::duration_cast<std::chrono::microseconds>(
-               std::chrono::steady_clock::now() - t_origin)
-        .count();
-  };
-  auto event = [&](const char *what, size_t b, long long t0) {
-    if (!trace) return;
-    const long long t1 = now_us();
-    std::lock_guard<std::mutex> l(trace_mu);
-    trace_ev.push_back(std::string("[\"") + what + "\"," + std::to_string(b) + "," +
-                       std::to_string(t0) + "," + std::to_string(t1 - t0) + "]");
-  };
+  PipeTrace pt;
+  const bool trace = pt.on;
+  auto now_us = [&] { return pt.now_us(); };
+  auto event = [&](const char *what, size_t b, long long t0) { pt.event(what, b, t0); };
   // The pipeline of one context over its blocks `mine` (in file order): its
   // own staging arenas, stream, filler and writers; `thr` host threads for
   // the copies.  Every result lands in a per-block slot (seg_cvs ranges,
@@ -558,12 +633,7 @@ int Commit::tier3(std::string *out_dir) {
     run(0);
     for (auto &t : others) t.join();
   }
-  if (trace) {
-    std::string line = "bfrs_commit_trace {\"thr\":" + std::to_string(threads) + ",\"events_us\":[";
-    for (size_t i = 0; i < trace_ev.size(); ++i) line += (i ? "," : "") + trace_ev[i];
-    line += "],\"total_us\":" + std::to_string(now_us()) + "}\n";
-    std::fputs(line.c_str(), stderr);
-  }
+  pt.print("bfrs_commit_trace", threads);
   for (size_t d = 0; d < n; ++d)
     if (rcs[d]) return set_error(rcs[d], n == 1 ? errs[d] : "context " + std::to_string(d) + ": " + errs[d]);
   if (!write_ok) return io_error("write tier-3 shards");

@@ -40,11 +40,15 @@ int Arena::reserve(size_t slot_bytes, size_t n, unsigned parts) {
 
 int BlockArena::reserve(size_t slot_bytes) {
   int rc = dev.reserve(slot_bytes, kBlockSegments + kParity, kArenaDevice);
-  if (!rc) rc = ring.reserve(slot_bytes, 2 * kRingThreads, kArenaHost);
   if (!rc) rc = out.reserve(slot_bytes, kOutSlots, kArenaHost);
+  return rc ? rc : reserve_ring(slot_bytes);
+}
+
+int BlockArena::reserve_ring(size_t slot_bytes, size_t slots) {
+  int rc = ring.reserve(slot_bytes, slots, kArenaHost);
   if (rc) return rc;
   if (!h2d) HIP_TRY(hipStreamCreateWithFlags(&h2d, hipStreamNonBlocking));
-  while (ring_ev.size() < 2 * kRingThreads) {
+  while (ring_ev.size() < ring.nslots) {
     hipEvent_t e = nullptr;
     HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     ring_ev.push_back(e);

@@ -55,7 +55,9 @@ struct BlockArena {
   BlockArena(const BlockArena &) = delete;
   BlockArena &operator=(const BlockArena &) = delete;
   ~BlockArena();
-  int reserve(size_t slot_bytes);  // on the context's device
+  int reserve(size_t slot_bytes);  // all of it, on the context's device
+  // the ring (at least `slots` slots), its stream and events only
+  int reserve_ring(size_t slot_bytes, size_t slots = 2 * kRingThreads);
 };
 
 // Device BLAKE3 -> lowercase hex digests (on `stream`, default the context's;
@@ -68,7 +70,8 @@ int gpu_hash_hex(bfrs_ctx *ctx, const std::vector<const uint8_t *> &d_msgs,
 
 // The context's staging arenas (Context::staging): archive calls on one
 // context take `mu` for their duration.  The RS(1,3) tiers' commit uses
-// a[0..1] as round arenas and a[2..3] as parity buffers.  Tier 3: repair and
+// a[0..1] as device round buffers, blk's ring to fill them and a[2..3] as
+// pinned parity buffers.  Tier 3: repair and
 // health check use `blk`; the commit uses blk.dev and blk2 as its two device
 // block buffers, blk's ring to fill them, blk.out slots [0,3) / [3,6) as the
 // pinned parity of the blocks being written, and `filled[i]` to mark a
