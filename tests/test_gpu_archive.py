@@ -511,6 +511,62 @@ def test_archive_concurrent_readers(ctx, bfrs, tmp_path):
     assert st["recovered_segments"] >= 2
 
 
+def test_handles_share_the_segment_pool(ctx, bfrs, tmp_path):
+    # the context pins one pool of segment buffers per segment size and lends
+    # it to every handle (archive.cpp segment_pool): two handles of the same
+    # segment size read side by side on 3 threads each, a third handle of
+    # another segment size beside them, handles close while others read, and
+    # a commit and a repair run on the same context meanwhile; every byte right
+    import threading
+    for sub in ("a", "b"):
+        (tmp_path / sub).mkdir()
+    a_dir, a_d = _tier3(ctx, bfrs, tmp_path / "a", seed=11)
+    b_dir, b_d = _tier3(ctx, bfrs, tmp_path / "b", nseg_full=35, tail=4242, seed=12)
+    n_c = 9 * (SEG // 2) + 778
+    c_path, c_d = _file(tmp_path, n_c, seed=13, name="c.bin")
+    c_dir = bfrs.commit(ctx, c_path, str(tmp_path / "c_archive"), segment_size=SEG // 2, tier=3)
+    _flip(os.path.join(a_dir, "blocks", "block_1", "segments", "segment_7.dat"))
+    _flip(os.path.join(b_dir, "blocks", "block_0", "segments", "segment_29.dat"))
+    os.remove(os.path.join(c_dir, "blocks", "block_0", "segments", "segment_3.dat"))
+    errors = []
+
+    def reader(adir, d, seed, cache):
+        rng = np.random.default_rng(seed)
+        try:
+            with bfrs.Archive(ctx, adir, cache_segments=cache) as h:
+                for _ in range(40):
+                    off = int(rng.integers(0, d.size))
+                    ln = int(rng.integers(1, 3 * SEG))
+                    if h.read(off, ln) != d[off:off + ln].tobytes():
+                        errors.append((adir, seed, off, ln))
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    def side_work():
+        try:
+            p, d = _file(tmp_path, 31 * SEG + 10, seed=14, name="side.bin")
+            sdir = bfrs.commit(ctx, p, str(tmp_path / "side"), segment_size=SEG, tier=3)
+            _flip(os.path.join(sdir, "blocks", "block_0", "segments", "segment_0.dat"))
+            if bfrs.repair(ctx, sdir)["segments_repaired"] != 1:
+                errors.append("side repair")
+            with bfrs.Archive(ctx, sdir) as h:
+                if h.read(0, d.size) != d.tobytes():
+                    errors.append("side read")
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    jobs = ([(a_dir, a_d, s, 4 + s) for s in range(3)] + [(b_dir, b_d, 10 + s, 3) for s in range(3)]
+            + [(c_dir, c_d, 20 + s, 5) for s in range(2)])
+    ts = [threading.Thread(target=reader, args=j) for j in jobs] + [threading.Thread(target=side_work)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert errors == []
+    with bfrs.Archive(ctx, a_dir, cache_segments=8) as h:  # after all closed: the pool again
+        assert h.read(0, a_d.size) == a_d.tobytes()
+
+
 def test_repair_tier3_parity_only(ctx, bfrs, tmp_path):
     adir, d = _tier3(ctx, bfrs, tmp_path)
     pdir = os.path.join(adir, "blocks", "block_1", "parity")
