@@ -849,21 +849,23 @@ def repair(ctx, archive_dir: str) -> dict:
 def health_check(ctx: Context, archive_dir: str) -> dict:
     """FileStore::health_check (src/filestore/health.rs:111-438), intended semantics."""
     import json
-    need = _sz()
-    _check(lib().bfrs_health_check(ctx.handle, os.fsencode(archive_dir), None, 0,
-                                   ctypes.byref(need)))
-    out = ctypes.create_string_buffer(need.value)
-    _check(lib().bfrs_health_check(ctx.handle, os.fsencode(archive_dir), out, len(out),
-                                   ctypes.byref(need)))
-    return json.loads(out.value.decode())
+    return json.loads(_json_call(lib().bfrs_health_check, ctx.handle, os.fsencode(archive_dir)))
+
+
+_JSON_GUESS = 1 << 18
 
 
 def _json_call(f, *args) -> str:
-    """Two-call JSON output convention (*needed = length + 1)."""
+    """JSON output convention (*needed = length + 1; a short buffer gets a
+    truncated report).  One call into a buffer that fits any usual report; a
+    second only if it was too short — a size query first would run the whole
+    check (every shard hashed) twice."""
     need = _sz()
-    _check(f(*args, None, 0, ctypes.byref(need)))
-    out = ctypes.create_string_buffer(need.value)
+    out = ctypes.create_string_buffer(_JSON_GUESS)
     _check(f(*args, out, len(out), ctypes.byref(need)))
+    if need.value > len(out):
+        out = ctypes.create_string_buffer(need.value)
+        _check(f(*args, out, len(out), ctypes.byref(need)))
     return out.value.decode()
 
 

@@ -64,35 +64,6 @@ struct Mapped {
   }
 };
 
-// Pipeline timeline, measurement build only (BFRS_TRACE): [what, unit,
-// start us, duration us] events, one line on stderr at the end.  `on` is
-// false in libbfrs.so (one branch per event).
-struct PipeTrace {
-  const bool on = BFRS_AB_KNOB("BFRS_TRACE") != nullptr;
-  const std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
-  std::mutex mu;
-  std::vector<std::string> ev;
-  long long now_us() const {
-    return (long long)std::chrono::duration_cast<std::chrono::microseconds>(
-               std::chrono::steady_clock::now() - t0)
-        .count();
-  }
-  void event(const char *what, size_t unit, long long start) {
-    if (!on) return;
-    const long long end = now_us();
-    std::lock_guard<std::mutex> l(mu);
-    ev.push_back(std::string("[\"") + what + "\"," + std::to_string(unit) + "," +
-                 std::to_string(start) + "," + std::to_string(end - start) + "]");
-  }
-  void print(const char *name, int threads) {
-    if (!on) return;
-    std::string line = std::string(name) + " {\"thr\":" + std::to_string(threads) + ",\"events_us\":[";
-    for (size_t i = 0; i < ev.size(); ++i) line += (i ? "," : "") + ev[i];
-    line += "],\"total_us\":" + std::to_string(now_us()) + "}\n";
-    std::fputs(line.c_str(), stderr);
-  }
-};
-
 struct Commit {
   bfrs_ctx *ctx;
   std::string root, name;
@@ -1238,26 +1209,50 @@ int repair_blocks(bfrs_ctx *ctx, const Geometry &g, const std::vector<size_t> &m
   StagingCache &sc = staging(ctx);
   std::lock_guard<std::mutex> staging_lock(sc.mu);
   BlockArena &a = sc.blk;
+  PipeTrace pt;
+  struct Print {  // the timeline on every exit (measurement build)
+    PipeTrace &pt;
+    ~Print() { pt.print("bfrs_repair_trace", hw_threads()); }
+  } print{pt};
   int rc;
+  // a block's restored segments are written (from the arena's out slots
+  // [0, 3)) while the next block loads; joined before the next restore
+  // reuses those slots, and on every exit path
+  std::atomic<bool> write_ok{true};
+  std::atomic<size_t> written{0};
+  BgTask writer;
+  auto finish_writes = [&]() -> int {
+    writer.join();
+    return write_ok ? BFRS_OK : io_error("write restored segment");
+  };
   for (const size_t b : mine) {
     if (stop && stop->load(std::memory_order_relaxed)) break;
     BlockState bs;
-    if ((rc = load_block(ctx, g, b, a, &bs))) return rc;
+    if ((rc = load_block(ctx, g, b, a, &bs, &pt))) return rc;
+    const long long t0 = pt.on ? pt.now_us() : 0;
     ++rep->blocks_checked;
     rep->segments_checked += bs.k;
-    const std::vector<uint8_t> was_ok = bs.seg_ok;
     const size_t parity_bad = kParity - bs.valid_parity();
+    if ((rc = finish_writes())) return rc;
     const int restored = restore_block(ctx, g, a, bs);
     if (restored == BFRS_E_NOT_ENOUGH_SHARDS) {
       ++rep->unrecoverable_blocks;
       continue;
     }
     if (restored < 0) return restored;
-    for (const auto &r : bs.restored) {  // exactly the segments that were damaged
-      if (!write_file(t3_seg(g.dir, b, r.first), r.second, bs.lens[r.first]))
-        return io_error("write restored segment");
-      ++rep->segments_repaired;
-    }
+    pt.event("restore", b, t0);
+    // exactly the segments that were damaged, one file per thread
+    writer.start([&, b, files = bs.restored, lens = bs.lens] {
+      const long long t1 = pt.on ? pt.now_us() : 0;
+      parallel_for(files.size(), int(files.size()), [&](size_t j) {
+        const size_t s = files[j].first;
+        if (write_file(t3_seg(g.dir, b, s), files[j].second, lens[s]))
+          ++written;
+        else
+          write_ok = false;
+      });
+      pt.event("write", b, t1);
+    });
     if (parity_bad) {
       const std::vector<uint8_t> par_was = bs.par_ok;
       if ((rc = reencode_parity(ctx, g, a, bs))) return rc;
@@ -1267,7 +1262,9 @@ int repair_blocks(bfrs_ctx *ctx, const Geometry &g, const std::vector<size_t> &m
       rep->parity_repaired += parity_bad;
     }
   }
-  return BFRS_OK;
+  rc = finish_writes();
+  rep->segments_repaired += written;
+  return rc;
 }
 
 // Tier-3 blocks dealt round-robin over the contexts (block b to context
@@ -1429,10 +1426,15 @@ int health_report(bfrs_ctx *ctx, const char *archive_dir, Json *out) {
     StagingCache &sc = staging(ctx);
     std::lock_guard<std::mutex> staging_lock(sc.mu);
     BlockArena &a = sc.blk;
+    PipeTrace pt;
+    struct Print {  // the timeline on every exit (measurement build)
+      PipeTrace &pt;
+      ~Print() { pt.print("bfrs_health_trace", hw_threads()); }
+    } print{pt};
     for (const auto &kv : g.mf.blocks) {
       const size_t b = size_t(kv.first);
       BlockState bs;
-      if ((rc = load_block(ctx, g, b, a, &bs))) return rc;
+      if ((rc = load_block(ctx, g, b, a, &bs, &pt))) return rc;
       const std::string bn = "block_" + std::to_string(b);
       for (size_t s = 0; s < bs.k; ++s)
         if (!bs.seg_ok[s]) {

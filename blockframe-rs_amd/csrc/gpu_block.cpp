@@ -106,7 +106,10 @@ size_t BlockState::valid_parity() const {
   return n;
 }
 
-int load_block(bfrs_ctx *ctx, const Geometry &g, size_t b, BlockArena &a, BlockState *st) {
+int load_block(bfrs_ctx *ctx, const Geometry &g, size_t b, BlockArena &a, BlockState *st,
+               PipeTrace *pt) {
+  const bool tr = pt && pt->on;
+  const long long t0 = tr ? pt->now_us() : 0;
   auto it = g.mf.blocks.find(int64_t(b));
   if (it == g.mf.blocks.end()) return set_error(BFRS_E_WRAPPER, "manifest has no block " + std::to_string(b));
   const BlockHashes &bh = it->second;
@@ -155,9 +158,13 @@ int load_block(bfrs_ctx *ctx, const Geometry &g, size_t b, BlockArena &a, BlockS
       if (!hip_ok(hipEventRecord(a.ring_ev[r], a.h2d))) return;
     }
   });
+  if (tr) pt->event("read", b, t0);
+  const long long t1 = tr ? pt->now_us() : 0;
   // the copies land before the hash takes hash_mu (and before any error
   // return: nothing may still be reading the ring)
   const hipError_t sync = hipStreamSynchronize(a.h2d);
+  if (tr) pt->event("h2d_tail", b, t1);
+  const long long t2 = tr ? pt->now_us() : 0;
   if (hip_rc.load() != int(hipSuccess))
     return hip_error(hipError_t(hip_rc.load()), "block shard H2D through the ring");
   if (sync != hipSuccess) return hip_error(sync, "hipStreamSynchronize (block ring)");
@@ -171,6 +178,7 @@ int load_block(bfrs_ctx *ctx, const Geometry &g, size_t b, BlockArena &a, BlockS
     }
   std::vector<std::string> hex;
   if ((rc = gpu_hash_hex(ctx, msgs, lens, &hex))) return rc;
+  if (tr) pt->event("hash", b, t2);
   st->seg_ok.assign(k, 0);
   st->par_ok.assign(kParity, 0);
   for (size_t j = 0; j < idx.size(); ++j) {

@@ -10,6 +10,9 @@
 // restored bytes are re-hashed on the device before anything reaches disk.
 #pragma once
 
+#include <atomic>
+#include <chrono>
+#include <cstdio>
 #include <cstddef>
 #include <cstdint>
 #include <map>
@@ -19,6 +22,7 @@
 #include <vector>
 
 #include "archive_io.hpp"
+#include "knobs.hpp"
 #include "runtime.hpp"
 
 namespace bfrs {
@@ -36,6 +40,35 @@ struct Arena {
   int reserve(size_t slot_bytes, size_t n, unsigned parts = kArenaBoth);
   uint8_t *hs(size_t i) const { return h + i * slot; }
   uint8_t *ds(size_t i) const { return d + i * slot; }
+};
+
+// Pipeline timeline, measurement build only (BFRS_TRACE): [what, unit,
+// start us, duration us] events, one line on stderr at the end.  `on` is
+// false in libbfrs.so (one branch per event).
+struct PipeTrace {
+  const bool on = BFRS_AB_KNOB("BFRS_TRACE") != nullptr;
+  const std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+  std::mutex mu;
+  std::vector<std::string> ev;
+  long long now_us() const {
+    return (long long)std::chrono::duration_cast<std::chrono::microseconds>(
+               std::chrono::steady_clock::now() - t0)
+        .count();
+  }
+  void event(const char *what, size_t unit, long long start) {
+    if (!on) return;
+    const long long end = now_us();
+    std::lock_guard<std::mutex> l(mu);
+    ev.push_back(std::string("[\"") + what + "\"," + std::to_string(unit) + "," +
+                 std::to_string(start) + "," + std::to_string(end - start) + "]");
+  }
+  void print(const char *name, int threads) {
+    if (!on) return;
+    std::string line = std::string(name) + " {\"thr\":" + std::to_string(threads) + ",\"events_us\":[";
+    for (size_t i = 0; i < ev.size(); ++i) line += (i ? "," : "") + ev[i];
+    line += "],\"total_us\":" + std::to_string(now_us()) + "}\n";
+    std::fputs(line.c_str(), stderr);
+  }
 };
 
 // A tier-3 block's staging: HBM slots for the whole block (k segments + 3
@@ -113,7 +146,8 @@ struct BlockState {
 // the shard size) into its HBM slots and verifies every shard against the
 // manifest with the device BLAKE3.  Each shard's H2D is queued as soon as
 // its file is read, so the copies overlap the other reads.
-int load_block(bfrs_ctx *ctx, const Geometry &g, size_t b, BlockArena &a, BlockState *st);
+int load_block(bfrs_ctx *ctx, const Geometry &g, size_t b, BlockArena &a, BlockState *st,
+               PipeTrace *pt = nullptr);
 // RS(k,3)-decodes every damaged segment into its own device slot, re-verifies
 // the restored bytes on the device and copies them to host memory: to
 // host_out[s] where given (pinned, >= lens[s] bytes), else to the arena's out

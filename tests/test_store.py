@@ -73,3 +73,13 @@ def test_get_all_fails_on_an_entry_without_manifest(bfrs, tmp_path):
 def test_missing_store_root_is_an_error(bfrs, tmp_path):
     with pytest.raises(bfrs.BfrsError):
         bfrs.FileStore(str(tmp_path / "nope")).get_all()
+
+
+def test_json_reports_longer_than_the_first_buffer(bfrs, tmp_path, monkeypatch):
+    # the binding makes one call into a guessed buffer and a second only when
+    # the report did not fit (a size query first would run a health check twice)
+    store = bfrs.FileStore(_setup_test_archive(tmp_path))
+    want = store.get_all()
+    monkeypatch.setattr(bfrs, "_JSON_GUESS", 8)
+    assert store.get_all() == want
+    assert store.find(want[0]["file_name"])["dir"] == want[0]["dir"]
