@@ -679,7 +679,23 @@ struct PinnedPool {
     std::lock_guard<std::mutex> g(mu);
     free_.push_back(p);
   }
+  // unpins idle buffers beyond `keep` (a handle closing: what a long-lived
+  // context retains is bounded, not the largest cache it ever served)
+  void trim(size_t keep) {
+    std::vector<uint8_t *> drop;
+    {
+      std::lock_guard<std::mutex> g(mu);
+      while (free_.size() > keep) {
+        drop.push_back(free_.back());
+        free_.pop_back();
+        all_.erase(std::find(all_.begin(), all_.end(), drop.back()));
+      }
+    }
+    for (uint8_t *p : drop) (void)hipHostFree(p);
+  }
 };
+// idle pinned segment buffers a context keeps per segment size: 2 GiB, >= 8
+inline size_t pool_keep(size_t slot) { return std::max<size_t>(8, (size_t(2) << 30) / slot); }
 
 // The context's pool for buffers of `bytes` (StagingCache::seg_pools).
 std::shared_ptr<PinnedPool> segment_pool(bfrs_ctx *ctx, size_t bytes) {
@@ -838,6 +854,7 @@ struct bfrs_archive {
     for (auto &w : workers)
       if (w.joinable()) w.join();
     cache.clear();
+    if (pool) pool->trim(pool_keep(pool->slot));
     trace.print();
   }
 

@@ -373,9 +373,10 @@ typedef struct {
   uint64_t prefetched;          /* segments loaded + verified ahead of the reader */
 } bfrs_archive_stats;
 /* Memory: cached segments live in pinned buffers drawn from a pool the
- * context keeps per segment size and shares between its handles (they stay
- * pinned until bfrs_close: about cache_segments + 8 buffers per handle open
- * at the same time); a tier-3 handle with prefetch also allocates a
+ * context keeps per segment size and shares between its handles (about
+ * cache_segments + 8 buffers per handle open at the same time; when a handle
+ * closes, idle buffers beyond 2 GiB per segment size are unpinned, the rest
+ * stay for the next handle until bfrs_close); a tier-3 handle with prefetch also allocates a
  * block arena (33 HBM segment slots, 22 pinned) at open, on a prefetch
  * thread, and one HBM segment buffer per verification lane (prefetch workers
  * + 1).  Both are freed by bfrs_archive_close. */
