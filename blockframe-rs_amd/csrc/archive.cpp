@@ -1214,6 +1214,57 @@ int bfrs_commit_multi(bfrs_ctx *const *ctxs, size_t n_ctx, const char *file_path
 }  // extern "C"
 
 namespace {
+// Runs body(block state) over the tier-3 blocks `blocks` in order, reading
+// block i + 1 through the ring into the other device buffer (sc.blk.dev /
+// sc.blk2) while block i is verified and handled.  Under sc.mu, on the
+// context's device.  `stop` (may be NULL) ends the loop before a block.
+template <class Body>
+int for_each_block(bfrs_ctx *ctx, const Geometry &g, StagingCache &sc,
+                   const std::vector<size_t> &blocks, PipeTrace &pt,
+                   const std::atomic<bool> *stop, Body body) {
+  if (blocks.empty()) return BFRS_OK;
+  BlockArena &a = sc.blk;
+  // sized for the largest block up front: the reader thread must not regrow
+  // buffers the verify and the body are using
+  size_t shard = 0;
+  for (size_t b : blocks) shard = std::max(shard, g.block_shard(b));
+  int rc = a.reserve(shard);
+  if (!rc) rc = sc.blk2.reserve(shard, kBlockSegments + kParity, kArenaDevice);
+  if (!rc) rc = sc.commit_events();  // the two end-of-block markers
+  if (rc) return rc;
+  Arena *dev[2] = {&a.dev, &sc.blk2};
+  BlockState st[2];
+  struct RingSync {  // on every exit nothing of this call still copies into the buffers
+    BlockArena &a;
+    ~RingSync() {
+      if (a.h2d) (void)hipStreamSynchronize(a.h2d);
+    }
+  } ring_sync{a};
+  auto reads = [&](size_t i) {
+    return load_block_reads(ctx, g, blocks[i], a, *dev[i % 2], sc.filled[i % 2], &st[i % 2], &pt);
+  };
+  if ((rc = reads(0))) return rc;
+  for (size_t i = 0; i < blocks.size(); ++i) {
+    if (stop && stop->load(std::memory_order_relaxed)) break;
+    int next_rc = BFRS_OK;
+    std::string next_err;
+    {
+      BgTask reader;
+      if (i + 1 < blocks.size())
+        reader.start([&, i] {
+          next_rc = reads(i + 1);
+          if (next_rc) next_err = bfrs_last_error();  // thread-local: carried back
+        });
+      rc = load_block_verify(ctx, g, &st[i % 2], sc.filled[i % 2], &pt);
+      if (!rc) rc = body(st[i % 2]);
+      reader.join();
+    }
+    if (rc) return rc;
+    if (next_rc) return set_error(next_rc, next_err);
+  }
+  return BFRS_OK;
+}
+
 // repair_blocked (health.rs:642-765), intended semantics, over the blocks
 // `mine` of a tier-3 archive on one context; counts land in *rep.
 // `stop`: set when another context's repair failed (repair_tier3); the
@@ -1231,7 +1282,6 @@ int repair_blocks(bfrs_ctx *ctx, const Geometry &g, const std::vector<size_t> &m
     PipeTrace &pt;
     ~Print() { pt.print("bfrs_repair_trace", hw_threads()); }
   } print{pt};
-  int rc;
   // a block's restored segments are written (from the arena's out slots
   // [0, 3)) while the next block loads; joined before the next restore
   // reuses those slots, and on every exit path
@@ -1242,19 +1292,18 @@ int repair_blocks(bfrs_ctx *ctx, const Geometry &g, const std::vector<size_t> &m
     writer.join();
     return write_ok ? BFRS_OK : io_error("write restored segment");
   };
-  for (const size_t b : mine) {
-    if (stop && stop->load(std::memory_order_relaxed)) break;
-    BlockState bs;
-    if ((rc = load_block(ctx, g, b, a, &bs, &pt))) return rc;
+  int rc = for_each_block(ctx, g, sc, mine, pt, stop, [&](BlockState &bs) -> int {
+    const size_t b = bs.b;
     const long long t0 = pt.on ? pt.now_us() : 0;
     ++rep->blocks_checked;
     rep->segments_checked += bs.k;
     const size_t parity_bad = kParity - bs.valid_parity();
-    if ((rc = finish_writes())) return rc;
+    int rc = finish_writes();
+    if (rc) return rc;
     const int restored = restore_block(ctx, g, a, bs);
     if (restored == BFRS_E_NOT_ENOUGH_SHARDS) {
       ++rep->unrecoverable_blocks;
-      continue;
+      return BFRS_OK;
     }
     if (restored < 0) return restored;
     pt.event("restore", b, t0);
@@ -1278,10 +1327,11 @@ int repair_blocks(bfrs_ctx *ctx, const Geometry &g, const std::vector<size_t> &m
           return io_error("write parity");
       rep->parity_repaired += parity_bad;
     }
-  }
-  rc = finish_writes();
+    return BFRS_OK;
+  });
+  const int wrc = finish_writes();
   rep->segments_repaired += written;
-  return rc;
+  return rc ? rc : wrc;
 }
 
 // Tier-3 blocks dealt round-robin over the contexts (block b to context
@@ -1440,18 +1490,18 @@ int health_report(bfrs_ctx *ctx, const char *archive_dir, Json *out) {
     else ++unrecoverable;
   };
   if (g.mf.tier == 3) {
+    HIP_TRY(hipSetDevice(ctx->impl.device));
     StagingCache &sc = staging(ctx);
     std::lock_guard<std::mutex> staging_lock(sc.mu);
-    BlockArena &a = sc.blk;
     PipeTrace pt;
     struct Print {  // the timeline on every exit (measurement build)
       PipeTrace &pt;
       ~Print() { pt.print("bfrs_health_trace", hw_threads()); }
     } print{pt};
-    for (const auto &kv : g.mf.blocks) {
-      const size_t b = size_t(kv.first);
-      BlockState bs;
-      if ((rc = load_block(ctx, g, b, a, &bs, &pt))) return rc;
+    std::vector<size_t> blocks;
+    for (const auto &kv : g.mf.blocks) blocks.push_back(size_t(kv.first));
+    rc = for_each_block(ctx, g, sc, blocks, pt, nullptr, [&](BlockState &bs) -> int {
+      const size_t b = bs.b;
       const std::string bn = "block_" + std::to_string(b);
       for (size_t s = 0; s < bs.k; ++s)
         if (!bs.seg_ok[s]) {
@@ -1464,7 +1514,9 @@ int health_report(bfrs_ctx *ctx, const char *archive_dir, Json *out) {
           (exists(t3_par(g.dir, b, p)) ? corrupt_parity : missing_parity).a.push_back(Json::str(n));
         }
       classify(bs.damaged_segments(), bs.valid_parity());
-    }
+      return BFRS_OK;
+    });
+    if (rc) return rc;
   } else {
     bfrs_archive ar;
     ar.ctx = ctx;

@@ -59,6 +59,7 @@ int BlockArena::reserve_ring(size_t slot_bytes, size_t slots) {
 BlockArena::~BlockArena() {
   if (h2d) (void)hipStreamSynchronize(h2d);
   for (hipEvent_t e : ring_ev) (void)hipEventDestroy(e);
+  if (done) (void)hipEventDestroy(done);
   if (h2d) (void)hipStreamDestroy(h2d);
 }
 
@@ -106,8 +107,8 @@ size_t BlockState::valid_parity() const {
   return n;
 }
 
-int load_block(bfrs_ctx *ctx, const Geometry &g, size_t b, BlockArena &a, BlockState *st,
-               PipeTrace *pt) {
+int load_block_reads(bfrs_ctx *ctx, const Geometry &g, size_t b, BlockArena &a, Arena &dev,
+                     hipEvent_t done, BlockState *st, PipeTrace *pt) {
   const bool tr = pt && pt->on;
   const long long t0 = tr ? pt->now_us() : 0;
   auto it = g.mf.blocks.find(int64_t(b));
@@ -116,6 +117,7 @@ int load_block(bfrs_ctx *ctx, const Geometry &g, size_t b, BlockArena &a, BlockS
   st->b = b;
   st->k = bh.segments.size();
   st->shard = g.block_shard(b);
+  st->dev = &dev;
   st->restored.clear();
   for (auto &p : st->parity_host) p = nullptr;
   const size_t k = st->k, shard = st->shard;
@@ -126,12 +128,14 @@ int load_block(bfrs_ctx *ctx, const Geometry &g, size_t b, BlockArena &a, BlockS
   // read handle's prefetch thread or an API thread bound to another GPU
   HIP_TRY(hipSetDevice(c.device));
   int rc = a.reserve(shard);
+  if (!rc) rc = dev.reserve(shard, kBlockSegments + kParity, kArenaDevice);
   if (rc) return rc;
   // thread w reads shards w, w + nthr, ... into its two ring slots in turn;
   // each shard's H2D goes as soon as its read ends
   const size_t n = k + kParity;
   const size_t nthr = std::min<size_t>(kRingThreads, size_t(std::max(1, hw_threads())));
-  std::vector<uint8_t> readable(n, 0);
+  std::vector<uint8_t> &readable = st->readable;
+  readable.assign(n, 0);
   std::atomic<int> hip_rc{int(hipSuccess)};
   auto hip_ok = [&](hipError_t e) {
     int ok = int(hipSuccess);
@@ -154,31 +158,41 @@ int load_block(bfrs_ctx *ctx, const Geometry &g, size_t b, BlockArena &a, BlockS
         readable[i] = read_file_into(t3_par(g.dir, b, i - k), h, a.ring.slot) == (long long)shard;
       }
       if (!readable[i]) continue;  // excluded from the hash and the decode: no copy
-      if (!hip_ok(hipMemcpyAsync(a.dev.ds(i), h, shard, hipMemcpyHostToDevice, a.h2d))) return;
+      if (!hip_ok(hipMemcpyAsync(dev.ds(i), h, shard, hipMemcpyHostToDevice, a.h2d))) return;
       if (!hip_ok(hipEventRecord(a.ring_ev[r], a.h2d))) return;
     }
   });
+  if (hip_rc.load() == int(hipSuccess)) hip_ok(hipEventRecord(done, a.h2d));
   if (tr) pt->event("read", b, t0);
-  const long long t1 = tr ? pt->now_us() : 0;
-  // the copies land before the hash takes hash_mu (and before any error
-  // return: nothing may still be reading the ring)
-  const hipError_t sync = hipStreamSynchronize(a.h2d);
-  if (tr) pt->event("h2d_tail", b, t1);
-  const long long t2 = tr ? pt->now_us() : 0;
-  if (hip_rc.load() != int(hipSuccess))
+  if (hip_rc.load() != int(hipSuccess)) {
+    (void)hipStreamSynchronize(a.h2d);  // nothing may still be reading the ring
     return hip_error(hipError_t(hip_rc.load()), "block shard H2D through the ring");
-  if (sync != hipSuccess) return hip_error(sync, "hipStreamSynchronize (block ring)");
+  }
+  return BFRS_OK;
+}
+
+int load_block_verify(bfrs_ctx *ctx, const Geometry &g, BlockState *st, hipEvent_t done,
+                      PipeTrace *pt) {
+  const bool tr = pt && pt->on;
+  const long long t1 = tr ? pt->now_us() : 0;
+  // the block's copies land before the hash takes hash_mu
+  HIP_TRY(hipEventSynchronize(done));
+  if (tr) pt->event("h2d_tail", st->b, t1);
+  const long long t2 = tr ? pt->now_us() : 0;
+  const BlockHashes &bh = g.mf.blocks.at(int64_t(st->b));
+  const size_t k = st->k, n = k + kParity;
   std::vector<const uint8_t *> msgs;
   std::vector<size_t> lens, idx;
   for (size_t i = 0; i < n; ++i)
-    if (readable[i]) {
-      msgs.push_back(a.dev.ds(i));
-      lens.push_back(i < k ? st->lens[i] : shard);
+    if (st->readable[i]) {
+      msgs.push_back(st->dev->ds(i));
+      lens.push_back(i < k ? st->lens[i] : st->shard);
       idx.push_back(i);
     }
   std::vector<std::string> hex;
-  if ((rc = gpu_hash_hex(ctx, msgs, lens, &hex))) return rc;
-  if (tr) pt->event("hash", b, t2);
+  int rc = gpu_hash_hex(ctx, msgs, lens, &hex);
+  if (rc) return rc;
+  if (tr) pt->event("hash", st->b, t2);
   st->seg_ok.assign(k, 0);
   st->par_ok.assign(kParity, 0);
   for (size_t j = 0; j < idx.size(); ++j) {
@@ -189,6 +203,16 @@ int load_block(bfrs_ctx *ctx, const Geometry &g, size_t b, BlockArena &a, BlockS
       st->par_ok[i - k] = hex[j] == bh.parity[i - k];
   }
   return BFRS_OK;
+}
+
+int load_block(bfrs_ctx *ctx, const Geometry &g, size_t b, BlockArena &a, BlockState *st,
+               PipeTrace *pt) {
+  if (!a.done) {
+    HIP_TRY(hipSetDevice(ctx->impl.device));
+    HIP_TRY(hipEventCreateWithFlags(&a.done, hipEventDisableTiming));
+  }
+  int rc = load_block_reads(ctx, g, b, a, a.dev, a.done, st, pt);
+  return rc ? rc : load_block_verify(ctx, g, st, a.done, pt);
 }
 
 int restore_block(bfrs_ctx *ctx, const Geometry &g, BlockArena &a, BlockState &st,
@@ -205,10 +229,10 @@ int restore_block(bfrs_ctx *ctx, const Geometry &g, BlockArena &a, BlockState &s
   std::vector<const uint8_t *> orig(k), rec(kParity);
   std::vector<uint8_t *> out(k);
   for (size_t s = 0; s < k; ++s) {
-    orig[s] = st.seg_ok[s] ? a.dev.ds(s) : nullptr;
-    out[s] = a.dev.ds(s);  // written only where erased: the restored segment lands in its own slot
+    orig[s] = st.seg_ok[s] ? st.dev->ds(s) : nullptr;
+    out[s] = st.dev->ds(s);  // written only where erased: the restored segment lands in its own slot
   }
-  for (size_t p = 0; p < kParity; ++p) rec[p] = st.par_ok[p] ? a.dev.ds(k + p) : nullptr;
+  for (size_t p = 0; p < kParity; ++p) rec[p] = st.par_ok[p] ? st.dev->ds(k + p) : nullptr;
   Context &c = ctx->impl;
   const uint32_t kk = uint32_t(k);
   int rc = decode_batch_on(ctx, 1, &kk, kParity, st.shard, orig.data(), rec.data(), out.data(),
@@ -219,7 +243,7 @@ int restore_block(bfrs_ctx *ctx, const Geometry &g, BlockArena &a, BlockState &s
   std::vector<size_t> lens, idx;
   for (size_t s = 0; s < k; ++s)
     if (!st.seg_ok[s]) {
-      msgs.push_back(a.dev.ds(s));
+      msgs.push_back(st.dev->ds(s));
       lens.push_back(st.lens[s]);
       idx.push_back(s);
     }
@@ -236,7 +260,7 @@ int restore_block(bfrs_ctx *ctx, const Geometry &g, BlockArena &a, BlockState &s
   for (size_t j = 0; j < idx.size(); ++j) {
     const size_t s = idx[j];
     uint8_t *dst = host_out && (*host_out)[s] ? (*host_out)[s] : a.out.hs(j);
-    HIP_TRY(hipMemcpyAsync(dst, a.dev.ds(s), st.lens[s], hipMemcpyDeviceToHost, c.stream));
+    HIP_TRY(hipMemcpyAsync(dst, st.dev->ds(s), st.lens[s], hipMemcpyDeviceToHost, c.stream));
     st.restored.emplace_back(s, dst);
   }
   HIP_TRY(hipStreamSynchronize(c.stream));
@@ -249,8 +273,8 @@ int reencode_parity(bfrs_ctx *ctx, const Geometry &g, BlockArena &a, BlockState 
   if (st.damaged_segments()) return set_error(BFRS_E_WRAPPER, "re-encode needs whole data");
   std::vector<const uint8_t *> orig(k);
   std::vector<uint8_t *> rec(kParity);
-  for (size_t s = 0; s < k; ++s) orig[s] = a.dev.ds(s);
-  for (size_t p = 0; p < kParity; ++p) rec[p] = a.dev.ds(k + p);
+  for (size_t s = 0; s < k; ++s) orig[s] = st.dev->ds(s);
+  for (size_t p = 0; p < kParity; ++p) rec[p] = st.dev->ds(k + p);
   Context &c = ctx->impl;
   const uint32_t kk = uint32_t(k);
   int rc = encode_batch_on(ctx, 1, &kk, kParity, st.shard, orig.data(), rec.data(), c.stream);
@@ -264,8 +288,8 @@ int reencode_parity(bfrs_ctx *ctx, const Geometry &g, BlockArena &a, BlockState 
     if (hex[p] != bh.parity[p])
       return set_error(BFRS_E_WRAPPER, "re-encoded parity fails the manifest hash");
   for (size_t p = 0; p < kParity; ++p) {
-    HIP_TRY(hipMemcpyAsync(a.out.hs(kParity + p), a.dev.ds(k + p), st.shard, hipMemcpyDeviceToHost,
-                           c.stream));
+    HIP_TRY(hipMemcpyAsync(a.out.hs(kParity + p), st.dev->ds(k + p), st.shard,
+                           hipMemcpyDeviceToHost, c.stream));
     st.parity_host[p] = a.out.hs(kParity + p);
   }
   HIP_TRY(hipStreamSynchronize(c.stream));

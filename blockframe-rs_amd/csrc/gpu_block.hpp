@@ -84,6 +84,7 @@ struct BlockArena {
   Arena dev, ring, out;
   hipStream_t h2d = nullptr;
   std::vector<hipEvent_t> ring_ev;
+  hipEvent_t done = nullptr;  // load_block's end-of-block marker
   BlockArena() = default;
   BlockArena(const BlockArena &) = delete;
   BlockArena &operator=(const BlockArena &) = delete;
@@ -113,7 +114,7 @@ struct StagingCache {
   std::mutex mu;
   Arena a[4];
   BlockArena blk;
-  Arena blk2;
+  Arena blk2;  // also repair's and the health check's second block buffer
   hipEvent_t filled[2] = {nullptr, nullptr};
   int commit_events();  // under mu, on the context's device
   StagingCache() = default;
@@ -132,6 +133,8 @@ StagingCache &staging(bfrs_ctx *ctx);
 // State of tier-3 block b in an Arena: slots [0, k) segments, [k, k+3) parity.
 struct BlockState {
   size_t b = 0, k = 0, shard = 0;
+  Arena *dev = nullptr;                // the HBM slots holding the block
+  std::vector<uint8_t> readable;       // shard files read whole (load_block_reads)
   std::vector<size_t> lens;            // unpadded segment lengths
   std::vector<uint8_t> seg_ok, par_ok;  // present and matching the manifest
   // where restore_block / reencode_parity left host copies: segment index ->
@@ -148,6 +151,15 @@ struct BlockState {
 // its file is read, so the copies overlap the other reads.
 int load_block(bfrs_ctx *ctx, const Geometry &g, size_t b, BlockArena &a, BlockState *st,
                PipeTrace *pt = nullptr);
+// load_block in two phases, so a caller can read block b+1 while block b is
+// verified and restored: load_block_reads reads the files through the ring
+// into `dev` (a.dev or a second device arena of k + 3 slots) and records
+// `done` on the ring's stream after the last H2D; load_block_verify waits
+// for `done` and hashes.  Between the two, st->dev must stay untouched.
+int load_block_reads(bfrs_ctx *ctx, const Geometry &g, size_t b, BlockArena &a, Arena &dev,
+                     hipEvent_t done, BlockState *st, PipeTrace *pt = nullptr);
+int load_block_verify(bfrs_ctx *ctx, const Geometry &g, BlockState *st, hipEvent_t done,
+                      PipeTrace *pt = nullptr);
 // RS(k,3)-decodes every damaged segment into its own device slot, re-verifies
 // the restored bytes on the device and copies them to host memory: to
 // host_out[s] where given (pinned, >= lens[s] bytes), else to the arena's out
