@@ -1,6 +1,7 @@
 // hash_gpu.cpp — host side of the device BLAKE3 (blake3_kernels.hip):
 // splits messages into 256 KiB groups, plans the CV reduction levels, and
 // exposes bfrs_blake3_batch_dev / bfrs_blake3_combine.
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -113,25 +114,31 @@ int Context::blake3_dev(size_t n, const uint8_t *const *d_msgs, const size_t *le
   const size_t b_out = align_up(n * 32, 256);
   const size_t need = b_groups + b_jobs + b_cv + b_cv1 + 2 * b_out;
   const size_t h_need = b_groups + b_jobs + 2 * b_out;
+  // Work areas grow rarely: at least 32 MiB / 1 MiB (a 4 GiB batch of
+  // 32 MiB messages needs ~17 MiB) and doubling, because a regrow waits for
+  // the whole device (a commit's next block is in flight on another stream)
+  constexpr size_t kDevFloor = size_t(32) << 20, kHostFloor = size_t(1) << 20;
   if (need > d_hash_cap) {
+    const size_t cap = std::max({need, kDevFloor, 2 * d_hash_cap});
     if (d_hash) {
       HIP_TRY(hipDeviceSynchronize());
       HIP_TRY(hipFree(d_hash));
       d_hash = nullptr;
       d_hash_cap = 0;
     }
-    HIP_TRY(hipMalloc(&d_hash, need));
-    d_hash_cap = need;
+    HIP_TRY(hipMalloc(&d_hash, cap));
+    d_hash_cap = cap;
   }
   if (h_need > h_hash_cap) {
+    const size_t cap = std::max({h_need, kHostFloor, 2 * h_hash_cap});
     if (h_hash) {
       HIP_TRY(hipDeviceSynchronize());
       HIP_TRY(hipHostFree(h_hash));
       h_hash = nullptr;
       h_hash_cap = 0;
     }
-    HIP_TRY(hipHostMalloc(&h_hash, h_need, hipHostMallocDefault));
-    h_hash_cap = h_need;
+    HIP_TRY(hipHostMalloc(&h_hash, cap, hipHostMallocDefault));
+    h_hash_cap = cap;
   }
   uint8_t *d = static_cast<uint8_t *>(d_hash);
   uint8_t *h = static_cast<uint8_t *>(h_hash);
