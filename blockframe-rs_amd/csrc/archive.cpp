@@ -315,10 +315,14 @@ int Commit::tier1(std::string *out_dir) {
   const std::string file_hash = hs[0].data;
   dir = root + "/" + name + "_" + file_hash;
   if (!mkdirs(dir)) return io_error("mkdir " + dir);
-  if (!write_file(dir + "/data.dat", m.p, m.n)) return io_error("write data.dat");
-  for (size_t p = 0; p < kParity; ++p)
-    if (!write_file(dir + "/parity_" + std::to_string(p) + ".dat", par[p].data(), shard))
-      return io_error("write parity");
+  std::atomic<bool> ok{true};
+  parallel_for(1 + kParity, 1 + kParity, [&](size_t f) {  // the four files side by side
+    const bool w = f == 0 ? write_file(dir + "/data.dat", m.p, m.n)
+                          : write_file(dir + "/parity_" + std::to_string(f - 1) + ".dat",
+                                       par[f - 1].data(), shard);
+    if (!w) ok = false;
+  });
+  if (!ok) return io_error("write tier-1 shards");
   Manifest mf;
   mf.tier = 1;
   mf.data_shards = 6;  // commit.rs:98 (sic)
