@@ -621,9 +621,10 @@ int Commit::tier3(std::string *out_dir) {
 }
 
 // ---------------------------------------------------------------------------
-// Verified bytes of one stored shard, CPU hash (tiers 1/2; small files).
+// Verified bytes of one stored shard, CPU hash on the host threads (tiers
+// 1/2: files of up to a segment; the digest does not depend on the threads).
 bool load_verified(const std::string &path, const std::string &want_hex, std::vector<uint8_t> *out,
-                   int threads = 1) {
+                   int threads = hw_threads()) {
   if (!read_file(path, out)) return false;
   return blake3_hex(out->data(), out->size(), threads) == want_hex;
 }
@@ -648,7 +649,7 @@ int recover_rs13(bfrs_ctx *ctx, const std::vector<std::string> &paths,
   int rc = bfrs_decode_host_batch(ctx, 1, &k1, kParity, shard, orig, rec.data(), outp);
   if (rc) return rc;
   restored.resize(std::min(expected, shard));
-  if (blake3_hex(restored.data(), restored.size()) != want)
+  if (blake3_hex(restored.data(), restored.size(), hw_threads()) != want)
     return set_error(BFRS_E_WRAPPER, "restored bytes fail the manifest hash");
   *out = std::move(restored);
   return BFRS_OK;
@@ -884,6 +885,11 @@ struct bfrs_archive {
   std::string expected_hash(size_t gi) const;
   std::string seg_path(size_t gi) const;
   int load_clean(size_t gi, SegPtr *out, bool *ok);  // no locks held
+  // device BLAKE3 of `len` pinned bytes on a free verification lane
+  int lane_hash(const uint8_t *buf, size_t len, size_t key, std::string *hex);
+  // *ok = the file at `path` hashes to want_hex (device BLAKE3; tiers 1/2's
+  // parity copies, up to one pool buffer long)
+  int verify_file(const std::string &path, const std::string &want_hex, bool *ok);
   int recover(size_t gi, SegPtr *out);              // no locks held
   // Verify segment gi (and reconstruct it if damaged) with mu released,
   // holding gi in `inflight` so that other readers wait for it.  Every exit,
@@ -951,36 +957,56 @@ int bfrs_archive::load_clean(size_t gi, SegPtr *out, bool *ok) {
   auto seg = std::make_shared<Seg>(pool, buf, len);
   const long long t_read = trace.on ? trace.ns() : 0;
   if (read_file_into(seg_path(gi), buf, pool->slot, 8) != (long long)len) return BFRS_OK;
-  const long long t_lock = trace.on ? trace.ns() : 0;
-  CleanLane *ln = nullptr;
-  std::unique_lock<std::mutex> lane_lock = take_lane(gi, &ln);
   const long long t_gpu = trace.on ? trace.ns() : 0;
   struct Done {  // trace only
     bfrs_archive *a;
     size_t gi;
-    long long t_read, t_lock, t_gpu;
+    long long t_read, t_gpu;
     ~Done() {
       if (!a->trace.on) return;
       const long long t_end = a->trace.ns();
-      a->trace.clean_read_ns += t_lock - t_read;
-      a->trace.gpu_lock_wait_ns += t_gpu - t_lock;
+      a->trace.clean_read_ns += t_gpu - t_read;
       a->trace.clean_gpu_ns += t_end - t_gpu;
       ++a->trace.cleans;
       a->trace.event("clean", gi, t_read, t_end);
     }
-  } done{this, gi, t_read, t_lock, t_gpu};
+  } done{this, gi, t_read, t_gpu};
+  std::string hex;
+  int rc = lane_hash(buf, len, gi, &hex);
+  if (rc) return rc;
+  if (hex == expected_hash(gi)) {
+    *ok = true;
+    *out = std::move(seg);
+  }
+  return BFRS_OK;
+}
+
+int bfrs_archive::lane_hash(const uint8_t *buf, size_t len, size_t key, std::string *hex) {
+  CleanLane *ln = nullptr;
+  std::unique_lock<std::mutex> lane_lock = take_lane(key, &ln);
   Context &c = ctx->impl;
   HIP_TRY(hipSetDevice(c.device));  // before the lane's HBM: a prefetch thread starts on device 0
   int rc = ln->ready(pool->slot);
   if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(ln->d, buf, len, hipMemcpyHostToDevice, ln->st));
   HIP_TRY(hipStreamSynchronize(ln->st));  // before the hash takes hash_mu
-  std::vector<std::string> hex;
-  if ((rc = gpu_hash_hex(ctx, {ln->d}, {len}, &hex, nullptr, nullptr, ln->st))) return rc;
-  if (hex[0] == expected_hash(gi)) {
-    *ok = true;
-    *out = std::move(seg);
-  }
+  std::vector<std::string> h;
+  if ((rc = gpu_hash_hex(ctx, {ln->d}, {len}, &h, nullptr, nullptr, ln->st))) return rc;
+  *hex = h[0];
+  return BFRS_OK;
+}
+
+int bfrs_archive::verify_file(const std::string &path, const std::string &want_hex, bool *ok) {
+  *ok = false;
+  uint8_t *buf = pool->get();
+  if (!buf) return set_error(BFRS_E_NOMEM, "pinned segment buffer allocation failed");
+  Seg hold(pool, buf, 0);  // back to the pool on every exit
+  const long long n = read_file_into(path, buf, pool->slot, 8);
+  if (n < 0) return BFRS_OK;  // missing, unreadable or longer than any shard here
+  std::string hex;
+  int rc = lane_hash(buf, size_t(n), 0, &hex);
+  if (rc) return rc;
+  *ok = hex == want_hex;
   return BFRS_OK;
 }
 
@@ -1439,7 +1465,7 @@ int repair_impl(const std::vector<bfrs_ctx *> &ctxs, const char *archive_dir,
     const uint32_t k1 = 1;
     if ((rc = bfrs_encode_host_batch(ctx, 1, &k1, kParity, shard, orig, outp))) return rc;
     for (size_t p : bad) {
-      if (blake3_hex(par[p].data(), shard) != phash[p])
+      if (blake3_hex(par[p].data(), shard, hw_threads()) != phash[p])
         return set_error(BFRS_E_WRAPPER, "re-encoded parity fails the manifest hash");
       if (!write_file(ppath[p], par[p].data(), shard)) return io_error("write parity");
       ++report->parity_repaired;
@@ -1538,8 +1564,9 @@ int health_report(bfrs_ctx *ctx, const char *archive_dir, Json *out) {
                                                 : t2_par(g.dir, i, p);
         const std::string want = g.mf.tier == 1 ? g.mf.leaves.count(int64_t(p + 1)) ? g.mf.leaves.at(int64_t(p + 1)) : ""
                                                 : g.mf.segments.at(int64_t(i)).parity.at(p);
-        std::vector<uint8_t> buf;
-        if (load_verified(path, want, &buf)) {
+        bool valid = false;
+        if ((rc = ar.verify_file(path, want, &valid))) return rc;
+        if (valid) {
           ++par_ok;
         } else {
           const std::string pn = g.mf.tier == 1 ? "parity_" + std::to_string(p) + ".dat"

@@ -53,6 +53,10 @@ def main():
             assert m2["merkle_tree"] == m["merkle_tree"] and m2["original_hash"] == m["original_hash"]
             shutil.rmtree(os.path.join(work, "again"))
             os.remove(src)
+            if tier == 2:  # every data and parity file hashed (tiers 1/2: on the host threads)
+                t = time.perf_counter()
+                assert bfrs.health_check(ctx, adir)["status"] == "Healthy"
+                res["health_check_tier2_MBps"] = round(n / (time.perf_counter() - t) / 1e6, 1)
             if tier == 3:
                 rng = np.random.default_rng(7)
                 damaged = 0
