@@ -1451,9 +1451,11 @@ int repair_impl(const std::vector<bfrs_ctx *> &ctxs, const char *archive_dir,
                                      : g.mf.leaves.at(int64_t(p + 1)));
     }
     std::vector<size_t> bad;
-    std::vector<uint8_t> tmp;
-    for (size_t p = 0; p < kParity; ++p)
-      if (!load_verified(ppath[p], phash[p], &tmp)) bad.push_back(p);
+    for (size_t p = 0; p < kParity; ++p) {  // device BLAKE3 on the lanes, as the data
+      bool valid = false;
+      if ((rc = a.verify_file(ppath[p], phash[p], &valid))) return rc;
+      if (!valid) bad.push_back(p);
+    }
     if (bad.empty()) continue;
     const size_t shard = (v->n + 63) / 64 * 64;  // generate.rs:34: padded to 64
     std::vector<uint8_t> padded(shard, 0);

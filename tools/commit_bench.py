@@ -57,6 +57,9 @@ def main():
                 t = time.perf_counter()
                 assert bfrs.health_check(ctx, adir)["status"] == "Healthy"
                 res["health_check_tier2_MBps"] = round(n / (time.perf_counter() - t) / 1e6, 1)
+                t = time.perf_counter()  # nothing to restore: every file verified
+                assert bfrs.repair(ctx, adir)["segments_repaired"] == 0
+                res["repair_tier2_clean_MBps"] = round(n / (time.perf_counter() - t) / 1e6, 1)
             if tier == 3:
                 rng = np.random.default_rng(7)
                 damaged = 0
