@@ -1,0 +1,1198 @@
+"""bench_legs.py -- the side legs of bench.py's line (the
+file that holds the timed region stays readable).
+
+bench.py imports every name below into its own namespace, so its line keys,
+its checkpoints and the tests that stand in for a leg (monkeypatching
+bench.<leg>) are unchanged.  Nothing here runs inside the timed region:
+
+  cpu_baseline          the oracle's AVX2 engine on C2's exact blocks (port, not the crate)
+  crate_api             the crate-shaped per-block host API (generate_parity /
+                        recover_segment_rs30_3) and rayon's all-blocks shape
+  pcie_inclusive        the C2 batch from pinned host memory (H2D + kernel + D2H)
+  blake3_device         the device BLAKE3 of C2's 128 segments against the golden
+  run_c5 and helpers    BASELINE configs[4]: read of a corrupted 4 GiB archive
+  check_config1         BASELINE configs[0]: RS(1,3) of an 8 MB file
+  live_pmc_traffic / live_kernel_trace
+                        the rocprofv3 child passes (PMC traffic, kernel trace) run
+                        before the measurement touches the GPU
+  host_info / host_budget / host_pressure / pinned_host_state
+                        what the host offers and what the run pins
+
+The oracle (oracle/) is imported only by cpu_baseline and c5_cpu_baseline, as
+the CPU baseline, after the timed region.
+"""
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if os.path.join(ROOT, "blockframe-rs_amd") not in sys.path:
+    sys.path.insert(0, os.path.join(ROOT, "blockframe-rs_amd"))
+
+
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+
+
+# ---------------------------------------------------------------- supervisor
+STATE_ENV = "BENCH_STATE_FILE"  # set by the supervisor in its measurement child
+
+
+def probe_env(**extra) -> dict:
+    """Environment of a probe child (PMC and trace passes, the rayon probe):
+    this process's, without the supervisor's state file (a probe's line must
+    never land in it; round 5's first box run lost both live passes that
+    way: the probes took the child's exit path, which skips rocprofv3's
+    output at exit) and without torchrun's job id (a probe never joins a
+    process group)."""
+    env = dict(os.environ, **extra)
+    env.pop(STATE_ENV, None)
+    env.pop("TORCHELASTIC_RUN_ID", None)
+    return env
+
+
+def host_budget(args, world):
+    """Pinned host memory the run asks for, per rank and for the node, beside
+    what the host offers (MemTotal / MemAvailable, the cgroup's memory.max).
+    At N > 1 the only pinned buffers are c4_strong.pcie_inclusive's: each
+    rank's stripes of config 4's data, parity and restored shards."""
+    from bfrs import parallel, synth
+    shapes = synth.block_shapes(args.c4_segments)
+    stripe = max(hi - lo for lo, hi in parallel.stripe_ranges(args.segment_bytes, world))
+    c4_pinned = ((sum(shapes) + 6 * len(shapes)) * stripe
+                 if args.c4 == "auto" and args.pcie == "auto" and not args.strong else 0)
+    per_rank = c4_pinned
+    if world == 1 and args.pcie == "auto" and not args.strong:  # + pcie_inclusive's C2 buffers
+        c2 = synth.block_shapes(args.segments)
+        per_rank = max(per_rank, (sum(c2) + 6 * len(c2)) * args.segment_bytes)
+    mem = {}
+    try:
+        for line in open("/proc/meminfo"):
+            k, v = line.split(":", 1)
+            if k in ("MemTotal", "MemAvailable"):
+                mem[k] = int(v.split()[0]) * 1024
+    except (OSError, ValueError):
+        pass
+    cg = None
+    try:
+        t = open("/sys/fs/cgroup/memory.max").read().strip()
+        cg = None if t == "max" else int(t)
+    except (OSError, ValueError):
+        pass
+    # rank 0 alone, after the other ranks are done: c4_one_process pins config
+    # 4's whole data, parity and restored shards
+    one_proc = ((sum(shapes) + 6 * len(shapes)) * args.segment_bytes
+                if args.c4 == "auto" and args.pcie == "auto" and not args.strong else 0)
+    node = per_rank * world + one_proc
+    avail = min(x for x in (mem.get("MemAvailable"), cg) if x) if (mem.get("MemAvailable") or cg) else None
+    return {"pinned_bytes_per_rank": per_rank, "ranks": world, "pinned_bytes_node": node,
+            "c4_pcie_pinned_bytes_per_rank": c4_pinned, "rank0_c4_one_process_bytes": one_proc,
+            "mem_total": mem.get("MemTotal"), "mem_available": mem.get("MemAvailable"),
+            "cgroup_memory_max": cg, "fits": None if avail is None else node < avail,
+            "what": "largest pinned host buffer set of one rank (c4_strong.pcie_inclusive at N>1; "
+                    "at N=1 also pcie_inclusive's C2 batch) x ranks, plus rank 0's "
+                    "c4_one_process buffers, against this host (upper bound: torch keeps "
+                    "freed pinned blocks cached)"}
+
+
+def check_config1(ctx):
+    """BASELINE configs[0]: a single 8 MB file's RS(1,3) through the product
+    (Chunker::generate_parity_segmented, generate.rs:26-57, then
+    recover_segment_rs13, recovery.rs:43-79): the 3 parity shards are the
+    data zero-padded to a multiple of 64 (LowRate RS(1,3) = replication,
+    src/filestore/README.md:178; tests/golden/rs_small.json's RS(1,3) cases)
+    and the recovery returns the file's bytes.  8 MiB, 8,000,000 B and an
+    unaligned 8,000,002 B (seed 1, bfrs/synth.py)."""
+    import numpy as np
+    import bfrs
+    from bfrs import synth
+    res = {}
+    for n in (8 * 1024 * 1024, 8_000_000, 8_000_002):
+        data = synth.segment_np(1, 0, n)
+        par = bfrs.Chunker(ctx).generate_parity_segmented(data)
+        padded = np.pad(data, (0, (n + 63) // 64 * 64 - n)).tobytes()
+        ok = par == [padded] * 3
+        ok = ok and bfrs.recover_segment_rs13(ctx, par, expected_size=n) == data.tobytes()
+        res[str(n)] = bool(ok)
+    return {"sizes": res, "match": all(res.values()),
+            "what": "RS(1,3) parity == pad64(data) x 3, and recover_segment_rs13 == data"}
+
+
+# ---------------------------------------------------------------- host side
+def host_info():
+    """CPU model and the core counts this host offers (nproc shows the whole
+    machine on the GPU boxes; the affinity mask and the cgroup quota show
+    this job's share)."""
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = float(q) / float(p)
+    except (OSError, ValueError):
+        pass
+    aff = len(os.sched_getaffinity(0))
+    share = aff
+    if quota:
+        share = min(share, max(1, int(quota)))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit():
+        share = min(share, int(omp))
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": aff,
+            "cgroup_cpu_quota": quota, "omp_num_threads": omp, "cpu_share": share}
+
+
+def cpu_baseline(args, sets, info):
+    """The oracle's AVX2 nibble-table engine (the crate's Avx2 technique) on
+    host cores, on C2's exact blocks (4 x RS(30,3) + 1 x RS(8,3) of 32 MiB,
+    copied from the GPU), encode then the same 3-erasure decodes:
+      striped       all cores, 64-B column stripes of every shard (value)
+      rayon_blocks  one block per thread, as rayon's into_par_iter over blocks
+                    (src/chunker/commit.rs:391-393): at most 5-way parallel
+      rayon_blocks_wrapper_copies  + the reference wrappers' copies: the pad
+                    to_vec of every segment and the to_vec of every output
+                    (src/chunker/generate.rs:75-82,95-96; recovery.rs:167-169)
+      single_core   one RS(30,3) block on one thread
+    Restatement of reed-solomon-simd 3.1.0, not the crate."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    eng = oracle.ENGINE_AVX2 if oracle.lib().oracle_have_avx2() else oracle.ENGINE_SCALAR
+    shapes, S = sets.shapes, sets.S
+    host = sets.data.cpu().numpy()  # C2's exact bytes
+    nb = len(shapes)
+    blocks, off = [], 0
+    for k in shapes:
+        blocks.append([host[off + i] for i in range(k)])
+        off += k
+    par = [[np.empty(S, np.uint8) for _ in range(3)] for _ in range(nb)]
+    rest = [[np.empty(S, np.uint8) if i in sets.erased[b] else None for i in range(k)]
+            for b, k in enumerate(shapes)]
+    dec_in = [[None if i in sets.erased[b] else blocks[b][i] for i in range(k)]
+              for b, k in enumerate(shapes)]
+    data_gib = sum(shapes) * S / 2**30
+    threads = args.cpu_threads or info["cpu_share"]
+
+    def run(nthreads, ks, orig, rec, out, decode, copies=False):
+        t0 = time.perf_counter()
+        oracle.batch(eng, decode, nthreads, ks, 3, len(orig[0][0]) if orig[0][0] is not None
+                     else len(rec[0][0]), orig, rec, out, copies=copies)
+        return time.perf_counter() - t0
+
+    res = {}
+    self_ok = True  # the engine's own results: last block's parity, every restored shard
+    # rayon over blocks (codec only, then + wrapper copies)
+    for name, copies in (("rayon_blocks", False), ("rayon_blocks_wrapper_copies", True)):
+        t_e = run(min(threads, nb), shapes, blocks, [[None] * 3] * nb, par, False, copies)
+        t_d = run(min(threads, nb), shapes, dec_in, par, rest, True, copies)
+        res[name] = {"threads": min(threads, nb), "encode_GiBps": round(data_gib / t_e, 3),
+                     "decode_GiBps": round(data_gib / t_d, 3),
+                     "value": round(2 * data_gib / (t_e + t_d), 3)}
+    for b, k in enumerate(shapes):
+        want = oracle.encode(blocks[b][:k], 3, eng) if b == nb - 1 else None
+        if want is not None:
+            self_ok &= all(np.array_equal(par[b][j], want[j]) for j in range(3))
+        for i in sets.erased[b]:
+            self_ok &= bool(np.array_equal(rest[b][i], blocks[b][i]))
+    # column stripes over all cores (64-B aligned)
+    def striped(nthreads, nst):
+        sw = S // nst
+        ks, so, sp, sd, sdo = [], [], [], [], []
+        for b, k in enumerate(shapes):
+            for t in range(nst):
+                sl = slice(t * sw, (t + 1) * sw)
+                ks.append(k)
+                so.append([blocks[b][i][sl] for i in range(k)])
+                sp.append([par[b][j][sl] for j in range(3)])
+                sd.append([None if x is None else x[sl] for x in dec_in[b]])
+                sdo.append([None if x is None else x[sl] for x in rest[b]])
+        t_e = run(nthreads, ks, so, [[None] * 3] * len(ks), sp, False)
+        t_d = run(nthreads, ks, sd, sp, sdo, True)
+        return {"threads": nthreads, "stripes_per_shard": nst,
+                "encode_GiBps": round(data_gib / t_e, 3), "decode_GiBps": round(data_gib / t_d, 3),
+                "value": round(2 * data_gib / (t_e + t_d), 3)}
+
+    res["striped"] = striped(threads, 16)
+    # (round 5 also ran T = nproc threads, oversubscribing the box's 16-CPU
+    # quota 16-fold; VERDICT r5 item 5 dropped that misleading variant)
+    # one core, one RS(30,3) block
+    b0 = [blocks[0]]
+    p0 = [[np.empty(S, np.uint8) for _ in range(3)]]
+    t_e = run(1, [shapes[0]], b0, [[None] * 3], p0, False)
+    t_d = run(1, [shapes[0]], [dec_in[0]], p0, [rest[0]], True)
+    g1 = shapes[0] * S / 2**30
+    res["single_core"] = {"threads": 1, "encode_GiBps": round(g1 / t_e, 3), "decode_GiBps": round(g1 / t_d, 3),
+                          "value": round(2 * g1 / (t_e + t_d), 3),
+                          "sample": f"block 0 of C2 (RS({shapes[0]},3), 32 MiB shards)"}
+    st = res["striped"]
+    return {
+        "value": st["value"], "unit": "GiB/s", "cores": threads, "kind": "port",
+        "self_check": bool(self_ok),
+        "engine": "avx2" if eng == oracle.ENGINE_AVX2 else "scalar",
+        "encode_GiBps": st["encode_GiBps"], "decode_GiBps": st["decode_GiBps"],
+        "sample": f"C2's exact blocks ({'+'.join(map(str, shapes))} x 32 MiB), encode + the bench's "
+                  f"3-erasure decodes, 64-B column stripes over {threads} threads (restatement of "
+                  "reed-solomon-simd 3.1.0, not the crate)",
+        "host": info,
+        "variants": res,
+    }
+
+
+def pcie_link(S, k, dec_in=None):
+    """Host link rates on this box (torch copies of k x S bytes, best of 3) and
+    the PCIe floor they put under one crate-shaped RS(k,3) block: encode moves
+    k shards in and 3 out; a one-target decode moves every present shard in
+    (`dec_in`, default k: the crate's decoder combines all the shards it was
+    given, so a bit-exact decode of possibly inconsistent inputs reads them
+    all; with one erasure that is k - 1 segments + 3 parity) and 1 out."""
+    import numpy as np
+    import torch
+    n = k * S
+    dev = torch.empty(n, dtype=torch.uint8, device="cuda")
+    pageable = torch.from_numpy(np.ones(n, np.uint8))
+    pinned = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+    pinned.fill_(1)
+
+    def best(f, reps=3):
+        ts = []
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            f()
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        return min(ts)
+
+    r = {"bytes": n,
+         "h2d_pageable_GBps": n / best(lambda: dev.copy_(pageable)) / 1e9,
+         "h2d_pinned_GBps": n / best(lambda: dev.copy_(pinned, non_blocking=True)) / 1e9,
+         "d2h_pinned_GBps": n / best(lambda: pinned.copy_(dev, non_blocking=True)) / 1e9,
+         "d2h_pageable_GBps": n / best(lambda: pageable.copy_(dev)) / 1e9}
+    h2d = max(r["h2d_pageable_GBps"], r["h2d_pinned_GBps"]) * 1e9
+    d2h = max(r["d2h_pageable_GBps"], r["d2h_pinned_GBps"]) * 1e9
+    r["floor_generate_parity_ms"] = (k * S / h2d + 3 * S / d2h) * 1e3
+    r["floor_recover_one_target_ms"] = ((dec_in or k) * S / h2d + S / d2h) * 1e3
+    r["recover_shards_in"] = dec_in or k
+    del dev, pageable, pinned
+    return {key: (round(v, 2) if isinstance(v, float) else v) for key, v in r.items()}
+
+
+def crate_api(ctx, sets, reps=7, staging_ab=True):
+    """The per-block host-memory path BlockFrame calls:
+    Chunker::generate_parity on one RS(30,3) block of 32 MiB segments
+    (src/chunker/generate.rs:59-104) and recover_segment_rs30_3 of one erased
+    segment (src/filestore/recovery.rs:118-173), pageable host buffers in and
+    out as the Rust Vecs are.  Timed at the C-ABI (what the Rust binding
+    calls): fresh, untouched output buffers per call, like the Vecs the
+    reference allocates (generate.rs:95-96), so their page faults count.  The
+    Python wrappers' extra bytes() copies are reported apart (`python_wrapper_ms`).
+    `breakdown` times the same block through the encoder / decoder objects
+    call by call (add / encode or decode / fetch of the outputs), `link` the
+    box's PCIe rates and the floor they set, `alt_staging` the other
+    BFRS_CODEC_STAGING mode on a second context, same block."""
+    import numpy as np
+    import bfrs
+    S, k = sets.S, sets.shapes[0]
+    segs = [sets.data[i].cpu().numpy() for i in range(k)]
+    ch = bfrs.Chunker(ctx)
+
+    medians = {}
+    recover_ok = []  # every wrappers() round checks its restored segment against the original
+
+    def timed(f, n=reps, key=None):
+        """Best of n wall-clock calls; the median is kept under `key`: the host
+        link and host memory are shared with the other GPUs' jobs on the
+        machine, so single calls vary by 2x."""
+        ts = []
+        for _ in range(n):
+            t0 = time.perf_counter()
+            f()
+            ts.append(time.perf_counter() - t0)
+        if key:
+            medians[key] = round(sorted(ts)[len(ts) // 2] * 1e3, 2)
+        return min(ts)
+
+    def settle_link(c, ms=400.0):
+        """Untimed calls until `ms` of wall time: after the GPU-only part of
+        the bench the host link sits idle, and the first ~150 ms of H2D run
+        at a fraction of the link rate while it ramps up (bfrs trace: adds of
+        51, 39, 38, then 17.9 ms per block).  A commit streams blocks back to
+        back, so the steady state is the figure; the first call is reported
+        apart as `cold_first_call_ms`."""
+        chk = bfrs.Chunker(c)
+        outs = [np.empty(S, np.uint8) for _ in range(3)]
+        t0 = time.perf_counter()
+        chk.generate_parity_into(segs, k, 3, outs)
+        first = time.perf_counter() - t0
+        while (time.perf_counter() - t0) * 1e3 < ms:
+            chk.generate_parity_into(segs, k, 3, outs)
+        return first
+
+    def wrappers(c):
+        chk = bfrs.Chunker(c)
+        # the fresh-output figure is timed after the touched and new-input ones:
+        # the first second or so of crate_api saw sporadic 2x slower H2D/D2H
+        # waits in every bench run (BFRS_TRACE: waits of 28-34 ms instead of
+        # 2-7 ms), whichever figure was timed first
+        par = [np.empty(S, np.uint8) for _ in range(3)]
+        chk.generate_parity_into(segs, k, 3, par)
+        tg_reuse = timed(lambda: chk.generate_parity_into(segs, k, 3, par))
+        # new input buffers for every call as well (copied untimed): BlockFrame
+        # hands over newly mmap'd segments for every block
+        tg_new_in = []
+        for _ in range(reps):
+            fresh = [np.array(x) for x in segs]
+            outs = [np.empty(S, np.uint8) for _ in range(3)]
+            t0 = time.perf_counter()
+            chk.generate_parity_into(fresh, k, 3, outs)
+            tg_new_in.append(time.perf_counter() - t0)
+            del fresh, outs
+        tg_new_in = min(tg_new_in)
+        tg = timed(lambda: chk.generate_parity_into(segs, k, 3,
+                                                    [np.empty(S, np.uint8) for _ in range(3)]),
+                   key=f"generate_parity_{id(c)}")
+        target = sets.erased[0][0]
+        slots = [None if i == target else segs[i] for i in range(k)] + [None] * (30 - k)
+        tr = timed(lambda: bfrs.recover_segment_rs30_3_into(c, slots, par, target,
+                                                            np.empty(S, np.uint8)),
+                   key=f"recover_{id(c)}")
+        got = np.empty(S, np.uint8)
+        ok = bfrs.recover_segment_rs30_3_into(c, slots, par, target, got) == S
+        recover_ok.append(ok and np.array_equal(got, segs[target]))
+        tr_reuse = timed(lambda: bfrs.recover_segment_rs30_3_into(c, slots, par, target, got))
+        return tg, tr, par, slots, target, tg_reuse, tr_reuse, tg_new_in
+
+    def all_blocks_figure():
+        # rayon's shape (commit.rs:391-466): one generate_parity per block, all of
+        # C2's blocks at once from worker threads sharing the one context (ctypes
+        # drops the GIL for the call)
+        import threading
+        blocks, off = [], 0
+        for kb in sets.shapes:
+            blocks.append([sets.data[off + i].cpu().numpy() for i in range(kb)])
+            off += kb
+        errors = []
+
+        def worker(b):
+            try:
+                bfrs.Chunker(ctx).generate_parity_into(
+                    blocks[b], len(blocks[b]), 3, [np.empty(S, np.uint8) for _ in range(3)])
+            except Exception as e:  # noqa: BLE001 - reported below
+                errors.append(repr(e))
+
+        def all_blocks():
+            ts = [threading.Thread(target=worker, args=(b,)) for b in range(len(blocks))]
+            t0 = time.perf_counter()
+            for t in ts:
+                t.start()
+            for t in ts:
+                t.join()
+            return time.perf_counter() - t0
+
+        # untimed rounds first: the pool grows to one slot per block (a new slot
+        # pins (k+3) x 32 MiB of host memory, ~0.1 s) and the link settles
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < 0.5:
+            all_blocks()
+        t_par = [all_blocks() for _ in range(5)]
+        assert not errors, errors
+        return t_par
+
+    cold = settle_link(ctx)
+    t_par = all_blocks_figure()
+    tg, tr, par, slots, target, tg_reuse, tr_reuse, tg_new_in = wrappers(ctx)
+    tg_py = timed(lambda: ch.generate_parity(segs, k, 3))
+    tr_py = timed(lambda: bfrs.recover_segment_rs30_3(ctx, slots, par, target))
+    gib = k * S / 2**30
+
+    def breakdown():
+        """Encoder / decoder objects call by call, best of reps each."""
+        best = {}
+
+        def upd(key, v):
+            best[key] = min(best.get(key, 1e9), v)
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            enc = bfrs.ReedSolomonEncoder(ctx, k, 3, S)
+            t1 = time.perf_counter()
+            for sgm in segs:
+                enc.add_original_shard(sgm)
+            t2 = time.perf_counter()
+            enc.encode()
+            t3 = time.perf_counter()
+            outs = [np.empty(S, np.uint8) for _ in range(3)]
+            for j in range(3):
+                outs[j][:] = enc.recovery_view(j)  # the to_vec() of generate.rs:95-96
+            t4 = time.perf_counter()
+            del enc
+            upd("encoder_new_ms", t1 - t0)
+            upd("encoder_add_ms", t2 - t1)
+            upd("encoder_encode_ms", t3 - t2)
+            upd("encoder_fetch_ms", t4 - t3)
+            t0 = time.perf_counter()
+            dec = bfrs.ReedSolomonDecoder(ctx, 30, 3, S)
+            t1 = time.perf_counter()
+            for i, sgm in enumerate(slots):
+                if sgm is not None:
+                    dec.add_original_shard(i, sgm)
+            for j in range(3):
+                dec.add_recovery_shard(j, par[j])
+            t2 = time.perf_counter()
+            dec.decode()
+            t3 = time.perf_counter()
+            out = np.empty(S, np.uint8)
+            out[:] = dec.restored_view(target)  # recovery.rs:167-169's to_vec()
+            t4 = time.perf_counter()
+            del dec
+            upd("decoder_new_ms", t1 - t0)
+            upd("decoder_add_ms", t2 - t1)
+            upd("decoder_decode_ms", t3 - t2)
+            upd("decoder_fetch_ms", t4 - t3)
+        return {key: round(v * 1e3, 2) for key, v in best.items()}
+
+    bd = breakdown()
+    par_gib = sum(sets.shapes) * S / 2**30
+    res = {
+        "staging": os.environ.get("BFRS_CODEC_STAGING", "pinned"),
+        "generate_parity": {"ms": round(tg * 1e3, 2), "GiBps": round(gib / tg, 2),
+                            "median_ms": medians[f"generate_parity_{id(ctx)}"],
+                            "touched_outputs_ms": round(tg_reuse * 1e3, 2),
+                            "new_inputs_ms": round(tg_new_in * 1e3, 2),
+                            "cold_first_call_ms": round(cold * 1e3, 2),
+                            "python_wrapper_ms": round(tg_py * 1e3, 2),
+                            "what": f"RS({k},3) block of {S >> 20} MiB segments, pageable host in/out"},
+        "recover_segment_rs30_3": {"ms": round(tr * 1e3, 2), "GiBps_of_block": round(gib / tr, 2),
+                                   "median_ms": medians[f"recover_{id(ctx)}"],
+                                   "touched_output_ms": round(tr_reuse * 1e3, 2),
+                                   "python_wrapper_ms": round(tr_py * 1e3, 2),
+                                   "what": "one erased segment of that block, pageable host in/out"},
+        "breakdown": bd,
+        "recover_match": bool(recover_ok) and all(recover_ok),
+        "generate_parity_all_blocks_threads": {
+            "ms": round(min(t_par) * 1e3, 2), "GiBps": round(par_gib / min(t_par), 2),
+            "median_ms": round(sorted(t_par)[len(t_par) // 2] * 1e3, 2),
+            "what": f"{len(sets.shapes)} blocks ({'+'.join(map(str, sets.shapes))} x {S >> 20} MiB) "
+                    "on as many threads, one shared context (rayon over blocks), fresh outputs, "
+                    "best of 5 after 0.5 s of untimed rounds",
+            "codec_slots": int(os.environ.get("BFRS_CODEC_SLOTS", "2"))},
+        "reps": reps, "timing": "C-ABI call (bfrs_generate_parity / bfrs_recover_segment_rs30_3) "
+                                "through ctypes, fresh output buffers, best of reps (median_ms "
+                                "beside it), wall clock, after 400 ms of untimed calls",
+    }
+    res["link"] = pcie_link(S, k, dec_in=sum(x is not None for x in slots) + len(par))
+    lk = res["link"]
+    ref = reference_copies(segs, S, reps)
+    res["reference_copies"] = ref
+    res["generate_parity"]["floor_plus_copy_out_ms"] = round(
+        lk["floor_generate_parity_ms"] + ref["copy_out_3_shards_ms"], 2)
+    res["generate_parity"]["at_or_under_floor_plus_copy_out"] = bool(
+        res["generate_parity"]["ms"] <= res["generate_parity"]["floor_plus_copy_out_ms"])
+    res["recover_segment_rs30_3"]["floor_plus_copy_out_ms"] = round(
+        lk["floor_recover_one_target_ms"] + ref["copy_out_1_shard_ms"], 2)
+    res["generate_parity_all_blocks_threads"]["floor_ms"] = round(
+        (sum(sets.shapes) * S / (max(lk["h2d_pageable_GBps"], lk["h2d_pinned_GBps"]) * 1e9) +
+         3 * len(sets.shapes) * S / (max(lk["d2h_pinned_GBps"], lk["d2h_pageable_GBps"]) * 1e9))
+        * 1e3, 2)
+    if staging_ab:
+        old = os.environ.get("BFRS_CODEC_STAGING")
+        alt = "direct" if res["staging"] == "pinned" else "pinned"
+        os.environ["BFRS_CODEC_STAGING"] = alt
+        try:
+            c2 = bfrs.Context(ctx.device)
+        finally:
+            if old is None:
+                del os.environ["BFRS_CODEC_STAGING"]
+            else:
+                os.environ["BFRS_CODEC_STAGING"] = old
+        try:
+            settle_link(c2, 200.0)
+            pg, pr, _, _, _, pg_reuse, pr_reuse, pg_new_in = wrappers(c2)
+        finally:
+            c2.close()
+        res["recover_match"] = all(recover_ok)
+        res["alt_staging"] = {"staging": alt, "generate_parity_ms": round(pg * 1e3, 2),
+                              "generate_parity_touched_outputs_ms": round(pg_reuse * 1e3, 2),
+                              "generate_parity_new_inputs_ms": round(pg_new_in * 1e3, 2),
+                              "recover_segment_rs30_3_ms": round(pr * 1e3, 2),
+                              "what": f"BFRS_CODEC_STAGING={alt} on a second context, same block"}
+    return res
+
+
+def reference_copies(segs, S, reps=7):
+    """The reference's own host copies on this box, in its shape: one thread,
+    fresh heap memory per call (glibc serves 32 MiB from new mmap pages, as it
+    does Rust's Vec), page faults included, best of reps.
+      copy_out_3_shards   generate.rs:95-96: recovery_iter().to_vec() of 3 shards
+      copy_out_1_shard    recovery.rs:166-170: restored_original(target).to_vec()
+      pad_copies          generate.rs:75-82: every segment's to_vec() + resize
+    A crate-shaped call that returns fresh Vecs pays the copy-out on top of
+    the link floor; generate_parity.floor_plus_copy_out_ms is that sum."""
+    import numpy as np
+
+    def best(n_out, srcs):
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            outs = []
+            for j in range(n_out):
+                o = np.empty(S, np.uint8)
+                o[:] = srcs[j % len(srcs)]
+                outs.append(o)
+            ts.append(time.perf_counter() - t0)
+            del outs
+        return min(ts)
+    return {"copy_out_3_shards_ms": round(best(3, segs) * 1e3, 2),
+            "copy_out_1_shard_ms": round(best(1, segs) * 1e3, 2),
+            "pad_copies_ms": round(best(len(segs), segs) * 1e3, 2),
+            "what": "numpy copies into fresh np.empty buffers on one thread (the reference's "
+                    "to_vec() shape: new mmap pages, faulted by the copy), best of "
+                    f"{reps}: 3 shards (generate.rs:95-96), 1 shard (recovery.rs:166-170), "
+                    f"all {len(segs)} segments (the pad copies, generate.rs:75-82)"}
+
+
+B3_GOLDEN = os.path.join(ROOT, "tests", "golden", "blake3_c2.json")
+
+
+# VALU ceilings of the device BLAKE3, 256 CUs x 4 SIMDs x 16
+# lanes per clock at the 2.4 GHz peak clock.  The compression function needs
+# ~690 VALU per 64-B block and lane (7 rounds x 8 G x 12 ops + the output
+# XORs); the algorithm runs 16 block compressions per 1 KiB chunk plus one
+# parent per chunk (n - 1 parents for n chunks), so 690 x 17/16 = 733 VALU per
+# 64 B of input is the algorithmic need (`peak`).  `peak_compression_only`
+# (690 per 64 B, no parents) and round 3's issued count (780) are reported too.
+B3_VALU_PER_BLOCK = 690
+
+
+B3_VALU_PER_64B_ALG = B3_VALU_PER_BLOCK * 17 / 16
+
+
+B3_LANE_OPS_PER_S = 256 * 64 * 2.4e9
+
+
+def b3_ceiling_gbps(valu_per_64b):
+    return B3_LANE_OPS_PER_S / valu_per_64b * 64 / 1e9
+
+
+def blake3_device(ctx, sets, calls=10):
+    """f2: the device BLAKE3 over C2's 128 HBM-resident data
+    segments in one bfrs_blake3_batch_dev call (descriptor upload, both
+    kernels and the digest download included), best and mean of `calls`,
+    against its VALU ceiling, and every digest against the oracle's golden
+    (tests/golden/blake3_c2.json: the per-segment hashes a tier-3 commit
+    writes, commit.rs:429)."""
+    import torch
+    rows = [sets.data[i] for i in range(sets.data.shape[0])]
+    nbytes = sum(r.numel() for r in rows)
+    for _ in range(3):
+        ctx.blake3_batch_dev(rows)
+    torch.cuda.synchronize()
+    wrapper = []
+    for _ in range(calls):  # the Python wrapper: marshalling + call + hex digests
+        t0 = time.perf_counter()
+        ctx.blake3_batch_dev(rows)
+        wrapper.append(time.perf_counter() - t0)
+    call, dig = ctx.blake3_batch_dev_call(rows)
+    ts = []
+    for _ in range(calls):  # the C-ABI call itself, arguments marshalled once
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        call()
+        ts.append(time.perf_counter() - t0)
+    hexes = [bytes(d).hex() for d in dig]
+    check = None
+    try:
+        g = json.load(open(B3_GOLDEN))
+    except (OSError, ValueError):
+        g = None
+    if g and g["segments"] == len(rows) and g["segment_size"] == sets.S and g["seed"] == 0xB10C:
+        bad = [i for i, h in enumerate(hexes) if h != g["blake3"][i]]
+        check = {"golden": "tests/golden/blake3_c2.json", "digests": len(hexes),
+                 "mismatched": bad, "match": not bad}
+    best = min(ts)
+    return {"GBps": round(nbytes / best / 1e9, 1), "ms": round(best * 1e3, 3),
+            "mean_ms": round(sum(ts) / len(ts) * 1e3, 3), "bytes": nbytes,
+            "python_wrapper_ms": round(min(wrapper) * 1e3, 3),
+            "kernels": None,
+            "roofline": {"bound": "valu", "achieved": round(nbytes / best / 1e9, 1),
+                         "peak": round(b3_ceiling_gbps(B3_VALU_PER_64B_ALG), 1), "unit": "GB/s",
+                         "frac": round(nbytes / best / 1e9 / b3_ceiling_gbps(B3_VALU_PER_64B_ALG), 4),
+                         "peak_compression_only": round(b3_ceiling_gbps(B3_VALU_PER_BLOCK), 1),
+                         "frac_compression_only": round(
+                             nbytes / best / 1e9 / b3_ceiling_gbps(B3_VALU_PER_BLOCK), 4),
+                         "peak_r3_issued_780": round(b3_ceiling_gbps(780), 1),
+                         "note": f"peak: {B3_VALU_PER_BLOCK} VALU per 64-B compression x 17/16 "
+                                 "(one parent per 1 KiB chunk) = the algorithm's VALU per 64 B of "
+                                 "input; 256 CUs x 64 lane-ops per clock at 2.4 GHz"},
+            "parity_check": check,
+            "what": "bfrs_blake3_batch_dev over C2's 128 x 32 MiB data segments in HBM, one C-ABI "
+                    "call through ctypes (upload + kernels + digest download), arguments "
+                    "marshalled once, best of 10 wall-clock calls; python_wrapper_ms: the same "
+                    "through Context.blake3_batch_dev (per-call marshalling and hex digests)"}
+
+
+def host_pressure():
+    """Load on the host this run shares with the other GPUs' jobs: the load
+    average and the kernel's pressure-stall figures (PSI, % of the last 10 s
+    some task waited for CPU / memory / IO), where the host exposes them."""
+    out = {}
+    try:
+        out["loadavg_1m"] = round(os.getloadavg()[0], 2)
+    except OSError:
+        pass
+    for res in ("cpu", "memory", "io"):
+        try:
+            for line in open(f"/proc/pressure/{res}"):
+                if line.startswith("some"):
+                    out[f"psi_{res}_some_avg10"] = float(line.split()[1].split("=")[1])
+        except (OSError, ValueError, IndexError):
+            pass
+    return out
+
+
+def pinned_host_state(rt):
+    """Pinned host memory this process holds at the time (torch's caching host
+    allocator: pinned buffers it keeps after they are freed)."""
+    if rt.stub:
+        return None
+    try:
+        st = rt.torch.cuda.host_memory_stats()
+        return {k: st.get(k) for k in ("allocated_bytes.current", "reserved_bytes.current",
+                                      "num_host_alloc", "num_host_free") if k in st} or dict(
+            list(st.items())[:8])
+    except Exception as e:  # noqa: BLE001 - informative only
+        return {"error": f"{type(e).__name__}: {e}"}
+
+
+def rayon_fresh_process():
+    """BlockFrame's commit_blocked shape (one generate_parity per block on
+    every rayon worker, commit.rs:391-466) in a process of its own, as a
+    BlockFrame commit runs: tools/rayon_probe.py (C2's 5 blocks on 5 threads,
+    one context, fresh outputs, new inputs every round) as a child started
+    before this process touches the GPU.  Inside the bench process, after the
+    device benchmark, the same calls run 20-40% slower (`crate_api.
+    generate_parity_all_blocks_threads`; cause not isolated)."""
+    cmd = ["timeout", "-s", "KILL", "90", sys.executable,
+           os.path.join(ROOT, "tools", "rayon_probe.py")]
+    env = probe_env(PROBE_MODES="pinned", PROBE_REPS="3")
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, env=env, cwd=ROOT)
+    except OSError as e:
+        return {"error": f"{type(e).__name__}: {e}"}
+    if r.returncode != 0:
+        return {"error": f"tools/rayon_probe.py exited {r.returncode}: {r.stderr[-300:]}"}
+    try:
+        res = json.loads(r.stdout.strip().splitlines()[-1])
+    except (ValueError, IndexError):
+        return {"error": "no JSON line from tools/rayon_probe.py"}
+    return {"ms": res["fresh_pinned"][0], "median_ms": res["fresh_pinned"][1],
+            "GiBps": res["fresh_pinned_GiBps"], "inputs_seen_before_ms": res["seen_pinned"][0],
+            "link_floor_ms": res["link_floor_ms"],
+            "what": "5 blocks (30+30+30+30+8 x 32 MiB) on 5 threads in a fresh process "
+                    "(tools/rayon_probe.py): new input buffers and fresh outputs every round, "
+                    "best of 3 (median beside it); link floor = torch H2D of all inputs + D2H "
+                    "of all parity from pinned memory"}
+
+
+def pcie_inclusive(ctx, sets, steps=2, rt=None, job_bytes=None):
+    """The reference path starts and ends in host memory: time the same batch
+    through bfrs_encode_host_batch / bfrs_decode_host_batch from pinned host
+    buffers (H2D + kernel + D2H pipelined over 3 streams).  Reported beside
+    `value`, never as `value`.  With rt (c4_strong): every rank times its own
+    stripes between barriers and the job rate uses the max over ranks."""
+    import torch
+    shapes, S = sets.shapes, sets.S
+    nseg, nb = sum(shapes), len(shapes)
+    h_data = torch.empty(nseg, S, dtype=torch.uint8, pin_memory=True)
+    h_data.copy_(sets.data)
+    h_par = torch.empty(3 * nb, S, dtype=torch.uint8, pin_memory=True)
+    h_rest = torch.empty(3 * nb, S, dtype=torch.uint8, pin_memory=True)
+    enc_in = [h_data[s] for s in range(nseg)]
+    enc_out = [h_par[i] for i in range(3 * nb)]
+    dec_in_h, dec_out_h, seg = [], [], 0
+    for b, k in enumerate(shapes):
+        er = sets.erased[b]
+        for i in range(k):
+            dec_in_h.append(None if i in er else h_data[seg + i])
+            dec_out_h.append(h_rest[3 * b + er.index(i)] if i in er else None)
+        seg += k
+    def clock(call):
+        call()  # warm
+        if rt:
+            rt.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            call()
+        t = (time.perf_counter() - t0) / steps
+        return rt.max_over_ranks(t) if rt else t
+
+    t_enc = clock(lambda: ctx.encode_host_batch(shapes, 3, S, enc_in, enc_out))
+    t_dec = clock(lambda: ctx.decode_host_batch(shapes, 3, S, dec_in_h, enc_out, dec_out_h))
+    seg, bad = 0, []
+    for b, k in enumerate(shapes):
+        for t, i in enumerate(sets.erased[b]):
+            if not torch.equal(h_rest[3 * b + t], h_data[seg + i]):
+                bad.append([b, i])
+        seg += k
+    gib = (job_bytes or nseg * S) / 2**30
+    return {
+        "decode_match": not bad, "decode_mismatched": bad,
+        "encode_GiBps": round(gib / t_enc, 2), "decode_GiBps": round(gib / t_dec, 2),
+        "encode_ms": round(t_enc * 1e3, 2), "decode_ms": round(t_dec * 1e3, 2),
+        "h2d_bytes_encode": nseg * S, "d2h_bytes_encode": 3 * nb * S,
+        "note": "pinned host buffers; bfrs_*_host_batch (8 MiB column slabs over 3 HIP streams)",
+    }
+
+
+PMC_PASS_TIMEOUT_S = 60
+
+
+def under_rocprof() -> bool:
+    """rocprofv3 exports ROCPROF_* variables to the program it profiles."""
+    return any(k.startswith("ROCPROF_") for k in os.environ)
+
+
+def _pmc_pass(counter, args, workdir):
+    """One `rocprofv3 --pmc <counter>` pass over the traffic probe; returns the
+    per-dispatch counter values of the full-size gf_apply launches."""
+    import csv
+    import glob
+    out = os.path.join(workdir, counter)
+    cmd = ["timeout", "-s", "KILL", str(PMC_PASS_TIMEOUT_S), "rocprofv3", "--pmc", counter,
+           "--output-format", "csv", "-d", out, "-o", "pmc", "--",
+           sys.executable, os.path.abspath(__file__), "--traffic-probe",
+           "--segments", str(args.segments), "--segment-bytes", str(args.segment_bytes),
+           "--pitch", str(args.pitch), "--layout", args.layout]
+    env = probe_env(TMPDIR=workdir, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    with open(os.path.join(workdir, f"{counter}.log"), "w") as log:
+        rc = subprocess.call(cmd, stdout=log, stderr=subprocess.STDOUT, env=env, cwd=workdir)
+    if rc != 0:
+        raise RuntimeError(f"rocprofv3 --pmc {counter} exited {rc}")
+    rows = [r for f in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True)
+            for r in csv.DictReader(open(f))
+            if "gf_apply" in r["Kernel_Name"] and r["Counter_Name"] == counter]
+    if not rows:
+        raise RuntimeError(f"no gf_apply dispatches with {counter} in the rocprofv3 output")
+    grid = max(int(r["Grid_Size"]) for r in rows)
+    per = {}
+    for r in rows:
+        if int(r["Grid_Size"]) == grid:  # the C2 launches (encode and decode share the grid)
+            per[r["Dispatch_Id"]] = per.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
+    return list(per.values())
+
+
+def live_pmc_traffic(args):
+    """HBM bytes per gf_apply launch measured in this run: two rocprofv3 child
+    passes (--pmc FETCH_SIZE, then --pmc WRITE_SIZE: separate runs, no trace
+    domains) over the bench's own C2 batch, started before this process touches
+    the GPU.  Corrections of MI355X_MICROARCH.md's HBM section: both counters
+    are KiB, and gfx950's FETCH_SIZE counts half of a 16 B/lane streaming read
+    (x2).  Returns (bytes, source) or (None, {"error": ...})."""
+    import shutil
+    import statistics
+    import tempfile
+    if shutil.which("rocprofv3") is None or shutil.which("timeout") is None:
+        return None, {"error": "rocprofv3 not on PATH"}
+    t0 = time.perf_counter()
+    workdir = tempfile.mkdtemp(prefix="bfrs_pmc_")
+    try:
+        fetch = _pmc_pass("FETCH_SIZE", args, workdir)
+        write = _pmc_pass("WRITE_SIZE", args, workdir)
+    except (OSError, RuntimeError, ValueError, KeyError) as e:
+        return None, {"error": f"{type(e).__name__}: {e}"}
+    finally:
+        shutil.rmtree(workdir, ignore_errors=True)
+    rd = int(statistics.median(fetch) * 1024 * 2)
+    wr = int(statistics.median(write) * 1024)
+    return rd + wr, {
+        "how": "measured in this run: rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate "
+               "child passes, before this process touched the GPU) over the same C2 batch "
+               "(3 encode + 3 decode launches each), median per dispatch",
+        "correction": "KiB; gfx950 FETCH_SIZE x2 (MI355X_MICROARCH.md HBM section)",
+        "dispatches": [len(fetch), len(write)],
+        "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
+        "seconds": round(time.perf_counter() - t0, 1)}
+
+
+TRACE_PASS_TIMEOUT_S = 150
+
+
+B3_PROBE_CALLS = 10
+
+
+def blake3_trace_figures(live_trace, nbytes):
+    """blake3_device.kernels: the device BLAKE3's kernel split from the
+    rocprofv3 child pass (trace_probe ends with B3_PROBE_CALLS calls over the
+    same 128 segments), so the call's wall time splits into device work and
+    the host side."""
+    b3 = (live_trace or {}).get("blake3")
+    if not b3:
+        return {"error": (live_trace or {}).get("error") or "no BLAKE3 dispatches in the trace pass"}
+    out = dict(b3)
+    if "group_kernel_ms" in out:
+        out["frac_group_kernel"] = round(
+            nbytes / (out["group_kernel_ms"] * 1e-3) / 1e9 / b3_ceiling_gbps(B3_VALU_PER_64B_ALG), 4)
+    return out
+
+
+def summarize_kernel_trace(csv_path, steps):
+    """The C2 launches of a kernel_trace.csv: gf_apply dispatches at the
+    largest grid (the C2 batch; encode and decode share the grid), in start
+    order; the last 2K of them are the probe's timed region."""
+    import csv
+    import statistics
+    rows = [r for r in csv.DictReader(open(csv_path)) if "gf_apply" in r["Kernel_Name"]]
+    if not rows:
+        raise RuntimeError("no gf_apply dispatches in the kernel trace")
+    grid = max(int(r["Grid_Size_X"]) for r in rows)
+    c2 = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"])
+                for r in rows if int(r["Grid_Size_X"]) == grid)
+    timed = c2[-2 * steps:]
+    if len(timed) < 2 * steps:
+        raise RuntimeError(f"kernel trace holds {len(timed)} C2 launches, expected {2 * steps}")
+    d = [(e - s) / 1e6 for s, e, _ in timed]
+    return {"kernel": timed[-1][2].rsplit("(", 1)[0].replace("void ", ""), "grid": grid,
+            "launches": len(d), "launches_in_trace": len(c2),
+            "mean_ms": round(statistics.mean(d), 4), "median_ms": round(statistics.median(d), 4),
+            "min_ms": round(min(d), 4), "max_ms": round(max(d), 4),
+            "span_ms_per_launch": round((timed[-1][1] - timed[0][0]) / 1e6 / len(d), 4)}
+
+
+def summarize_blake3_trace(csv_path, calls):
+    """The device BLAKE3 calls at the end of the trace pass: the group
+    kernel's median duration, the reduce kernels' time and count per call,
+    and each call's device span (first dispatch start to last dispatch end;
+    a call starts at its group kernel)."""
+    import csv
+    import statistics
+    rows = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"])
+                  for r in csv.DictReader(open(csv_path)) if "blake3" in r["Kernel_Name"])
+    group = [(t0, t1) for t0, t1, n in rows if "group" in n]
+    reduce_ = [(t0, t1) for t0, t1, n in rows if "reduce" in n]
+    if len(group) < calls:
+        return None
+    spans = []
+    for j, (g0, _) in enumerate(group):
+        g_next = group[j + 1][0] if j + 1 < len(group) else float("inf")
+        spans.append((max(t1 for t0, t1, _n in rows if g0 <= t0 < g_next) - g0) / 1e6)
+    return {"group_kernel_ms": round(statistics.median((t1 - t0) / 1e6 for t0, t1 in group), 4),
+            "reduce_kernels_ms_per_call": round(sum(t1 - t0 for t0, t1 in reduce_) / 1e6 / len(group), 4),
+            "reduce_launches_per_call": len(reduce_) // len(group),
+            "device_span_ms": round(min(spans), 4), "calls": len(group),
+            "how": "rocprofv3 --kernel-trace child pass (trace_probe's last "
+                   f"{len(group)} bfrs_blake3_batch_dev calls over C2's 128 segments)"}
+
+
+def live_kernel_trace(args, profile_dir=None):
+    """roofline.trace measured in this run: one `rocprofv3 --kernel-trace
+    --stats` child pass (the program right after `--`, no shell hop) over the
+    bench's own device loop (trace_probe), started before this process touches
+    the GPU.  Returns the C2 launch summary of the child's timed region, the
+    child's own HIP-event launch time and the --stats top kernels, or
+    {"error": ...}.  With profile_dir, the stats CSV and the summary are kept
+    there (the committed profiles/ evidence of a bench line)."""
+    import csv
+    import glob
+    import shutil
+    import tempfile
+    if shutil.which("rocprofv3") is None or shutil.which("timeout") is None:
+        return {"error": "rocprofv3 not on PATH"}
+    t0 = time.perf_counter()
+    workdir = tempfile.mkdtemp(prefix="bfrs_trace_")
+    out = os.path.join(workdir, "trace")
+    cmd = ["timeout", "-s", "KILL", str(TRACE_PASS_TIMEOUT_S), "rocprofv3", "--kernel-trace",
+           "--stats", "--output-format", "csv", "-d", out, "-o", "run", "--",
+           sys.executable, os.path.abspath(__file__), "--trace-probe",
+           "--segments", str(args.segments), "--segment-bytes", str(args.segment_bytes),
+           "--pitch", str(args.pitch), "--layout", args.layout, "--steps", str(args.steps),
+           "--warmup", str(args.warmup), "--settle-ms", str(args.settle_ms)]
+    env = probe_env(TMPDIR=workdir, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    try:
+        log_path = os.path.join(workdir, "trace.log")
+        with open(log_path, "w") as log:
+            rc = subprocess.call(cmd, stdout=log, stderr=subprocess.STDOUT, env=env, cwd=workdir)
+        if rc != 0:
+            raise RuntimeError(f"rocprofv3 --kernel-trace exited {rc}: "
+                               f"{open(log_path).read()[-300:]}")
+        child = None
+        for line in open(log_path):
+            if line.startswith("{") and '"launch_ms"' in line:
+                child = json.loads(line)
+        traces = glob.glob(os.path.join(out, "**", "*kernel_trace.csv"), recursive=True)
+        stats = glob.glob(os.path.join(out, "**", "*kernel_stats.csv"), recursive=True)
+        if not traces:
+            raise RuntimeError("no kernel_trace.csv in the rocprofv3 output")
+        summ = summarize_kernel_trace(traces[0], args.steps)
+        summ["blake3"] = summarize_blake3_trace(traces[0], B3_PROBE_CALLS)
+        top = []
+        if stats:
+            for r in list(csv.DictReader(open(stats[0])))[:4]:
+                top.append({"name": r["Name"][:90], "calls": int(r["Calls"]),
+                            "average_ms": round(float(r["AverageNs"]) / 1e6, 4),
+                            "percentage": float(r["Percentage"])})
+        summ.update({
+            "how": "measured in this run: rocprofv3 --kernel-trace --stats child pass (before this "
+                   "process touched the GPU) over the bench's own C2 batch and device loop "
+                   f"(settle, {args.warmup} warmup, {args.steps} timed steps); the last "
+                   f"{2 * args.steps} C2 dispatches = the child's timed region",
+            "child_event_launch_ms": round(child["launch_ms"], 4) if child else None,
+            "stats_top": top, "seconds": round(time.perf_counter() - t0, 1)})
+        if profile_dir:
+            os.makedirs(profile_dir, exist_ok=True)
+            if stats:
+                shutil.copy(stats[0], os.path.join(profile_dir, "trace_kernel_stats.csv"))
+            with open(os.path.join(profile_dir, "trace_c2_launch_summary.json"), "w") as f:
+                json.dump(summ, f, indent=1)
+        return summ
+    except (OSError, RuntimeError, ValueError, KeyError) as e:
+        return {"error": f"{type(e).__name__}: {e}", "seconds": round(time.perf_counter() - t0, 1)}
+    finally:
+        shutil.rmtree(workdir, ignore_errors=True)
+
+
+def pmc_traffic(alg_bytes):
+    """HBM bytes per launch from the committed rocprofv3 PMC record of this
+    launch shape (FETCH_SIZE / WRITE_SIZE, separate passes), with its source.
+    Used only when the live passes (live_pmc_traffic) are off or failed."""
+    if not os.path.exists(PMC_FILE):
+        return None, None
+    try:
+        rec = json.load(open(PMC_FILE))
+    except (OSError, ValueError):
+        return None, None
+    if rec.get("algorithmic_read_bytes", 0) + rec.get("algorithmic_write_bytes", 0) != alg_bytes:
+        return None, None
+    src = {"file": os.path.relpath(PMC_FILE, ROOT), "round": rec.get("round"),
+           "box": rec.get("box"), "kernel": rec.get("kernel"), "how": rec.get("source"),
+           "ratio_to_algorithmic": rec.get("ratio_to_algorithmic"),
+           "rocprof_trace_mean_launch_ms": (rec.get("trace") or {}).get("mean_ms")}
+    return rec.get("hbm_bytes_per_launch"), src
+
+
+# ---------------------------------------------------------------- c5
+def c5_make_file(path, nbytes, seed=5):
+    """Synthetic file bytes (splitmix64 on the GPU, 256 MiB pieces)."""
+    import torch
+    from bfrs import synth
+    piece = 256 << 20
+    buf = torch.empty(piece + 8, dtype=torch.uint8, device="cuda")
+    with open(path, "wb") as f:
+        left, i = nbytes, 0
+        while left:
+            c = min(left, piece)
+            c8 = (c + 7) // 8 * 8
+            synth.fill_segment_torch(buf[:c8], seed, i)
+            f.write(buf[:c].cpu().numpy().tobytes())
+            left -= c
+            i += 1
+    del buf
+
+
+def run_c5(args, ctx=None):
+    """BASELINE configs[4]: FUSE read of a corrupted large file.  The mount's
+    read() core (src/mount/filesystem_unix.rs:176-305) is bfrs_archive_read:
+    offset -> segment, LRU cache, device BLAKE3 on every miss, RS(k,3) block
+    reconstruction on the GPU with device re-verify, prefetch.  Driven
+    in-process with FUSE-sized sequential reads (no kernel mount on the
+    boxes); files sit in the page cache (written by this run), so this is the
+    read path, not the disk.  value = file bytes / time of the sequential read
+    of the corrupted archive (3 bit-flipped segments per block)."""
+    import shutil
+    import tempfile
+    import numpy as np
+    import bfrs
+    own = ctx is None
+    if own:
+        ctx = bfrs.Context(0)
+    work = tempfile.mkdtemp(prefix="bfrs_c5_", dir=args.c5_dir)
+    try:
+        n = int(args.c5_gib * (1 << 30)) + 12345  # ragged tail segment
+        src = os.path.join(work, "large.bin")
+        c5_make_file(src, n)
+        t0 = time.perf_counter()
+        adir = bfrs.commit(ctx, src, os.path.join(work, "archive"), segment_size=args.segment_bytes)
+        commit_s = time.perf_counter() - t0
+        # the same commit again: the context's staging is pinned by now
+        t0 = time.perf_counter()
+        bfrs.commit(ctx, src, os.path.join(work, "again"), segment_size=args.segment_bytes)
+        commit_again_s = time.perf_counter() - t0
+        shutil.rmtree(os.path.join(work, "again"))
+        os.unlink(src)
+        m = json.load(open(os.path.join(adir, "manifest.json")))
+        want = m["original_hash"]
+
+        def sweep(c):
+            with bfrs.Archive(c, adir, cache_segments=64) as a:
+                out = np.empty(n, np.uint8)
+                out[::4096] = 0  # fault the destination in before timing
+                rb = args.c5_read_bytes
+                t = time.perf_counter()
+                off = 0
+                base = out.__array_interface__["data"][0]
+                read = a.read_into_ptr
+                while off < n:  # FUSE-sized reads straight into the caller's buffer
+                    off += read(off, base + off, min(rb, n - off))
+                return time.perf_counter() - t, a.stats(), out
+
+        clean_s, clean_st, out = sweep(ctx)
+        clean_ok = bfrs.blake3_hex(out, threads=16) == want
+        del out
+        rng = np.random.default_rng(6)
+        damaged = []
+        for b, blk in sorted(m["merkle_tree"]["blocks"].items(), key=lambda kv: int(kv[0])):
+            for s in sorted(rng.choice(len(blk["segments"]), size=min(3, len(blk["segments"])),
+                                       replace=False).tolist()):
+                p = os.path.join(adir, "blocks", f"block_{b}", "segments", f"segment_{s}.dat")
+                with open(p, "r+b") as f:
+                    f.seek(int(rng.integers(0, os.path.getsize(p))))
+                    c = f.read(1)
+                    f.seek(-1, 1)
+                    f.write(bytes([c[0] ^ 0xFF]))
+                damaged.append((int(b), s))
+        dirty_s, dirty_st, out = sweep(ctx)
+        ok = clean_ok and bfrs.blake3_hex(out, threads=16) == want
+        del out
+        # the same read on a context of its own: its segment pool is pinned
+        # during the read (the handles above share the first one's pool)
+        cold_ctx = bfrs.Context(ctx.device)
+        try:
+            cold_s, _, out = sweep(cold_ctx)
+        finally:
+            cold_ctx.close()
+        ok = ok and bfrs.blake3_hex(out, threads=16) == want
+        del out
+        res = {
+            "metric": "MB/s end-to-end read of a corrupted tier-3 file (BASELINE configs[4])",
+            "value": round(n / dirty_s / 1e6, 1), "unit": "MB/s",
+            "workload": "configs[4]: 4 GiB tier-3 archive, 3 bit-flipped segments per block, "
+                        "sequential 128 KiB reads through bfrs_archive_read; files in the page cache",
+            "bytes": n, "segment_bytes": args.segment_bytes, "read_bytes": args.c5_read_bytes,
+            "blocks": len(m["merkle_tree"]["blocks"]), "damaged_segments": len(damaged),
+            "clean_read_MBps": round(n / clean_s / 1e6, 1),
+            "corrupted_read_fresh_context_MBps": round(n / cold_s / 1e6, 1),
+            "handles": "clean sweep = the context's first read handle (pins the segment pool); "
+                       "value = a second handle on that context, as a long-lived mount serves "
+                       "its reads; corrupted_read_fresh_context_MBps = the value's read on a "
+                       "new context",
+            "commit_MBps": round(n / commit_s / 1e6, 1),
+            "commit_again_MBps": round(n / commit_again_s / 1e6, 1),
+            "stats_corrupted": dirty_st, "stats_clean": clean_st, "blake3_match": ok,
+        }
+        if args.cpu_baseline == "auto":  # reads the damaged files: before the repair below
+            res["cpu_baseline"] = c5_cpu_baseline(adir, m, damaged, n)
+        res["repair"] = c5_repair(ctx, adir, n, len(damaged))
+        return res
+    finally:
+        shutil.rmtree(work, ignore_errors=True)
+        if own:
+            ctx.close()
+
+
+def c5_repair(ctx, adir, nbytes, n_damaged):
+    """The callers either side of the read path on the same damaged archive
+    (rows a4/f1): FileStore::health_check (health.rs:111-438) and
+    FileStore::repair (health.rs:470-495), intended semantics (every shard
+    hashed on the device, RS(k,3) decode of each damaged block, restored
+    bytes re-verified and written to their own in-block index), then a second
+    health check that must say Healthy.  MB/s = file bytes / wall time."""
+    import bfrs
+    t0 = time.perf_counter()
+    before = bfrs.health_check(ctx, adir)
+    t1 = time.perf_counter()
+    rep = bfrs.repair(ctx, adir)
+    t2 = time.perf_counter()
+    after = bfrs.health_check(ctx, adir)
+    ok = (before.get("status") == "Recoverable" and after.get("status") == "Healthy"
+          and rep.get("segments_repaired") == n_damaged)
+    return {"health_check_MBps": round(nbytes / (t1 - t0) / 1e6, 1),
+            "repair_MBps": round(nbytes / (t2 - t1) / 1e6, 1),
+            "status_before": before.get("status"), "status_after": after.get("status"),
+            "report": rep, "match": ok,
+            "what": "bfrs_health_check, bfrs_repair, bfrs_health_check on the damaged archive "
+                    "(files in the page cache)"}
+
+
+def c5_cpu_baseline(adir, m, damaged, nbytes):
+    """CPU port of the reference's read path, one thread (the FUSE daemon is
+    single-threaded, &mut self), timed on a bounded sample of the same
+    archive: (a) a clean-segment miss = read + BLAKE3 verify; (b) a damaged-
+    segment miss = read + verify (mismatch), then recover_segment_rs30_3 with
+    its intended semantics (recovery.rs:118-173): read + verify the block's
+    other segments and parity, RS(30,3) decode (oracle AVX2 engine), verify
+    the restored segment.  The whole-file rate is derived: clean misses for
+    the undamaged segments, one recovery per damaged segment (the reference
+    recovers per missed segment)."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    eng = oracle.ENGINE_AVX2 if oracle.lib().oracle_have_avx2() else oracle.ENGINE_SCALAR
+    S = m["segment_size"]
+    b, target = damaged[0]
+    blk = m["merkle_tree"]["blocks"][str(b)]
+    seg_path = lambda s: os.path.join(adir, "blocks", f"block_{b}", "segments", f"segment_{s}.dat")
+    par_path = lambda p: os.path.join(adir, "blocks", f"block_{b}", "parity", f"block_parity_{p}.dat")
+    read = lambda p: np.fromfile(p, dtype=np.uint8)
+    clean = next(s for s in range(len(blk["segments"])) if (b, s) not in damaged)
+    t0 = time.perf_counter()
+    d = read(seg_path(clean))
+    assert oracle.blake3_hex(d) == blk["segments"][clean]
+    t_clean = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    d = read(seg_path(target))
+    assert oracle.blake3_hex(d) != blk["segments"][target]
+    segs = []
+    for s in range(len(blk["segments"])):
+        if s == target:
+            segs.append(None)
+            continue
+        x = read(seg_path(s))
+        good = oracle.blake3_hex(x) == blk["segments"][s]
+        if good and x.size < S:
+            x = np.concatenate([x, np.zeros(S - x.size, np.uint8)])
+        segs.append(x if good else None)
+    par = []
+    for p in range(3):
+        x = read(par_path(p))
+        par.append(x if oracle.blake3_hex(x) == blk["parity"][p] else None)
+    restored = oracle.decode(segs, par, eng)[target]
+    assert oracle.blake3_hex(restored[:d.size]) == blk["segments"][target]
+    t_recover = time.perf_counter() - t0
+    nseg = -(-nbytes // S)
+    total = (nseg - len(damaged)) * t_clean + len(damaged) * t_recover
+    return {
+        "value": round(nbytes / total / 1e6, 1), "unit": "MB/s", "cores": 1, "kind": "port",
+        "engine": "avx2" if eng == oracle.ENGINE_AVX2 else "scalar",
+        "clean_segment_miss_s": round(t_clean, 4), "damaged_segment_recovery_s": round(t_recover, 3),
+        "sample": f"one clean-segment miss and one damaged-segment recovery (block {b}, RS(30,3), "
+                  f"{S >> 20} MiB segments) timed; file rate derived for {nseg} segments of which "
+                  f"{len(damaged)} damaged (restatement of blake3 + reed-solomon-simd, not the crates)",
+    }
+
+
+# ---------------------------------------------------------------- main
+def stub_leg_standins():
+    """CPU stand-ins for the side legs (--stub-legs-builtin: the supervisor
+    and launcher tests run bench.py as a subprocess, where they cannot
+    monkeypatch); each reports a passing check and says it is a stand-in."""
+    return {
+        "check_config1": lambda ctx: {"match": True, "stub": True},
+        "blake3_device": lambda ctx, sets: {"bytes": 0, "parity_check": {"match": True},
+                                            "stub": True},
+        "pcie_inclusive": lambda ctx, sets: {"decode_match": True, "stub": True},
+        "crate_api": lambda ctx, sets: {"recover_match": True, "stub": True},
+        "cpu_baseline": lambda args, sets, info: {"self_check": True, "stub": True},
+        "run_c5": lambda args, ctx: {"blake3_match": True, "repair": {"match": True},
+                                     "stub": True},
+        "c4_one_process": lambda args, ctx, world, one: {"match": True, "contexts": world,
+                                                         "stub": True},
+    }

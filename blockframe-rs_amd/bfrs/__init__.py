@@ -73,6 +73,48 @@ class BfrsError(RuntimeError):
 
 _lib: Optional[ctypes.CDLL] = None
 
+# Live handles, for the ordered close at interpreter exit.
+# Left to the garbage collector, objects still alive at exit are finalised in
+# no particular order -- a context's __del__ may run before that of an
+# archive handle whose prefetch threads still use it -- or not at all, so the
+# HIP runtime's own teardown would meet live streams and pinned memory.
+import atexit
+import weakref
+
+_LIVE_ARCHIVES: "weakref.WeakSet" = weakref.WeakSet()
+_LIVE_CODECS: "weakref.WeakSet" = weakref.WeakSet()
+_LIVE_CONTEXTS: "weakref.WeakSet" = weakref.WeakSet()
+
+
+def close_all() -> None:
+    """Close every live handle in dependency order: archive handles (their
+    prefetch threads are joined), then encoder / decoder objects, then each
+    context after a device synchronize.  Registered with atexit; safe to call
+    more than once."""
+    for a in list(_LIVE_ARCHIVES):
+        try:
+            a.close()
+        except Exception:
+            pass
+    for o in list(_LIVE_CODECS):
+        try:
+            o.free()
+        except Exception:
+            pass
+    for c in list(_LIVE_CONTEXTS):
+        try:
+            if c.handle:
+                c.synchronize()
+        except Exception:
+            pass
+        try:
+            c.close()
+        except Exception:
+            pass
+
+
+atexit.register(close_all)
+
 
 class RepairReport(ctypes.Structure):
     """bfrs_repair_report (include/bfrs.h)."""
@@ -320,8 +362,12 @@ class Context:
         _check(lib().bfrs_open(device, ctypes.byref(h)))
         self.handle = h
         self.device = device
+        _LIVE_CONTEXTS.add(self)
 
     def close(self) -> None:
+        """bfrs_close: archive handles still open on the context are detached
+        by the library (their threads joined; later reads fail), codec objects
+        stay valid to free."""
         if self.handle:
             lib().bfrs_close(self.handle)
             self.handle = None
@@ -561,11 +607,15 @@ class ReedSolomonEncoder:
         _check(lib().bfrs_encoder_new(ctx.handle, original_count, recovery_count, shard_bytes,
                                       ctypes.byref(h)))
         self.handle, self.ctx, self.recovery_count = h, ctx, recovery_count
+        _LIVE_CODECS.add(self)
 
-    def __del__(self):
+    def free(self) -> None:
         if getattr(self, "handle", None):
             lib().bfrs_encoder_free(self.handle)
             self.handle = None
+
+    def __del__(self):
+        self.free()
 
     def _h(self):
         return _live_codec(self)
@@ -598,11 +648,15 @@ class ReedSolomonDecoder:
         _check(lib().bfrs_decoder_new(ctx.handle, original_count, recovery_count, shard_bytes,
                                       ctypes.byref(h)))
         self.handle, self.ctx = h, ctx
+        _LIVE_CODECS.add(self)
 
-    def __del__(self):
+    def free(self) -> None:
         if getattr(self, "handle", None):
             lib().bfrs_decoder_free(self.handle)
             self.handle = None
+
+    def __del__(self):
+        self.free()
 
     def _h(self):
         return _live_codec(self)
@@ -905,6 +959,7 @@ class Archive:
                                        1 if write_back else 0, ctypes.byref(h)))
         self.handle = h.value
         self._read = lib().bfrs_archive_read
+        _LIVE_ARCHIVES.add(self)
 
     @property
     def size(self) -> int:

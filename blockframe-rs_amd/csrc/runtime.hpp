@@ -30,6 +30,22 @@ inline size_t shard_pitch(size_t shard_bytes) {
   return p + (12288 + 65536 - p % 65536) % 65536;
 }
 
+// Makes `dev` current for a scope and restores the caller's device after it:
+// the last codec object of a pool may be freed on any thread (a GC running
+// in a worker bound to another GPU), which must not be left switched to this
+// pool's device.
+struct DeviceScope {
+  int prev = -1;
+  explicit DeviceScope(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (dev >= 0 && dev != prev) (void)hipSetDevice(dev);
+  }
+  ~DeviceScope() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
 // Thread-local error reporting (bfrs_last_error).
 int set_error(int code, const std::string &msg);
 int hip_error(hipError_t e, const char *what);
@@ -182,6 +198,14 @@ struct Context {
   std::shared_ptr<void> staging;
   std::mutex staging_init;
 
+  // Read handles open on this context (bfrs_archive_open).  bfrs_close
+  // detaches them first (detach_archives): their prefetch threads are joined
+  // and they drop everything of the context, so a handle closed after its
+  // context -- a drop order the caller may not control -- touches nothing
+  // freed, and no thread of the library outlives the context.
+  std::mutex handles_mu;
+  std::vector<bfrs_archive *> handles;
+
   // BLAKE3 (hash_gpu.cpp): device work area + pinned descriptor/result area,
   // guarded by hash_mu (callers on several threads may share a context).
   std::mutex hash_mu;
@@ -240,6 +264,9 @@ struct bfrs_ctx {
 };
 
 namespace bfrs {
+// bfrs_close's first step (archive.cpp): stop and detach every read handle
+// still open on the context.
+void detach_archives(bfrs_ctx *ctx);
 // Pointer and shape checks of the host-memory batch API (one block list).
 int check_host_batch(bfrs_ctx *ctx, size_t nblocks, const uint32_t *ks, size_t m,
                      size_t shard_bytes, bool decode, const uint8_t *const *orig,

@@ -567,6 +567,86 @@ def test_handles_share_the_segment_pool(ctx, bfrs, tmp_path):
         assert h.read(0, a_d.size) == a_d.tobytes()
 
 
+def test_context_closed_before_its_archive_handle(bfrs, tmp_path):
+    """bfrs_close with a read handle still open (its
+    prefetch workers running, a damaged block queued) joins the handle's
+    threads and detaches it; a later read fails with an error naming the
+    closed context and closing the handle afterwards touches nothing freed.
+    (A Rust caller's Drop order, or a Python GC at exit, may close the context
+    first.)"""
+    c = bfrs.Context(0)
+    adir, d = _tier3(c, bfrs, tmp_path)
+    _flip(os.path.join(adir, "blocks", "block_1", "segments", "segment_3.dat"), 77)
+    a = bfrs.Archive(c, adir, cache_segments=16)
+    assert a.read(0, 2 * SEG) == d[:2 * SEG].tobytes()  # prefetch now runs ahead
+    c.close()
+    with pytest.raises(bfrs.BfrsError) as e:
+        a.read(0, 10)
+    assert e.value.code == bfrs.E_INVALID_ARGUMENT and "context was closed" in str(e.value)
+    assert a.size == d.size  # the geometry stays readable
+    a.close()
+    # the same archive on a new context reads back whole, the damaged block included
+    c2 = bfrs.Context(0)
+    try:
+        with bfrs.Archive(c2, adir, cache_segments=16) as h:
+            assert h.read(0, d.size) == d.tobytes()
+    finally:
+        c2.close()
+
+
+_LEAVE_OPEN_SCRIPT = r"""
+import os, sys
+import numpy as np
+root, mode, work = sys.argv[1], sys.argv[2], sys.argv[3]
+sys.path.insert(0, os.path.join(root, "blockframe-rs_amd"))
+import bfrs
+if mode == "gc":  # no ordered close: the interpreter's finalisation order decides
+    import atexit
+    atexit.unregister(bfrs.close_all)
+SEG = 256 * 1024
+ctx = bfrs.Context(0)
+d = np.random.default_rng(7).integers(0, 256, 45 * SEG + 321, dtype=np.uint8)
+src = os.path.join(work, "f.bin")
+d.tofile(src)
+adir = bfrs.commit(ctx, src, os.path.join(work, "archive"), segment_size=SEG, tier=3)
+seg = os.path.join(adir, "blocks", "block_1", "segments", "segment_2.dat")
+b = bytearray(open(seg, "rb").read()); b[5] ^= 1; open(seg, "wb").write(bytes(b))
+a = bfrs.Archive(ctx, adir, cache_segments=16)
+assert a.read(0, SEG) == d[:SEG].tobytes()  # prefetch workers running, block 1 queued
+rng = np.random.default_rng(1)
+shards = [rng.integers(0, 256, 1 << 20, dtype=np.uint8) for _ in range(30)]
+enc = bfrs.ReedSolomonEncoder(ctx, 30, 3, 1 << 20)
+for x in shards:
+    enc.add_original_shard(x)
+enc.encode()
+view = enc.recovery_view(0)
+dec = bfrs.ReedSolomonDecoder(ctx, 30, 3, 1 << 20)
+for i in range(1, 30):
+    dec.add_original_shard(i, shards[i])
+if mode == "ctx_first":  # the context closed while the handle and objects live on
+    ctx.close()
+print("left open:", mode, flush=True)
+"""
+
+
+@pytest.mark.parametrize("mode", ["atexit", "gc", "ctx_first"])
+def test_exit_with_handles_left_open(tmp_path, mode):
+    """a process that leaves a context, a read handle with
+    running prefetch threads, an encoder (and a view of its row) and a
+    half-filled decoder open exits normally with status 0: through the
+    binding's ordered close (atexit), through the interpreter's own
+    finalisation order (no atexit close), and with the context closed before
+    the rest (bfrs_close detaches the handle)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-X", "faulthandler", "-c", _LEAVE_OPEN_SCRIPT, root, mode,
+                        str(tmp_path)], capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, (r.returncode, r.stdout[-1000:], r.stderr[-3000:])
+    assert f"left open: {mode}" in r.stdout
+    assert "Fatal Python error" not in r.stderr and "Segmentation fault" not in r.stderr
+
+
 def test_repair_tier3_parity_only(ctx, bfrs, tmp_path):
     adir, d = _tier3(ctx, bfrs, tmp_path)
     pdir = os.path.join(adir, "blocks", "block_1", "parity")
@@ -732,6 +812,18 @@ def test_config5_full_size_corrupted_read(ctx, bfrs, oracle, tmp_path):
             off += a.read_into_ptr(off, base + off, min(rb, n - off))
         st = a.stats()
     assert st["recovered_segments"] == 15
+    # the served bytes against the regenerated source bytes
+    # directly (no product hash path in between), piece by piece on the GPU
+    buf = torch.empty(piece + 8, dtype=torch.uint8, device="cuda")
+    left, i = n, 0
+    while left:
+        c = min(left, piece)
+        synth.fill_segment_torch(buf[:(c + 7) // 8 * 8], 5, i)
+        got = torch.from_numpy(out[i * piece:i * piece + c]).cuda()
+        assert torch.equal(got, buf[:c]), f"served bytes differ in piece {i}"
+        left -= c
+        i += 1
+    del buf, got
     assert bfrs.blake3_hex(out, threads=16) == m["original_hash"]
     roots = []
     for b in range(5):

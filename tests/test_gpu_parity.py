@@ -953,6 +953,77 @@ def test_failed_slab_call_leaves_its_slot_reusable():
     assert r.returncode == 0 and "reuse ok" in r.stdout, (r.stdout[-1000:], r.stderr[-2000:])
 
 
+_LDS_VARIANT_SCRIPT = r'''
+import os, sys
+import numpy as np
+root = os.environ["BFRS_TEST_ROOT"]
+sys.path.insert(0, os.path.join(root, "blockframe-rs_amd"))
+sys.path.insert(0, os.path.join(root, "oracle"))
+import bfrs, oracle
+assert bfrs.LIB_PATH.endswith("libbfrs_ab.so"), bfrs.LIB_PATH
+ctx = bfrs.Context(0)
+rng = np.random.default_rng(0x1D5)
+eng = oracle.ENGINE_AVX2 if oracle.lib().oracle_have_avx2() else oracle.ENGINE_SCALAR
+n_cases = 0
+# shard sizes: one chunk, a ragged wave run, ragged tiles with a tail, several
+# read groups of whole tiles
+sizes = [64, 64 * 63 + 10, 64 * 300 + 38, (1 << 20) + 64 * 3, (3 << 20) + 64 * 77 + 2]
+for v in os.environ["LDS_VARIANTS"].split(","):
+    os.environ["BFRS_KERNEL_VARIANT"] = v
+    for k in (30, 29, 20, 19, 8, 7):   # odd k: padded to 30 / 20 / 8, unrotated
+        for S in sizes:
+            segs = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(k)]
+            want = oracle.encode(segs, 3, eng)
+            got = ctx.encode(segs, 3)
+            assert all(np.array_equal(got[j], want[j]) for j in range(3)), (v, k, S, "encode")
+            er = sorted(rng.choice(k, size=min(3, k), replace=False).tolist())
+            rec = [w.copy() for w in want]
+            if S > 64 and k > 3:   # a corrupted recovery shard: the crate decoder's linear map
+                er = er[:2]
+                rec[2][int(rng.integers(0, S))] ^= 0x5A
+            orig = [None if i in er else segs[i] for i in range(k)]
+            out = ctx.decode(orig, rec)
+            ref = oracle.decode(orig, rec, eng)
+            for i in er:
+                assert np.array_equal(out[i], ref[i]), (v, k, S, "decode", i)
+            n_cases += 2
+    # one launch holding blocks of different n_in (the C2 / C4 last-block shape)
+    S = (2 << 20) + 64 * 9
+    ks = [30, 8, 20]
+    segs = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(sum(ks))]
+    outs = [np.empty(S, np.uint8) for _ in range(3 * len(ks))]
+    ctx.encode_host_batch(ks, 3, S, segs, outs)
+    off = 0
+    for b, k in enumerate(ks):
+        want = oracle.encode(segs[off:off + k], 3, eng)
+        assert all(np.array_equal(outs[3 * b + j], want[j]) for j in range(3)), (v, "batch", k)
+        off += k
+    n_cases += len(ks)
+ctx.close()
+print(f"lds variants ok: {n_cases} cases")
+'''
+
+
+def test_lds_dma_variants_match_the_oracle():
+    """Round 6 (VERDICT r5 item 2): the measurement build's LDS-DMA input-ring
+    kernels (v107-v109: 4 KiB per wave and input staged with
+    global_load_lds_dwordx4) against the oracle before any timing is trusted:
+    RS(k,3) encodes and decodes (incl. a corrupted recovery shard) for every
+    unrolled size and its odd neighbour, shard sizes from one chunk to ragged
+    multi-group runs with tails, and one launch mixing n_in 30 / 8 / 20.  Runs
+    in a child on libbfrs_ab.so (the product does not carry them)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if not os.path.exists(os.path.join(root, "blockframe-rs_amd", "libbfrs_ab.so")):
+        pytest.skip("libbfrs_ab.so not built (make -C blockframe-rs_amd/csrc ab)")
+    env = dict(os.environ, BFRS_LIB="libbfrs_ab.so", BFRS_TEST_ROOT=root,
+               LDS_VARIANTS="107,108,109")
+    r = subprocess.run([sys.executable, "-c", _LDS_VARIANT_SCRIPT], capture_output=True,
+                       text=True, timeout=300, env=env)
+    assert r.returncode == 0 and "lds variants ok" in r.stdout, (r.stdout[-1000:], r.stderr[-2000:])
+
+
 @pytest.mark.parametrize("n", [64 * 150 + 38, (16 << 20) + 64 * 5 + 38])
 def test_host_batch_pinned_strided_rows_vs_oracle(ctx, oracle, n):
     """Pinned shard rows at a constant pitch (one pinned tensor, as the bench

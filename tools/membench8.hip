@@ -189,13 +189,13 @@ __global__ __launch_bounds__(64 * WAVES) void probe(Args a) {
 // LDS-DMA staging variant: each wave streams its NL KiB run of input i into an
 // LDS ring slot with global_load_lds_dwordx4 (M0 = slot base), D+1 slots per
 // wave, then reads it back with ds_read_b128.  Traffic-only like `probe`.
-template <int K, int O, int NL, int NTL, int NTS, int D>
-__global__ __launch_bounds__(256) void probe_lds(Args a) {
+template <int K, int O, int NL, int NTL, int NTS, int D, int WAVES = 4>
+__global__ __launch_bounds__(64 * WAVES) void probe_lds(Args a) {
   extern __shared__ __attribute__((aligned(16))) u32x4 lds[];
   const uint32_t wg = xcd_remap16(blockIdx.x, gridDim.x);
   const uint32_t blk = wg / a.tiles_per_block, tile = wg % a.tiles_per_block;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const uint32_t col0 = (tile * 4 + wave) * NL * 1024;
+  const uint32_t col0 = (tile * WAVES + wave) * NL * 1024;
   const AS_CONST uint64_t *in = (const AS_CONST uint64_t *)(uintptr_t)(a.in + size_t(blk) * K);
   const uint32_t rot = K > 1 ? ((tile >> 4) * 4) % K : 0;
   // per-wave ring of D+1 slots of NL KiB
@@ -332,17 +332,20 @@ void run(const char *tag, int occ = 0) {
                                          dim3(64 * WAVES), lds, 0, a); }, bytes);
 }
 
-template <int K, int O, int NL, int NTL, int NTS, int D>
-void run_lds(const char *tag) {
+// extra_lds: bytes reserved on top of the ring (the computing kernel's nibble
+// tables, 30 x 512 B), so the probe runs at the kernel's workgroups per CU
+template <int K, int O, int NL, int NTL, int NTS, int D, int WAVES = 4>
+void run_lds(const char *tag, size_t extra_lds = 0) {
   constexpr uint32_t B = kShards / K;
-  const uint32_t wg_bytes = 4 * NL * 1024;
+  const uint32_t wg_bytes = WAVES * NL * 1024;
   Args a = make_args<K, O>(wg_bytes);
   const double bytes = double(kS) * B * (K + O);
-  const size_t lds = size_t(4) * (D + 1) * NL * 1024;
+  const size_t lds = size_t(WAVES) * (D + 1) * NL * 1024 + extra_lds;
   char name[160];
-  snprintf(name, sizeof name, "%s_lds_k%d_o%d_nl%d_ntl%d_nts%d_d%d", tag, K, O, NL, NTL, NTS, D);
-  timeit(name, [&] { hipLaunchKernelGGL((probe_lds<K, O, NL, NTL, NTS, D>), dim3(a.total_tiles),
-                                         dim3(256), lds, 0, a); }, bytes);
+  snprintf(name, sizeof name, "%s_lds_k%d_o%d_nl%d_ntl%d_nts%d_d%d_w%d_x%zu", tag, K, O, NL, NTL,
+           NTS, D, WAVES, extra_lds);
+  timeit(name, [&] { hipLaunchKernelGGL((probe_lds<K, O, NL, NTL, NTS, D, WAVES>), dim3(a.total_tiles),
+                                         dim3(64 * WAVES), lds, 0, a); }, bytes);
 }
 
 int main(int argc, char **argv) {
@@ -434,6 +437,32 @@ int main(int argc, char **argv) {
       run<30, 3, 4, 0, 1, 1, 2, 1, 0, 4>("rs", 4);   // 4 KiB/wave, 16 KiB/WG
       run<30, 3, 1, 0, 1, 1, 2, 1, 0, 8>("rs", 5);   // 1 KiB/wave, 8 KiB/WG
       run<30, 3, 2, 0, 1, 1, 2, 1, 0, 16>("rs", 5);  // 2 KiB/wave, 32 KiB/WG
+    }
+    if (!strcmp(only, "ldsplace") && rep == 0) {
+      // round 6: the LDS-DMA ring at the occupancy of the
+      // computing kernels v107-v109 (tables reserved), beside the register
+      // probes, on six separately allocated data sets
+      const int copies = 6;
+      std::vector<uint8_t *> keep;
+      for (int c = 0; c < copies; ++c) {
+        uint8_t *d = nullptr;
+        CHECK(hipMalloc(&d, g.pitch * kShards));
+        CHECK(hipMemset(d, 0x5a, g.pitch * kShards));
+        keep.push_back(d);
+      }
+      for (int c = 0; c < copies; ++c) {
+        g.data = keep[c];
+        char t[32];
+        snprintf(t, sizeof t, "c%d_rs", c);
+        run<30, 3, 2, 0, 1, 1, 2, 1, 0, 4>(t, 5);  // product: 2 KiB/wave, registers, 5 waves/SIMD
+        run<30, 3, 4, 0, 1, 1, 2, 1, 0, 4>(t, 4);  // 4 KiB/wave, registers
+        // probe_lds keeps D+1 slots (its D is the inputs in flight past the
+        // consumed one): D=1 -> 2 slots = the kernels' D=2 ring
+        run_lds<30, 3, 4, 1, 1, 1, 8>(t, 15360);   // v107: 8 waves, 2 slots: 2 WGs/CU
+        run_lds<30, 3, 4, 1, 1, 1, 4>(t, 15360);   // v108: 4 waves, 2 slots: 3 WGs/CU
+        run_lds<30, 3, 4, 1, 1, 2, 4>(t, 15360);   // v109: 4 waves, 3 slots: 2 WGs/CU
+      }
+      return 0;
     }
     if (!strcmp(only, "place") && rep == 0) {
       // placement study: the same patterns on several separately

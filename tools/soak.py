@@ -31,7 +31,18 @@ def main():
     ap.add_argument("--huge", type=float, default=0.0,
                     help="this fraction of cases with 8-40 MiB shards (k <= 6, ragged sizes): "
                          "the threaded staging copies and their shared budget (host_copy.cpp)")
+    ap.add_argument("--maps", default=None,
+                    help="write /proc/self/maps here after the context opens and again at the "
+                         "end, so the raw PCs of a fault handler's stack resolve to DSO + offset "
+                         "(default: gpurun_out/soak_<pid>.maps if gpurun_out/ exists)")
     a = ap.parse_args()
+    if a.maps is None and os.path.isdir("gpurun_out"):
+        a.maps = f"gpurun_out/soak_{os.getpid()}.maps"
+
+    def write_maps(tag):
+        if a.maps:
+            with open("/proc/self/maps") as f, open(a.maps, "w") as o:
+                o.write(f"# {tag}, pid {os.getpid()}\n" + f.read())
     os.environ.setdefault("BFRS_PLAN_CACHE", "16")
     import numpy as np
     import torch
@@ -39,6 +50,7 @@ def main():
     import oracle
 
     ctx = bfrs.Context(0)
+    write_maps("after bfrs_open")
     stats = {"cases": 0, "bytes": 0, "by_api": {}, "failures": []}
     lock = threading.Lock()
     # What every thread is running right now (case number, API, shape, start
@@ -243,6 +255,7 @@ def main():
     stats["threads"] = a.threads
     stats["huge_fraction"] = a.huge
     stats["seconds"] = a.seconds
+    write_maps("at the end")
     print(json.dumps(stats))
     return 1 if stats["failures"] else 0
 
