@@ -664,7 +664,7 @@ struct PinnedPool {
   std::vector<uint8_t *> free_, all_;
   explicit PinnedPool(size_t s) : slot(std::max<size_t>(256, (s + 255) / 256 * 256)) {}
   ~PinnedPool() {
-    for (uint8_t *p : all_) (void)hipHostFree(p);
+    for (uint8_t *p : all_) pinned_free(p, slot);
   }
   uint8_t *get() {
     {
@@ -675,8 +675,8 @@ struct PinnedPool {
         return p;
       }
     }
-    void *p = nullptr;
-    if (hipHostMalloc(&p, slot, hipHostMallocDefault) != hipSuccess) return nullptr;
+    void *p = pinned_alloc(slot);
+    if (!p) return nullptr;
     std::lock_guard<std::mutex> g(mu);
     all_.push_back(static_cast<uint8_t *>(p));
     return static_cast<uint8_t *>(p);
@@ -702,7 +702,7 @@ struct PinnedPool {
         all_.erase(std::find(all_.begin(), all_.end(), drop.back()));
       }
     }
-    for (uint8_t *p : drop) (void)hipHostFree(p);
+    for (uint8_t *p : drop) pinned_free(p, slot);
   }
 };
 // idle pinned segment buffers a context keeps per segment size: 2 GiB, >= 8

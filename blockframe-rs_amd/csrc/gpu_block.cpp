@@ -11,7 +11,7 @@
 namespace bfrs {
 
 Arena::~Arena() {
-  if (h) (void)hipHostFree(h);
+  pinned_free(h, slot * nslots);
   if (d) (void)hipFree(d);
 }
 
@@ -23,7 +23,7 @@ int Arena::reserve(size_t slot_bytes, size_t n, unsigned parts) {
   parts |= (h ? kArenaHost : 0u) | (d ? kArenaDevice : 0u);
   if (h || d) HIP_TRY(hipDeviceSynchronize());
   if (h) {
-    HIP_TRY(hipHostFree(h));
+    pinned_free(h, slot * nslots);
     h = nullptr;
   }
   if (d) {
@@ -32,8 +32,10 @@ int Arena::reserve(size_t slot_bytes, size_t n, unsigned parts) {
   }
   slot = std::max(slot, slot_bytes);
   nslots = std::max(nslots, n);
-  if (parts & kArenaHost)
-    HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&h), slot * nslots, hipHostMallocDefault));
+  if (parts & kArenaHost) {
+    h = static_cast<uint8_t *>(pinned_alloc(slot * nslots));
+    if (!h) return set_error(BFRS_E_NOMEM, "pinned staging arena allocation failed");
+  }
   if (parts & kArenaDevice) HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d), slot * nslots));
   return BFRS_OK;
 }

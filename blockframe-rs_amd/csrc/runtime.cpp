@@ -5,6 +5,8 @@
 // There is no CPU compute path: without a HIP device every codec entry point
 // fails with BFRS_E_NO_DEVICE.
 #include "runtime.hpp"
+
+#include <sys/mman.h>
 #include "knobs.hpp"
 
 #include <algorithm>
@@ -100,6 +102,63 @@ int copy_rows(const std::vector<RowCopy> &rows, size_t len, hipMemcpyKind kind, 
 }
 }  // namespace
 
+namespace {
+constexpr size_t kHugePage = size_t(2) << 20;
+#ifndef MADV_POPULATE_WRITE
+#define MADV_POPULATE_WRITE 23
+#endif
+// the measurement build can force hipHostMalloc for a same-box A/B
+bool pin_by_register() {
+  const char *e = BFRS_AB_KNOB("BFRS_PIN_MODE");
+  return !(e && std::strcmp(e, "malloc") == 0);
+}
+}  // namespace
+
+// below this, hipHostMalloc (a huge-page mapping would round a small buffer
+// up to 2 MiB; the codec slots of small shapes come and go often)
+constexpr size_t kRegisterMin = size_t(4) << 20;
+
+void *pinned_alloc(size_t bytes) {
+  if (bytes == 0) return nullptr;
+  const size_t len = round_up(bytes, kHugePage);
+  if (bytes >= kRegisterMin && pin_by_register()) {
+    // over-allocate by one huge page and trim, so the range is 2 MiB aligned
+    void *raw = mmap(nullptr, len + kHugePage, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS,
+                     -1, 0);
+    if (raw != MAP_FAILED) {
+      const uintptr_t r = reinterpret_cast<uintptr_t>(raw);
+      const uintptr_t a = round_up(r, kHugePage);
+      if (a > r) munmap(raw, a - r);
+      if (r + kHugePage > a) munmap(reinterpret_cast<void *>(a + len), r + kHugePage - a);
+      void *p = reinterpret_cast<void *>(a);
+      (void)madvise(p, len, MADV_HUGEPAGE);
+      if (madvise(p, len, MADV_POPULATE_WRITE) != 0) std::memset(p, 0, len);  // first touch
+      if (hipHostRegister(p, len, hipHostRegisterPortable) == hipSuccess) return p;
+      (void)hipGetLastError();
+      munmap(p, len);
+    }
+  }
+  void *p = nullptr;
+  if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return p;
+}
+
+void pinned_free(void *p, size_t bytes) {
+  if (!p) return;
+  // a registered mapping, or else hipHostMalloc'd (small, or the fallback)
+  if (bytes >= kRegisterMin) {
+    if (hipHostUnregister(p) == hipSuccess) {
+      munmap(p, round_up(bytes, kHugePage));
+      return;
+    }
+    (void)hipGetLastError();
+  }
+  (void)hipHostFree(p);
+}
+
 int set_error(int code, const std::string &msg) {
   g_last_error = msg;
   return code;
@@ -193,7 +252,7 @@ CodecSlot::~CodecSlot() {
     (void)hipStreamDestroy(aux);
   }
   if (d) (void)hipFree(d);
-  if (h) (void)hipHostFree(h);
+  pinned_free(h, stride * nshards);
 }
 
 int CodecPool::init_streams(size_t n, bool copy_streams) {
@@ -236,7 +295,8 @@ int CodecPool::acquire(size_t nshards, size_t shard_bytes, std::unique_ptr<Codec
       s->own_stream = true;
     }
     HIP_TRY(hipMalloc(&s->d, stride * nshards));
-    HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&s->h), stride * nshards, hipHostMallocDefault));
+    s->h = static_cast<uint8_t *>(pinned_alloc(stride * nshards));
+    if (!s->h) return set_error(BFRS_E_NOMEM, "pinned codec slot allocation failed");
   }
   if (!streams.empty()) {  // the shared stream with the fewest live slots
     std::lock_guard<std::mutex> g(mu);

@@ -46,6 +46,17 @@ struct DeviceScope {
   }
 };
 
+// Pinned host memory of the staging buffers (archive segment pools and block
+// arenas): anonymous mmap, 2 MiB aligned, MADV_HUGEPAGE, populated, then
+// hipHostRegister (portable).  hipHostMalloc pinned 5.3-7.0 GB/s on the
+// boxes -- faulting in 4 KiB pages is most of its cost -- against 22.6 GB/s
+// this way, whose register step alone runs ~390 GB/s (tools/pin_probe.py,
+// profiles/r06/pin/), so a first commit or read on a context waits a quarter
+// as long for its staging.  Falls back to hipHostMalloc when
+// any step fails.  pinned_free takes the size pinned_alloc was given.
+void *pinned_alloc(size_t bytes);
+void pinned_free(void *p, size_t bytes);
+
 // Thread-local error reporting (bfrs_last_error).
 int set_error(int code, const std::string &msg);
 int hip_error(hipError_t e, const char *what);

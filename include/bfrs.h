@@ -33,7 +33,12 @@
  *
  * Lifetimes: an encoder or decoder may be freed before or after bfrs_close of
  * its context (it shares the context's slot pool); every other call on it
- * needs the context open.  Free archive handles before bfrs_close.
+ * needs the context open.  An archive handle should be closed before its
+ * context; if it is not, bfrs_close detaches it (joins its prefetch threads
+ * and drops what it holds of the context), later bfrs_archive_read calls on
+ * it fail with BFRS_E_INVALID_ARGUMENT and bfrs_archive_close still frees it.
+ * No library thread outlives bfrs_close.  bfrs_close must not run while
+ * another thread is inside a call on the same context or one of its handles.
  *
  * Environment: libbfrs.so reads exactly these six knobs (tests/test_abi.py
  * checks the BFRS_* strings in the binary against this list).  The knobs of
@@ -374,12 +379,15 @@ typedef struct {
 } bfrs_archive_stats;
 /* Memory: cached segments live in pinned buffers drawn from a pool the
  * context keeps per segment size and shares between its handles (about
- * cache_segments + 8 buffers per handle open at the same time; when a handle
- * closes, idle buffers beyond 2 GiB per segment size are unpinned, the rest
- * stay for the next handle until bfrs_close); a tier-3 handle with prefetch also allocates a
- * block arena (33 HBM segment slots, 22 pinned) at open, on a prefetch
- * thread, and one HBM segment buffer per verification lane (prefetch workers
- * + 1).  Both are freed by bfrs_archive_close. */
+ * cache_segments + 8 buffers per handle open at the same time).  When a
+ * handle closes, idle buffers beyond 2 GiB per segment size are unpinned, and
+ * the pools no open handle uses keep at most 2 GiB of idle buffers together
+ * (the least recently released pools go first); the rest stay for the next
+ * handle until bfrs_close.  The tier-3 block reconstructions of all handles
+ * of a context share ONE block arena (33 HBM segment slots, 22 pinned),
+ * reserved by the first tier-3 handle's prefetch thread and kept until
+ * bfrs_close.  Each handle has one HBM segment buffer per verification lane
+ * (prefetch workers + 1), freed by bfrs_archive_close. */
 int bfrs_archive_open(bfrs_ctx *ctx, const char *archive_dir, size_t cache_segments,
                       int write_back, bfrs_archive **out);
 int bfrs_archive_size(bfrs_archive *a, uint64_t *size);

@@ -511,6 +511,66 @@ def test_archive_concurrent_readers(ctx, bfrs, tmp_path):
     assert st["recovered_segments"] >= 2
 
 
+_WORKERS_SCRIPT = r"""
+import os, sys, threading
+import numpy as np
+root, work = sys.argv[1], sys.argv[2]
+sys.path.insert(0, os.path.join(root, "blockframe-rs_amd"))
+import bfrs
+assert bfrs.LIB_PATH.endswith("libbfrs_ab.so"), bfrs.LIB_PATH
+SEG = 256 * 1024
+ctx = bfrs.Context(0)
+d = np.random.default_rng(9).integers(0, 256, 75 * SEG + 999, dtype=np.uint8)
+src = os.path.join(work, "w.bin")
+d.tofile(src)
+adir = bfrs.commit(ctx, src, os.path.join(work, "archive"), segment_size=SEG, tier=3)
+for b, s in ((0, 2), (1, 5), (1, 29), (2, 3)):
+    p = os.path.join(adir, "blocks", f"block_{b}", "segments", f"segment_{s}.dat")
+    x = bytearray(open(p, "rb").read()); x[11] ^= 0x40; open(p, "wb").write(bytes(x))
+errors = []
+with bfrs.Archive(ctx, adir, cache_segments=12) as a:
+    def reader(seed):
+        rng = np.random.default_rng(seed)
+        try:
+            off = int(rng.integers(0, d.size // 2))
+            while off < d.size:  # sequential runs from random starts, FUSE-sized
+                n = min(128 << 10, d.size - off)
+                if a.read(off, n) != d[off:off + n].tobytes():
+                    errors.append((seed, off))
+                off += n
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+    ts = [threading.Thread(target=reader, args=(s,)) for s in range(6)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    st = a.stats()
+ctx.close()
+assert not errors, errors[:5]
+assert st["recovered_segments"] >= 4, st
+print("workers ok", os.environ["BFRS_PREFETCH_WORKERS"], st["prefetched"])
+"""
+
+
+@pytest.mark.parametrize("workers", ["1", "4"])
+def test_prefetch_worker_counts_with_concurrent_readers(tmp_path, workers):
+    """the verification lanes (a try-lock over the handle's lanes,
+    then a blocking fallback to lanes[gi % n]) under more and fewer prefetch
+    workers than the product's 2: six readers on one handle of a tier-3
+    archive with damage in three blocks, 1 and 4 workers (measurement build,
+    BFRS_PREFETCH_WORKERS), every served byte against the source."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if not os.path.exists(os.path.join(root, "blockframe-rs_amd", "libbfrs_ab.so")):
+        pytest.skip("libbfrs_ab.so not built (make -C blockframe-rs_amd/csrc ab)")
+    env = dict(os.environ, BFRS_LIB="libbfrs_ab.so", BFRS_PREFETCH_WORKERS=workers)
+    r = subprocess.run([sys.executable, "-c", _WORKERS_SCRIPT, root, str(tmp_path)],
+                       capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0 and "workers ok" in r.stdout, (r.stdout[-1000:], r.stderr[-2000:])
+
+
 def test_handles_share_the_segment_pool(ctx, bfrs, tmp_path):
     # the context pins one pool of segment buffers per segment size and lends
     # it to every handle (archive.cpp segment_pool): two handles of the same
