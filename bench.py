@@ -381,6 +381,7 @@ class Runtime:
         import torch
         self.torch = torch
         self.stub = args.stub
+        self.stub_ordinal = 0 if args.one_device else self.local
         if self.stub:
             self.device = torch.device("cpu")
         else:
@@ -405,8 +406,9 @@ class Runtime:
     def device_info(self) -> dict:
         """This rank's device as the process sees it: the HIP ordinal and the
         PCI bus id (distinct ids per rank prove one GPU per rank)."""
-        if self.stub:
-            return {"rank": self.rank, "device": "cpu", "pci_bus_id": None}
+        if self.stub:  # the ordinal the real run binds (cuda:LOCAL_RANK), for the launcher tests
+            return {"rank": self.rank, "device": "cpu", "pci_bus_id": None,
+                    "stub_ordinal": self.stub_ordinal}
         p = self.torch.cuda.get_device_properties(self.device)
         bus = getattr(p, "pci_bus_id", None)
         return {"rank": self.rank, "device": self.torch.cuda.current_device(),

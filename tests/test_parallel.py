@@ -226,3 +226,10 @@ def test_torchrun_two_ranks_supervised_line():
     assert line["n_gpus"] == 2 and line["world_size_observed"] == 2
     assert line["parity_check"]["all_ok"] and len(line["rank_ms_per_step"]) == 2
     assert line["c4_strong"]["pcie_inclusive_one_process"]["match"] is True
+    # the N>1 line carries c4_strong's own check and one
+    # device per rank (distinct ordinals: cuda:LOCAL_RANK on a real node)
+    assert line["c4_strong"]["parity_check"]["decode"]["match"] is True
+    assert "c4_one_process" in line["parity_check"]["expected"]
+    devs = line["rank_devices"]
+    assert sorted(d["rank"] for d in devs) == [0, 1]
+    assert len({d["stub_ordinal"] for d in devs}) == 2
