@@ -28,6 +28,7 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
+BENCH_PY = os.path.join(ROOT, "bench.py")  # the probe passes run bench.py itself
 if os.path.join(ROOT, "blockframe-rs_amd") not in sys.path:
     sys.path.insert(0, os.path.join(ROOT, "blockframe-rs_amd"))
 
@@ -770,7 +771,7 @@ def _pmc_pass(counter, args, workdir):
     out = os.path.join(workdir, counter)
     cmd = ["timeout", "-s", "KILL", str(PMC_PASS_TIMEOUT_S), "rocprofv3", "--pmc", counter,
            "--output-format", "csv", "-d", out, "-o", "pmc", "--",
-           sys.executable, os.path.abspath(__file__), "--traffic-probe",
+           sys.executable, BENCH_PY, "--traffic-probe",
            "--segments", str(args.segments), "--segment-bytes", str(args.segment_bytes),
            "--pitch", str(args.pitch), "--layout", args.layout]
     env = probe_env(TMPDIR=workdir, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
@@ -912,7 +913,7 @@ def live_kernel_trace(args, profile_dir=None):
     out = os.path.join(workdir, "trace")
     cmd = ["timeout", "-s", "KILL", str(TRACE_PASS_TIMEOUT_S), "rocprofv3", "--kernel-trace",
            "--stats", "--output-format", "csv", "-d", out, "-o", "run", "--",
-           sys.executable, os.path.abspath(__file__), "--trace-probe",
+           sys.executable, BENCH_PY, "--trace-probe",
            "--segments", str(args.segments), "--segment-bytes", str(args.segment_bytes),
            "--pitch", str(args.pitch), "--layout", args.layout, "--steps", str(args.steps),
            "--warmup", str(args.warmup), "--settle-ms", str(args.settle_ms)]

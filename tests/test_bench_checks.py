@@ -98,6 +98,8 @@ def test_live_pmc_passes_parse_and_correct(monkeypatch):
         calls.append(cmd)
         assert cmd[:4] == ["timeout", "-s", "KILL", str(bench.PMC_PASS_TIMEOUT_S)]
         assert "--traffic-probe" in cmd and cmd[cmd.index("--") + 1] == sys.executable
+        # the probe is bench.py itself (round 6: the legs moved to bench_legs.py)
+        assert os.path.basename(cmd[cmd.index("--") + 2]) == "bench.py"
         assert "TORCHELASTIC_RUN_ID" not in env and env["WORLD_SIZE"] == "1"
         counter = cmd[cmd.index("--pmc") + 1]
         out = os.path.join(cmd[cmd.index("-d") + 1], "host", "123")
@@ -331,6 +333,7 @@ def test_live_kernel_trace_child_pass(monkeypatch, tmp_path):
         assert cmd[:4] == ["timeout", "-s", "KILL", str(bench.TRACE_PASS_TIMEOUT_S)]
         i = cmd.index("--")
         assert cmd[i + 1] == sys.executable and "--trace-probe" in cmd  # no shell hop
+        assert os.path.basename(cmd[i + 2]) == "bench.py"
         assert "--kernel-trace" in cmd[:i] and "--stats" in cmd[:i] and "--pmc" not in cmd
         out = os.path.join(cmd[cmd.index("-d") + 1], "host", "1")
         os.makedirs(out)

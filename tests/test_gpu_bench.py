@@ -45,3 +45,35 @@ def test_bench_two_ranks_strong_stripes_assemble_to_oracle_parity(oracle, tmp_pa
             got = np.concatenate([p[3 * b + j] for _, _, p in parts])
             assert np.array_equal(got, want[j]), (b, j)
         seg += k
+
+
+def test_driver_scale_form_at_one_rank_over_rccl():
+    """The driver's SCALE command at N = 1 (`python -m torch.distributed.run
+    --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 ... bench.py --gpus 1`):
+    under torchrun the rank joins an RCCL process group even alone, so this
+    runs the real collectives of an N > 1 line (barriers, the max-over-ranks
+    all-reduce, the rank_devices all-gather) on the GPU, behind the
+    supervisor, with small sizes.  One line, both C2 and C4 checks green."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(ROOT, "bench.py"), "--gpus", "1", "--segments", "8",
+           "--segment-bytes", str(1 << 20), "--steps", "3", "--warmup", "1", "--settle-ms", "20",
+           "--c4-segments", "40", "--cpu-baseline", "off", "--pcie", "off", "--crate", "off",
+           "--c5", "off", "--pmc", "off", "--trace", "off"]
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 1 and line["world_size_observed"] == 1
+    pc = line["parity_check"]
+    assert pc["all_ok"], pc
+    assert line["c4_strong"]["parity_check"]["decode"]["match"] is True
+    assert line["rank_devices"][0]["device"] == 0
