@@ -689,6 +689,19 @@ struct PinnedPool {
     std::lock_guard<std::mutex> g(mu);
     return free_.size() * slot;
   }
+  size_t size() {
+    std::lock_guard<std::mutex> g(mu);
+    return all_.size();
+  }
+  // pins one more buffer into the idle list (a handle's pre-pinning thread)
+  bool grow() {
+    void *p = pinned_alloc(slot);
+    if (!p) return false;
+    std::lock_guard<std::mutex> g(mu);
+    all_.push_back(static_cast<uint8_t *>(p));
+    free_.push_back(static_cast<uint8_t *>(p));
+    return true;
+  }
   uint64_t last_release = 0;  // StagingCache::pool_tick at the last release (pools_mu)
   // unpins idle buffers beyond `keep` (a handle closing: what a long-lived
   // context retains is bounded, not the largest cache it ever served)
@@ -874,6 +887,11 @@ struct bfrs_archive {
   long long last_gi = -1;
   bool stop = false;
   std::vector<std::thread> workers;
+  // Pre-pinning at open: reserves the context's read
+  // arena (tier 3) and pins the pool up to what this handle's cache and
+  // prefetch will hold, beside the first reads instead of inside them.
+  std::atomic<bool> stop_pin{false};
+  BgTask pinner;
 
   std::mutex gpu_mu;  // tier 1/2 reconstructions, one at a time (tier 3: StagingCache::read_mu)
   std::vector<std::unique_ptr<CleanLane>> lanes;  // clean-segment verification
@@ -898,6 +916,7 @@ struct bfrs_archive {
   }
 
   void stop_workers() {
+    stop_pin = true;
     {
       std::lock_guard<std::mutex> l(mu);
       stop = true;
@@ -906,7 +925,12 @@ struct bfrs_archive {
     for (auto &w : workers)
       if (w.joinable()) w.join();
     workers.clear();
+    try {
+      pinner.join();
+    } catch (...) {  // the pre-pinning is best effort
+    }
   }
+  void prepin();
   // bfrs_close of the context (under its handles_mu): joins the prefetch
   // threads and lets go of everything of the context; later reads fail with
   // an error and bfrs_archive_close frees only the handle.
@@ -1179,17 +1203,26 @@ int bfrs_archive::recover(size_t gi, SegPtr *out) {
   return BFRS_OK;
 }
 
-void bfrs_archive::prefetch_loop(size_t worker) {
-  if (worker == 0 && g.mf.tier == 3) {
+void bfrs_archive::prepin() {
+  if (hipSetDevice(ctx->impl.device) != hipSuccess) return;
+  if (g.mf.tier == 3) {
     // the context's read arena (~1.1 GiB HBM + 22 pinned slots at 32 MiB
     // segments), reserved here -- once per context, by its first tier-3
     // handle -- rather than when the first damaged block is found and the
     // reader is about to need it; a failure is left to that reconstruction
     StagingCache &sc = staging(ctx);
     std::lock_guard<std::mutex> lg(sc.read_mu);
-    if (hipSetDevice(ctx->impl.device) == hipSuccess)
-      (void)sc.read_blk.reserve(pool->slot);
+    (void)sc.read_blk.reserve(pool->slot);
   }
+  // then the segment pool, up to the buffers this handle's cache, prefetch
+  // and readers hold at once (a pool another handle filled is left as is);
+  // pinning runs ~22 GB/s (pinned_alloc), ahead of a ~15 GB/s reader
+  const size_t want = std::min(g.nseg, cap + prefetch_workers + 2);
+  while (!stop_pin && pool->size() < want)
+    if (!pool->grow()) return;
+}
+
+void bfrs_archive::prefetch_loop(size_t) {
   std::unique_lock<std::mutex> l(mu);
   for (;;) {
     cv.wait(l, [&] { return stop || !wantq.empty(); });
@@ -1857,6 +1890,13 @@ int bfrs_archive_open(bfrs_ctx *ctx, const char *archive_dir, size_t cache_segme
     } catch (const std::system_error &) {  // no thread: fewer prefetch workers, or none
     }
     a->prefetch = !a->workers.empty();
+    if (a->prefetch) {
+      bfrs_archive *h = a.get();
+      try {
+        h->pinner.start([h] { h->prepin(); });
+      } catch (...) {  // start() runs the task inline if no thread can be made
+      }
+    }
   }
   *out = a.release();
   return BFRS_OK;

@@ -622,12 +622,19 @@ int Context::run_window(const std::vector<BlockIO> &blocks, size_t shard_bytes,
         const uint32_t n_pad = (p.c1 - p.c0 + 1) & ~1u;
         unrolled_sizes = unrolled_sizes && p.subfield && (n_pad == 30 || n_pad == 20 || n_pad == 8);
       }
-      const uint32_t tb = tile_bytes(unrolled_sizes);
-      const uint32_t n_tiles = uint32_t((full_chunks * 64 + tb - 1) / tb);
-      // Workgroup sizing: one tile per workgroup unless the grid is huge.
-      const uint64_t total_tiles = uint64_t(n_tiles) * (last - first);
-      uint32_t tpw = uint32_t(std::max<uint64_t>(1, total_tiles / 65536));
-      if (const char *e = BFRS_AB_KNOB("BFRS_TILES_PER_WG")) tpw = std::max(1, atoi(e));
+      uint32_t tb = 0, n_tiles = 0, tpw = 1;
+      for (;;) {
+        tb = tile_bytes(unrolled_sizes);
+        n_tiles = uint32_t((full_chunks * 64 + tb - 1) / tb);
+        // Workgroup sizing: one tile per workgroup unless the grid is huge.
+        const uint64_t total_tiles = uint64_t(n_tiles) * (last - first);
+        tpw = uint32_t(std::max<uint64_t>(1, total_tiles / 65536));
+        if (const char *e = BFRS_AB_KNOB("BFRS_TILES_PER_WG")) tpw = std::max(1, atoi(e));
+        // the wide tiles exist only for one tile per workgroup: otherwise
+        // the launch falls back to 8 KiB tiles, so size the grid for them
+        if (tpw == 1 || !unrolled_sizes || tb == tile_bytes(false)) break;
+        unrolled_sizes = false;
+      }
       const uint32_t wgs_per_pass = (n_tiles + tpw - 1) / tpw;
 
       KernArgs ka{};

@@ -999,6 +999,17 @@ for v in os.environ["LDS_VARIANTS"].split(","):
         assert all(np.array_equal(outs[3 * b + j], want[j]) for j in range(3)), (v, "batch", k)
         off += k
     n_cases += len(ks)
+# two tiles per workgroup (the measurement build's BFRS_TILES_PER_WG): the
+# LDS-DMA kernels take one tile per workgroup only, so the launch falls back
+# to v76's 8 KiB tiles and its grid must be sized for them
+os.environ["BFRS_TILES_PER_WG"] = "2"
+S = (1 << 20) + 64 * 3
+segs = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(30)]
+want = oracle.encode(segs, 3, eng)
+got = ctx.encode(segs, 3)
+assert all(np.array_equal(got[j], want[j]) for j in range(3)), "tiles_per_wg 2"
+del os.environ["BFRS_TILES_PER_WG"]
+n_cases += 1
 ctx.close()
 print(f"lds variants ok: {n_cases} cases")
 '''
