@@ -1073,6 +1073,17 @@ def run_c5(args, ctx=None):
             cold_ctx.close()
         ok = ok and bfrs.blake3_hex(out, threads=16) == want
         del out
+        # and once more with the archive's files dropped from the page cache
+        # (fsync + POSIX_FADV_DONTNEED, no privileges needed): the read then
+        # includes the storage under the work directory, named beside it
+        evicted = evict_tree(adir)
+        ev_ctx = bfrs.Context(ctx.device)
+        try:
+            ev_s, ev_st, out = sweep(ev_ctx)
+        finally:
+            ev_ctx.close()
+        ok = ok and bfrs.blake3_hex(out, threads=16) == want
+        del out
         res = {
             "metric": "MB/s end-to-end read of a corrupted tier-3 file (BASELINE configs[4])",
             "value": round(n / cold_s / 1e6, 1), "unit": "MB/s",
@@ -1083,6 +1094,8 @@ def run_c5(args, ctx=None):
             "clean_read_MBps": round(n / clean_s / 1e6, 1),
             "corrupted_read_fresh_context_MBps": round(n / cold_s / 1e6, 1),
             "corrupted_read_warm_context_MBps": round(n / dirty_s / 1e6, 1),
+            "corrupted_read_files_evicted_MBps": round(n / ev_s / 1e6, 1),
+            "files_evicted": evicted,
             "handles": "value = the corrupted read through the first handle of a NEW context "
                        "(its staging pinned at open, beside the reads); "
                        "corrupted_read_warm_context_MBps = a second handle on the context of "
@@ -1100,6 +1113,43 @@ def run_c5(args, ctx=None):
         shutil.rmtree(work, ignore_errors=True)
         if own:
             ctx.close()
+
+
+def fs_type(path):
+    """(mount point, file system type) holding `path`, from /proc/mounts."""
+    real = os.path.realpath(path)
+    best = ("/", "unknown")
+    try:
+        for line in open("/proc/mounts"):
+            f = line.split()
+            if len(f) >= 3 and (real == f[1] or real.startswith(f[1].rstrip("/") + "/")):
+                if len(f[1]) >= len(best[0]):
+                    best = (f[1], f[2])
+    except OSError:
+        pass
+    return best
+
+
+def evict_tree(root):
+    """Drop every file under `root` from the page cache: fsync (the commit's
+    pages may still be dirty), then POSIX_FADV_DONTNEED.  Returns what was
+    done and where the files live (tmpfs / overlay in memory cannot evict)."""
+    files = nbytes = 0
+    for d, _, names in os.walk(root):
+        for name in names:
+            p = os.path.join(d, name)
+            fd = os.open(p, os.O_RDONLY)
+            try:
+                os.fsync(fd)
+                os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_DONTNEED)
+                nbytes += os.fstat(fd).st_size
+                files += 1
+            finally:
+                os.close(fd)
+    mnt, fst = fs_type(root)
+    return {"files": files, "bytes": nbytes, "mount": mnt, "fs_type": fst,
+            "in_memory_fs": fst in ("tmpfs", "ramfs"),
+            "how": "fsync + posix_fadvise(POSIX_FADV_DONTNEED) per file"}
 
 
 def c5_repair(ctx, adir, nbytes, n_damaged):
