@@ -38,9 +38,14 @@ def main():
                          "3 restored rows consecutive in one buffer, as the archive arenas); "
                          "suffix c = physically contiguous allocations (hipDeviceMallocContiguous); "
                          "suffix s = data, parity and restored rows in one allocation; suffix r = every row its own allocation")
+    ap.add_argument("--pad-gib", type=float, default=0.0,
+                    help="allocate (and keep) this much HBM before the layouts: does a layout's "
+                         "placement mode follow its allocation order? (round 6)")
     a = ap.parse_args()
     import numpy as np
     import torch
+    pad = (torch.empty(int(a.pad_gib * 2**30), dtype=torch.uint8, device="cuda")
+           if a.pad_gib > 0 else None)
     import bfrs
     from bfrs import synth
     os.environ["BFRS_ALLOW_PROBE"] = "1"
@@ -247,6 +252,8 @@ def main():
     # (placement study: does speed follow the virtual address?)
     out["addresses"] = {x: {"data": hex(L["data"][0].data_ptr()), "par": hex(L["par"][0].data_ptr()),
                             "rest": hex(L["rest"][0].data_ptr())} for x, L in layouts.items()}
+    out["pad_gib"] = a.pad_gib
+    del pad
     print(json.dumps({"decode": a.decode, "alg_bytes": alg, **out}, indent=1))
 
 
