@@ -83,6 +83,24 @@ def test_batch_encode_mixed_blocks_vs_oracle(ctx, oracle, shard_bytes):
             assert np.array_equal(got, want[j]), (b, ks[b], j)
 
 
+@pytest.mark.parametrize("byte", [0x00, 0xAB, 0xFF])
+def test_constant_byte_segments_vs_oracle(ctx, oracle, byte):
+    """SURVEY §8(d)'s constant-byte variant of the synthetic inputs
+    (chunker/tests.rs:19-27 commits files of one repeated byte): RS(30,3) and
+    RS(8,3) of constant segments at 1 MiB + 3 chunks, encode and a 3-erasure
+    decode, against the oracle (a zero-skip or constant-folding shortcut in
+    the kernel would show here)."""
+    n = (1 << 20) + 64 * 3
+    for k in (30, 8):
+        segs = [np.full(n, byte, np.uint8) for _ in range(k)]
+        want = oracle.encode(segs, 3)
+        got = ctx.encode(segs, 3)
+        assert all(np.array_equal(got[j], want[j]) for j in range(3)), (k, byte)
+        er = [0, k // 2, k - 1]
+        out = ctx.decode([None if i in er else segs[i] for i in range(k)], want)
+        assert all(np.array_equal(out[i], segs[i]) for i in er), (k, byte)
+
+
 def test_batch_decode_random_erasures_vs_oracle(ctx, oracle):
     rng = np.random.default_rng(7)
     n = 256 * 1024
