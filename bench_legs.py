@@ -1089,7 +1089,9 @@ def run_c5(args, ctx=None):
             "metric": "MB/s end-to-end read of a corrupted tier-3 file (BASELINE configs[4])",
             "value": round(n / cold_s / 1e6, 1), "unit": "MB/s",
             "workload": "configs[4]: 4 GiB tier-3 archive, 3 bit-flipped segments per block, "
-                        "sequential 128 KiB reads through bfrs_archive_read; files in the page cache",
+                        "sequential 128 KiB reads through bfrs_archive_read; value with the files in "
+                        "the page cache, corrupted_read_files_evicted_MBps with them evicted (the "
+                        "storage included, SURVEY 8(d) C5)",
             "bytes": n, "segment_bytes": args.segment_bytes, "read_bytes": args.c5_read_bytes,
             "blocks": len(m["merkle_tree"]["blocks"]), "damaged_segments": len(damaged),
             "clean_read_MBps": round(n / clean_s / 1e6, 1),
