@@ -741,6 +741,12 @@ struct PinnedPool {
 inline size_t pool_keep(size_t slot) { return std::max<size_t>(8, (size_t(2) << 30) / slot); }
 // idle pinned bytes a context keeps over every pool no open handle uses
 constexpr size_t kIdlePinnedCap = size_t(2) << 30;
+// the measurement build may lower it (BFRS_IDLE_PIN_CAP, bytes) so a test can
+// drive the eviction with small files (tests/test_gpu_archive.py)
+size_t idle_pinned_cap() {
+  if (const char *e = BFRS_AB_KNOB("BFRS_IDLE_PIN_CAP")) return size_t(std::strtoull(e, nullptr, 10));
+  return kIdlePinnedCap;
+}
 
 // A read handle lets go of its pool (closing or detached).  The pool keeps at
 // most pool_keep idle buffers; then, over the pools of the context that no
@@ -773,7 +779,7 @@ void release_pool(bfrs_ctx *ctx, std::shared_ptr<PinnedPool> pool) {
     }
     std::sort(idle.begin(), idle.end(), [](const Idle &a, const Idle &b) { return a.tick < b.tick; });
     for (const Idle &i : idle) {
-      if (total <= kIdlePinnedCap) break;
+      if (total <= idle_pinned_cap()) break;
       auto it = sc.seg_pools.find(i.key);
       drop.push_back(std::move(it->second));
       sc.seg_pools.erase(it);
@@ -2032,8 +2038,28 @@ void bfrs_archive_close(bfrs_archive *a) { delete a; }
 
 namespace bfrs {
 void detach_archives(bfrs_ctx *ctx) {
-  std::lock_guard<std::mutex> l(ctx->impl.handles_mu);
-  for (bfrs_archive *a : ctx->impl.handles) a->detach();
-  ctx->impl.handles.clear();
+  {
+    std::lock_guard<std::mutex> l(ctx->impl.handles_mu);
+    for (bfrs_archive *a : ctx->impl.handles) a->detach();
+    ctx->impl.handles.clear();
+  }
+  // measurement build (BFRS_TRACE): the context's segment pools as bfrs_close
+  // finds them, one stderr line (tests check the idle cap with it)
+  if (BFRS_AB_KNOB("BFRS_TRACE") && ctx->impl.staging) {
+    StagingCache &sc = staging(ctx);
+    std::lock_guard<std::mutex> l(sc.pools_mu);
+    std::ostringstream os;
+    size_t idle = 0;
+    os << "bfrs_pools {\"pools\":" << sc.seg_pools.size() << ",\"slots\":[";
+    bool first = true;
+    for (auto &e : sc.seg_pools) {
+      auto *pp = static_cast<PinnedPool *>(e.second.get());
+      idle += pp->idle_bytes();
+      os << (first ? "" : ",") << pp->slot;
+      first = false;
+    }
+    os << "],\"idle_bytes\":" << idle << ",\"idle_cap\":" << idle_pinned_cap() << "}\n";
+    std::fputs(os.str().c_str(), stderr);
+  }
 }
 }  // namespace bfrs

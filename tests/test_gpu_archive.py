@@ -571,6 +571,62 @@ def test_prefetch_worker_counts_with_concurrent_readers(tmp_path, workers):
     assert r.returncode == 0 and "workers ok" in r.stdout, (r.stdout[-1000:], r.stderr[-2000:])
 
 
+_POOL_CAP_SCRIPT = r"""
+import json, os, sys
+import numpy as np
+root, work = sys.argv[1], sys.argv[2]
+sys.path.insert(0, os.path.join(root, "blockframe-rs_amd"))
+import bfrs
+assert bfrs.LIB_PATH.endswith("libbfrs_ab.so"), bfrs.LIB_PATH
+sizes = [4_500_000 + 500_000 * i for i in range(6)]  # six tier-1 files: six pool sizes
+rng = np.random.default_rng(3)
+ctx = bfrs.Context(0)
+dirs = []
+for i, n in enumerate(sizes):
+    d = rng.integers(0, 256, n, dtype=np.uint8)
+    p = os.path.join(work, f"f{i}.bin")
+    d.tofile(p)
+    dirs.append((bfrs.commit(ctx, p, os.path.join(work, f"a{i}")), d))
+for cap in ("", str(8 << 20)):  # the default 2 GiB, then 8 MiB
+    if cap:
+        os.environ["BFRS_IDLE_PIN_CAP"] = cap
+    c = bfrs.Context(0)
+    for adir, d in dirs:  # one handle per file, opened, read whole, closed
+        with bfrs.Archive(c, adir, cache_segments=4) as a:
+            assert a.read(0, d.size) == d.tobytes()
+    c.close()  # BFRS_TRACE: one bfrs_pools line on stderr
+ctx.close()
+print("pool cap ok")
+"""
+
+
+def test_idle_segment_pools_are_capped_per_context(tmp_path):
+    """a context no longer keeps one pinned pool per distinct
+    segment size until bfrs_close.  Six tier-1 archives of six sizes, each read
+    through its own handle on one context: with the default cap all six idle
+    pools stay (a reopened handle reuses its buffer); with the measurement
+    build's cap lowered to 8 MiB (BFRS_IDLE_PIN_CAP) the least recently
+    released pools are unpinned as handles close, so at bfrs_close at most the
+    last one is left and the idle bytes fit the cap."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if not os.path.exists(os.path.join(root, "blockframe-rs_amd", "libbfrs_ab.so")):
+        pytest.skip("libbfrs_ab.so not built (make -C blockframe-rs_amd/csrc ab)")
+    env = dict(os.environ, BFRS_LIB="libbfrs_ab.so", BFRS_TRACE="1")
+    env.pop("BFRS_IDLE_PIN_CAP", None)
+    r = subprocess.run([sys.executable, "-c", _POOL_CAP_SCRIPT, root, str(tmp_path)],
+                       capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0 and "pool cap ok" in r.stdout, (r.stdout[-1000:], r.stderr[-2000:])
+    lines = [json.loads(l.split(" ", 1)[1]) for l in r.stderr.splitlines()
+             if l.startswith("bfrs_pools ")]
+    assert len(lines) == 3, r.stderr[-2000:]  # the two read contexts, then the commit context
+    default, capped = lines[0], lines[1]
+    assert default["pools"] == 6 and default["idle_cap"] == 2 << 30
+    assert capped["idle_cap"] == 8 << 20
+    assert capped["pools"] <= 1 and capped["idle_bytes"] <= 8 << 20, capped
+
+
 def test_handles_share_the_segment_pool(ctx, bfrs, tmp_path):
     # the context pins one pool of segment buffers per segment size and lends
     # it to every handle (archive.cpp segment_pool): two handles of the same
