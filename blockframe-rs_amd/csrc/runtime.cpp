@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <mutex>
 #include <thread>
+#include <unordered_set>
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
@@ -112,6 +113,11 @@ bool pin_by_register() {
   const char *e = BFRS_AB_KNOB("BFRS_PIN_MODE");
   return !(e && std::strcmp(e, "malloc") == 0);
 }
+// The registered mappings: a large buffer may still be hipHostMalloc'd (the
+// registration failed, or the A/B malloc mode), so pinned_free goes by what
+// pinned_alloc did, not by the size.
+std::mutex g_reg_mu;
+std::unordered_set<void *> g_registered;
 }  // namespace
 
 // below this, hipHostMalloc (a huge-page mapping would round a small buffer
@@ -133,7 +139,11 @@ void *pinned_alloc(size_t bytes) {
       void *p = reinterpret_cast<void *>(a);
       (void)madvise(p, len, MADV_HUGEPAGE);
       if (madvise(p, len, MADV_POPULATE_WRITE) != 0) std::memset(p, 0, len);  // first touch
-      if (hipHostRegister(p, len, hipHostRegisterPortable) == hipSuccess) return p;
+      if (hipHostRegister(p, len, hipHostRegisterPortable) == hipSuccess) {
+        std::lock_guard<std::mutex> g(g_reg_mu);
+        g_registered.insert(p);
+        return p;
+      }
       (void)hipGetLastError();
       munmap(p, len);
     }
@@ -149,12 +159,15 @@ void *pinned_alloc(size_t bytes) {
 void pinned_free(void *p, size_t bytes) {
   if (!p) return;
   // a registered mapping, or else hipHostMalloc'd (small, or the fallback)
-  if (bytes >= kRegisterMin) {
-    if (hipHostUnregister(p) == hipSuccess) {
-      munmap(p, round_up(bytes, kHugePage));
-      return;
-    }
-    (void)hipGetLastError();
+  bool registered = false;
+  {
+    std::lock_guard<std::mutex> g(g_reg_mu);
+    registered = g_registered.erase(p) != 0;
+  }
+  if (registered) {
+    if (hipHostUnregister(p) != hipSuccess) (void)hipGetLastError();
+    munmap(p, round_up(bytes, kHugePage));
+    return;
   }
   (void)hipHostFree(p);
 }

@@ -1053,6 +1053,50 @@ def test_lds_dma_variants_match_the_oracle():
     assert r.returncode == 0 and "lds variants ok" in r.stdout, (r.stdout[-1000:], r.stderr[-2000:])
 
 
+_PIN_MALLOC_SCRIPT = r'''
+import os, sys
+import numpy as np
+root = os.environ["BFRS_TEST_ROOT"]
+sys.path.insert(0, os.path.join(root, "blockframe-rs_amd"))
+sys.path.insert(0, os.path.join(root, "oracle"))
+import bfrs, oracle
+assert bfrs.LIB_PATH.endswith("libbfrs_ab.so"), bfrs.LIB_PATH
+rng = np.random.default_rng(0x91A)
+eng = oracle.ENGINE_AVX2 if oracle.lib().oracle_have_avx2() else oracle.ENGINE_SCALAR
+for rnd in range(3):   # slots of >= 4 MiB freed and taken again, then the context
+    ctx = bfrs.Context(0)
+    for S in ((1 << 20) + 64 * 3 + 5, (6 << 20) + 38):
+        segs = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(30)]
+        want = oracle.encode(segs, 3, eng)
+        got = ctx.encode(segs, 3)
+        assert all(np.array_equal(got[j], want[j]) for j in range(3)), (rnd, S, "encode")
+        orig = [None if i in (2, 17, 29) else segs[i] for i in range(30)]
+        out = ctx.decode(orig, want)
+        assert all(np.array_equal(out[i], segs[i]) for i in (2, 17, 29)), (rnd, S, "decode")
+    ctx.close()
+print("pin malloc ok")
+'''
+
+
+def test_large_pinned_buffers_from_hip_host_malloc():
+    """Round 6 (review of pinned_free): a pinned buffer of >= 4 MiB is
+    normally a registered huge-page mapping, but falls back to hipHostMalloc
+    when the registration fails.  pinned_free must free such a buffer with
+    hipHostFree, not unregister and munmap it.  The measurement build's
+    hipHostMalloc mode (BFRS_PIN_MODE=malloc) forces the fallback for every
+    codec slot.  Three contexts in turn, each with 1 MiB and 6 MiB RS(30,3)
+    encodes and decodes checked against the oracle."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if not os.path.exists(os.path.join(root, "blockframe-rs_amd", "libbfrs_ab.so")):
+        pytest.skip("libbfrs_ab.so not built (make -C blockframe-rs_amd/csrc ab)")
+    env = dict(os.environ, BFRS_LIB="libbfrs_ab.so", BFRS_TEST_ROOT=root, BFRS_PIN_MODE="malloc")
+    r = subprocess.run([sys.executable, "-c", _PIN_MALLOC_SCRIPT], capture_output=True,
+                       text=True, timeout=180, env=env)
+    assert r.returncode == 0 and "pin malloc ok" in r.stdout, (r.stdout[-1000:], r.stderr[-2000:])
+
+
 @pytest.mark.parametrize("n", [64 * 150 + 38, (16 << 20) + 64 * 5 + 38])
 def test_host_batch_pinned_strided_rows_vs_oracle(ctx, oracle, n):
     """Pinned shard rows at a constant pitch (one pinned tensor, as the bench
