@@ -12,7 +12,7 @@
 #include <algorithm>
 #include <mutex>
 #include <thread>
-#include <unordered_set>
+#include <unordered_map>
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
@@ -113,11 +113,19 @@ bool pin_by_register() {
   const char *e = BFRS_AB_KNOB("BFRS_PIN_MODE");
   return !(e && std::strcmp(e, "malloc") == 0);
 }
-// The registered mappings: a large buffer may still be hipHostMalloc'd (the
-// registration failed, or the A/B malloc mode), so pinned_free goes by what
-// pinned_alloc did, not by the size.
-std::mutex g_reg_mu;
-std::unordered_set<void *> g_registered;
+// The registered mappings and their mapped lengths: a large buffer may still
+// be hipHostMalloc'd (the registration failed, or the A/B malloc mode), so
+// pinned_free goes by what pinned_alloc did, not by the size it is handed.
+// Never destroyed: a caller's own static destructor may free staging after
+// this library's statics are gone (__cxa_finalize order across DSOs).
+struct Registry {
+  std::mutex mu;
+  std::unordered_map<void *, size_t> len;
+};
+Registry &registry() {
+  static Registry *r = new Registry;
+  return *r;
+}
 }  // namespace
 
 // below this, hipHostMalloc (a huge-page mapping would round a small buffer
@@ -140,8 +148,9 @@ void *pinned_alloc(size_t bytes) {
       (void)madvise(p, len, MADV_HUGEPAGE);
       if (madvise(p, len, MADV_POPULATE_WRITE) != 0) std::memset(p, 0, len);  // first touch
       if (hipHostRegister(p, len, hipHostRegisterPortable) == hipSuccess) {
-        std::lock_guard<std::mutex> g(g_reg_mu);
-        g_registered.insert(p);
+        Registry &reg = registry();
+        std::lock_guard<std::mutex> g(reg.mu);
+        reg.len[p] = len;
         return p;
       }
       (void)hipGetLastError();
@@ -156,17 +165,22 @@ void *pinned_alloc(size_t bytes) {
   return p;
 }
 
-void pinned_free(void *p, size_t bytes) {
+void pinned_free(void *p, size_t) {
   if (!p) return;
   // a registered mapping, or else hipHostMalloc'd (small, or the fallback)
-  bool registered = false;
+  size_t mapped = 0;
   {
-    std::lock_guard<std::mutex> g(g_reg_mu);
-    registered = g_registered.erase(p) != 0;
+    Registry &reg = registry();
+    std::lock_guard<std::mutex> g(reg.mu);
+    auto it = reg.len.find(p);
+    if (it != reg.len.end()) {
+      mapped = it->second;
+      reg.len.erase(it);
+    }
   }
-  if (registered) {
+  if (mapped) {
     if (hipHostUnregister(p) != hipSuccess) (void)hipGetLastError();
-    munmap(p, round_up(bytes, kHugePage));
+    munmap(p, mapped);
     return;
   }
   (void)hipHostFree(p);

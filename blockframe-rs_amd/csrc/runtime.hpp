@@ -53,7 +53,7 @@ struct DeviceScope {
 // this way, whose register step alone runs ~390 GB/s (tools/pin_probe.py,
 // profiles/r06/pin/), so a first commit or read on a context waits a quarter
 // as long for its staging.  Falls back to hipHostMalloc when
-// any step fails.  pinned_free takes the size pinned_alloc was given.
+// any step fails.  pinned_free frees by what pinned_alloc did (it records each mapping's length).
 void *pinned_alloc(size_t bytes);
 void pinned_free(void *p, size_t bytes);
 

@@ -1065,7 +1065,7 @@ rng = np.random.default_rng(0x91A)
 eng = oracle.ENGINE_AVX2 if oracle.lib().oracle_have_avx2() else oracle.ENGINE_SCALAR
 for rnd in range(3):   # slots of >= 4 MiB freed and taken again, then the context
     ctx = bfrs.Context(0)
-    for S in ((1 << 20) + 64 * 3 + 5, (6 << 20) + 38):
+    for S in ((1 << 20) + 64 * 3 + 6, (6 << 20) + 38):
         segs = [rng.integers(0, 256, S, dtype=np.uint8) for _ in range(30)]
         want = oracle.encode(segs, 3, eng)
         got = ctx.encode(segs, 3)
