@@ -262,6 +262,65 @@ __global__ __launch_bounds__(64 * WAVES) void probe_lds(Args a) {
   }
 }
 
+// Round 6 (tiled layout question): the same traffic with each block's shards
+// stored tile-major -- for tile t of block b, the K input pieces of WG bytes
+// (and, INTER=1, the O output pieces) sit next to each other -- so the chip
+// reads one near-sequential stream instead of K streams 32 MiB apart.  No read
+// rotation (the pieces are read in address order).
+struct TArgs {
+  uint64_t data, out;
+  uint32_t tiles_per_block, total_tiles;
+};
+
+template <int K, int O, int NL, int NTL, int NTS, int D, int INTER, int XG, int WAVES = 4>
+__global__ __launch_bounds__(64 * WAVES) void probe_tiled(TArgs a) {
+  const uint32_t wg = XG ? xcd_remap16(blockIdx.x, gridDim.x) : blockIdx.x;
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  constexpr uint32_t WGB = WAVES * NL * 1024;
+  constexpr uint32_t P = INTER ? K + O : K;  // pieces per tile in the data region
+  const uint64_t region = a.data + uint64_t(wg) * P * WGB;
+  const uint32_t off0 = wave * NL * 1024 + lane * 16;
+  u32x4 buf[K][NL];
+  u32x4 acc = {0, 0, 0, 0};
+#pragma unroll
+  for (int i = 0; i < K + D + 1; ++i) {
+    if (i < K) {
+      const uint64_t base = region + uint64_t(i) * WGB;
+#pragma unroll
+      for (int j = 0; j < NL; ++j) gload<NTL>(buf[i][j], base, off0 + uint32_t(j) * 1024);
+    }
+    const int c = i - D;
+    if (c >= 0 && c < K) {
+      const int after = (K - 1 - c) < D ? (K - 1 - c) : D;
+      switch (after * NL) {
+        case 0: wait_buf<0, NL>(buf[c]); break;
+        case 2: wait_buf<2, NL>(buf[c]); break;
+        case 4: wait_buf<4, NL>(buf[c]); break;
+        case 6: wait_buf<6, NL>(buf[c]); break;
+        case 8: wait_buf<8, NL>(buf[c]); break;
+        case 12: wait_buf<12, NL>(buf[c]); break;
+        case 16: wait_buf<16, NL>(buf[c]); break;
+        default: wait_buf<0, NL>(buf[c]); break;
+      }
+#pragma unroll
+      for (int j = 0; j < NL; ++j) axor(acc, buf[c][j]);
+    }
+  }
+  if constexpr (O > 0) {
+#pragma unroll
+    for (int o = 0; o < O; ++o) {
+      const uint64_t base =
+          INTER ? region + uint64_t(K + o) * WGB : a.out + (uint64_t(wg) * O + o) * WGB;
+#pragma unroll
+      for (int j = 0; j < NL; ++j)
+        gstore<NTS>(base, off0 + uint32_t(j) * 1024, acc + u32x4{uint32_t(o + j), 0, 0, 0});
+    }
+  } else {
+    if (acc.x == 0x9e3779b9u && acc.y == 0x7f4a7c15u)
+      *(u32x4 *)(uintptr_t)(a.out + lane * 16) = acc;
+  }
+}
+
 struct Bufs {
   uint8_t *data = nullptr, *outp = nullptr;
   uint64_t pitch = 0;
@@ -346,6 +405,25 @@ void run_lds(const char *tag, size_t extra_lds = 0) {
            NTS, D, WAVES, extra_lds);
   timeit(name, [&] { hipLaunchKernelGGL((probe_lds<K, O, NL, NTL, NTS, D, WAVES>), dim3(a.total_tiles),
                                          dim3(64 * WAVES), lds, 0, a); }, bytes);
+}
+
+// tiled probe over a data region of B x tiles x (K [+O]) pieces
+template <int K, int O, int NL, int NTL, int NTS, int D, int INTER, int XG, int WAVES = 4>
+void run_tiled(const char *tag, uint8_t *data, uint8_t *out, int occ) {
+  constexpr uint32_t B = kShards / K;
+  const uint32_t wg_bytes = WAVES * NL * 1024;
+  TArgs a;
+  a.data = uint64_t(data);
+  a.out = uint64_t(out);
+  a.tiles_per_block = uint32_t(kS / wg_bytes);
+  a.total_tiles = a.tiles_per_block * B;
+  const double bytes = double(kS) * B * (K + O);
+  const size_t lds = occ > 0 ? (size_t(160) << 10) / occ / 1024 * 1024 : 0;
+  char name[160];
+  snprintf(name, sizeof name, "%s_tiled_k%d_o%d_nl%d_ntl%d_nts%d_d%d_inter%d_xg%d_occ%d_w%d", tag, K, O,
+           NL, NTL, NTS, D, INTER, XG, occ, WAVES);
+  timeit(name, [&] { hipLaunchKernelGGL((probe_tiled<K, O, NL, NTL, NTS, D, INTER, XG, WAVES>),
+                                         dim3(a.total_tiles), dim3(64 * WAVES), lds, 0, a); }, bytes);
 }
 
 int main(int argc, char **argv) {
@@ -461,6 +539,32 @@ int main(int argc, char **argv) {
         run_lds<30, 3, 4, 1, 1, 1, 8>(t, 15360);   // v107: 8 waves, 2 slots: 2 WGs/CU
         run_lds<30, 3, 4, 1, 1, 1, 4>(t, 15360);   // v108: 4 waves, 2 slots: 3 WGs/CU
         run_lds<30, 3, 4, 1, 1, 2, 4>(t, 15360);   // v109: 4 waves, 3 slots: 2 WGs/CU
+      }
+      return 0;
+    }
+    if (!strcmp(only, "tplace") && rep == 0) {
+      // round 6: row layout (the product's) vs tile-major layout on the same
+      // six separately allocated copies; each copy holds the rows at pitch
+      // S + 12 KiB (4.03 GB) or the interleaved tiles (4.43 GB)
+      const int copies = 6;
+      const size_t cbytes = size_t(kShards / 30) * 33 * kS;
+      std::vector<uint8_t *> keep;
+      for (int c = 0; c < copies; ++c) {
+        uint8_t *d = nullptr;
+        CHECK(hipMalloc(&d, cbytes));
+        CHECK(hipMemset(d, 0x5a, cbytes));
+        keep.push_back(d);
+      }
+      for (int c = 0; c < copies; ++c) {
+        g.data = keep[c];
+        char t[32];
+        snprintf(t, sizeof t, "c%d_rs", c);
+        run<30, 3, 2, 0, 1, 1, 2, 1, 0, 4>(t, 5);                  // product rows, 8 KiB/WG
+        run_tiled<30, 3, 2, 1, 1, 2, 1, 1>(t, keep[c], g.outp, 5);  // tiles, parity interleaved
+        run_tiled<30, 3, 2, 1, 1, 2, 1, 0>(t, keep[c], g.outp, 5);  //   no XCD grouping
+        run_tiled<30, 3, 2, 1, 1, 2, 0, 1>(t, keep[c], g.outp, 5);  // tiles, parity separate
+        run_tiled<30, 3, 4, 1, 1, 2, 1, 1>(t, keep[c], g.outp, 4);  // 16 KiB tiles
+        run_tiled<30, 0, 2, 1, 1, 2, 0, 1>(t, keep[c], g.outp, 5);  // reads only
       }
       return 0;
     }
