@@ -53,8 +53,7 @@ EXPORTS = (
     "bfrs_encoder_encode", "bfrs_encoder_recovery", "bfrs_encoder_free", "bfrs_decoder_new",
     "bfrs_decoder_add_original_shard", "bfrs_decoder_add_recovery_shard", "bfrs_decoder_decode",
     "bfrs_decoder_restored_original", "bfrs_decoder_free", "bfrs_encode", "bfrs_decode",
-    "bfrs_encode_batch_dev", "bfrs_decode_batch_dev", "bfrs_encode_batch_dev_tiled",
-    "bfrs_decode_batch_dev_tiled", "bfrs_encode_host_batch",
+    "bfrs_encode_batch_dev", "bfrs_decode_batch_dev", "bfrs_encode_host_batch",
     "bfrs_decode_host_batch", "bfrs_encode_host_batch_multi", "bfrs_decode_host_batch_multi",
     "bfrs_generate_parity",
     "bfrs_generate_parity_segmented", "bfrs_recover_segment_rs13", "bfrs_recover_segment_rs30_3",
@@ -148,7 +147,6 @@ class ArchiveStats(ctypes.Structure):
 _vp = ctypes.c_void_p
 _sz = ctypes.c_size_t
 _pp = ctypes.POINTER(ctypes.c_void_p)
-_szp = ctypes.POINTER(ctypes.c_size_t)
 
 
 def _torch_runtime_first() -> None:
@@ -206,10 +204,6 @@ def lib() -> ctypes.CDLL:
                                        _pp, _vp], ctypes.c_int),
             "bfrs_decode_batch_dev": ([_vp, _sz, ctypes.POINTER(ctypes.c_uint32), _sz, _sz, _pp,
                                        _pp, _pp, _vp], ctypes.c_int),
-            "bfrs_encode_batch_dev_tiled": ([_vp, _sz, ctypes.POINTER(ctypes.c_uint32), _sz, _sz,
-                                             _pp, _szp, _pp, _szp, _vp], ctypes.c_int),
-            "bfrs_decode_batch_dev_tiled": ([_vp, _sz, ctypes.POINTER(ctypes.c_uint32), _sz, _sz,
-                                             _pp, _szp, _pp, _szp, _pp, _szp, _vp], ctypes.c_int),
             "bfrs_encode_host_batch": ([_vp, _sz, ctypes.POINTER(ctypes.c_uint32), _sz, _sz, _pp,
                                         _pp], ctypes.c_int),
             "bfrs_decode_host_batch": ([_vp, _sz, ctypes.POINTER(ctypes.c_uint32), _sz, _sz, _pp,
@@ -360,52 +354,6 @@ def empty_shards(n: int, shard_bytes: int, device="cuda"):
     return buf.as_strided((n, shard_bytes), (pitch, 1))
 
 
-TILE_BYTES = 8192  # BFRS_TILE_BYTES
-
-
-def empty_tiled_shards(n: int, shard_bytes: int, device="cuda"):
-    """n shards of shard_bytes as ONE tile-major set (bfrs_*_batch_dev_tiled):
-    tile t of shard i at byte (t * n + i) * TILE_BYTES.  Returns the n shard
-    views, each a (shard_bytes / TILE_BYTES, TILE_BYTES) uint8 tensor with row
-    stride n * TILE_BYTES, which the batch calls below pass as tiled shards."""
-    import torch
-    if shard_bytes % TILE_BYTES:
-        raise ValueError(f"tile-major shards need shard_bytes % {TILE_BYTES} == 0")
-    tiles = shard_bytes // TILE_BYTES
-    buf = torch.empty(max(1, tiles * n * TILE_BYTES), dtype=torch.uint8, device=device)
-    v = buf[:tiles * n * TILE_BYTES].view(tiles, n, TILE_BYTES)
-    return [v[:, i, :] for i in range(n)]
-
-
-def _shard_ref(t):
-    """(device address, tile stride in bytes; 0 = contiguous row) of a shard
-    argument: a 1-D contiguous tensor, an int address, an (address, stride)
-    pair, or a (tiles, TILE_BYTES) tensor view with unit column stride."""
-    if t is None:
-        return None, 0
-    if isinstance(t, int):
-        return t, 0
-    if isinstance(t, tuple):
-        return int(t[0]), int(t[1])
-    if t.dim() == 2:
-        if t.shape[1] != TILE_BYTES or t.stride(1) != 1 or t.element_size() != 1:
-            raise ValueError("a 2-D shard must be a (tiles, TILE_BYTES) uint8 view with unit column stride")
-        return t.data_ptr(), (t.stride(0) if t.shape[0] > 1 else TILE_BYTES)
-    if t.dim() == 1 and not t.is_contiguous():
-        raise ValueError("a 1-D shard must be contiguous")
-    return t.data_ptr(), 0
-
-
-def _shard_args(ts):
-    """Pointer array, keep-alive, and the stride array (None when every shard is a row)."""
-    refs = [_shard_ref(t) for t in ts]
-    p, k = _ptr_array([a for a, _ in refs])
-    if not any(st for _, st in refs):
-        return p, k, None
-    strides = (_sz * max(1, len(refs)))(*[st for _, st in refs])
-    return p, (k, strides), strides
-
-
 class Context:
     """A bfrs_ctx on one HIP device (no CPU fallback)."""
 
@@ -442,55 +390,47 @@ class Context:
 
     def encode_batch_dev(self, original_counts, recovery_count, shard_bytes, d_originals,
                          d_recovery, stream=None) -> None:
-        """bfrs_encode_batch_dev; shards given as 2-D tile views (empty_tiled_shards)
-        or (address, stride) pairs go through bfrs_encode_batch_dev_tiled."""
-        self.prepare_encode(original_counts, recovery_count, shard_bytes, d_originals,
-                            d_recovery)(_stream_handle(stream, list(d_originals) + list(d_recovery)))
+        ks = (ctypes.c_uint32 * len(original_counts))(*original_counts)
+        po, ko = _ptr_array([self._addr(t) for t in d_originals])
+        pr, kr = _ptr_array([self._addr(t) for t in d_recovery])
+        _check(lib().bfrs_encode_batch_dev(self.handle, len(original_counts), ks, recovery_count,
+                                           shard_bytes, po, pr,
+                                           _stream_handle(stream, list(d_originals) + list(d_recovery))))
 
     def decode_batch_dev(self, original_counts, recovery_count, shard_bytes, d_originals,
                          d_recovery, d_restored, stream=None) -> None:
-        self.prepare_decode(original_counts, recovery_count, shard_bytes, d_originals, d_recovery,
-                            d_restored)(_stream_handle(stream, list(d_originals) + list(d_recovery)
-                                                       + list(d_restored)))
+        ks = (ctypes.c_uint32 * len(original_counts))(*original_counts)
+        po, ko = _ptr_array([self._addr(t) for t in d_originals])
+        pr, kr = _ptr_array([self._addr(t) for t in d_recovery])
+        pd, kd = _ptr_array([self._addr(t) for t in d_restored])
+        _check(lib().bfrs_decode_batch_dev(self.handle, len(original_counts), ks, recovery_count,
+                                           shard_bytes, po, pr, pd,
+                                           _stream_handle(stream, list(d_originals) + list(d_recovery)
+                                                          + list(d_restored))))
 
     def prepare_encode(self, original_counts, recovery_count, shard_bytes, d_originals,
                        d_recovery):
         """Pre-built argument arrays for repeated bfrs_encode_batch_dev calls on
         the same buffers (bench loops); returns f(stream_handle)."""
         ks = (ctypes.c_uint32 * len(original_counts))(*original_counts)
-        po, ko, so = _shard_args(d_originals)
-        pr, kr, sr = _shard_args(d_recovery)
-        h, n = self.handle, len(original_counts)
-        if so is None and sr is None:
-            fn = lib().bfrs_encode_batch_dev
+        po, ko = _ptr_array([self._addr(t) for t in d_originals])
+        pr, kr = _ptr_array([self._addr(t) for t in d_recovery])
+        fn, h, n = lib().bfrs_encode_batch_dev, self.handle, len(original_counts)
 
-            def call(stream_handle=None, _keep=(ks, ko, kr)):
-                _check(fn(h, n, ks, recovery_count, shard_bytes, po, pr, stream_handle))
-        else:
-            fn = lib().bfrs_encode_batch_dev_tiled
-
-            def call(stream_handle=None, _keep=(ks, ko, kr)):
-                _check(fn(h, n, ks, recovery_count, shard_bytes, po, so, pr, sr, stream_handle))
+        def call(stream_handle=None, _keep=(ks, ko, kr)):
+            _check(fn(h, n, ks, recovery_count, shard_bytes, po, pr, stream_handle))
         return call
 
     def prepare_decode(self, original_counts, recovery_count, shard_bytes, d_originals,
                        d_recovery, d_restored):
         ks = (ctypes.c_uint32 * len(original_counts))(*original_counts)
-        po, ko, so = _shard_args(d_originals)
-        pr, kr, sr = _shard_args(d_recovery)
-        pd, kd, sd = _shard_args(d_restored)
-        h, n = self.handle, len(original_counts)
-        if so is None and sr is None and sd is None:
-            fn = lib().bfrs_decode_batch_dev
+        po, ko = _ptr_array([self._addr(t) for t in d_originals])
+        pr, kr = _ptr_array([self._addr(t) for t in d_recovery])
+        pd, kd = _ptr_array([self._addr(t) for t in d_restored])
+        fn, h, n = lib().bfrs_decode_batch_dev, self.handle, len(original_counts)
 
-            def call(stream_handle=None, _keep=(ks, ko, kr, kd)):
-                _check(fn(h, n, ks, recovery_count, shard_bytes, po, pr, pd, stream_handle))
-        else:
-            fn = lib().bfrs_decode_batch_dev_tiled
-
-            def call(stream_handle=None, _keep=(ks, ko, kr, kd)):
-                _check(fn(h, n, ks, recovery_count, shard_bytes, po, so, pr, sr, pd, sd,
-                          stream_handle))
+        def call(stream_handle=None, _keep=(ks, ko, kr, kd)):
+            _check(fn(h, n, ks, recovery_count, shard_bytes, po, pr, pd, stream_handle))
         return call
 
     def blake3_batch_dev(self, d_msgs, lens=None, stream=None, with_cvs=False,

@@ -54,12 +54,6 @@ struct alignas(16) PassDesc {
 constexpr uint32_t kMaxLaunchPasses = 16;
 constexpr uint32_t kMaxLaunchPtrs = 376;
 
-// A launch pointer (KernArgs::ptrs) is a device address in its low 48 bits;
-// the top 16 carry E = (tile stride / 8 KiB) - 1 for a shard of a tile-major
-// set (bfrs_*_batch_dev_tiled), 0 for a contiguous row.
-constexpr uint32_t kLaunchStrideShift = 48;
-constexpr uint64_t kLaunchAddrMask = (uint64_t(1) << kLaunchStrideShift) - 1;
-
 struct alignas(16) KernArgs {
   uint32_t n_passes;
   uint32_t tiles_per_wg;
@@ -78,10 +72,6 @@ uint32_t tile_bytes(bool unrolled_sizes);
 // the A/B variants live in libbfrs_ab.so, rs_kernels.hip).
 int kernel_variant();
 bool ab_build();
-// The selected variant reads tile-major shards (launch pointers with a stride
-// tag): the product kernels 76 / 75 / 73 and the A/B variants built on the
-// same contiguous-line loads; not the half-chunk or LDS-DMA A/B kernels.
-bool kernel_takes_tiles();
 
 // subfield: every pass of the launch has GF(2^8)-subfield coefficients
 // (PlanPass::subfield), so the subfield kernel form may run; unrolled_sizes as

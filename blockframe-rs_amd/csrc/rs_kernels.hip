@@ -49,17 +49,6 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
 
-// Tile-major shard sets (bfrs_*_batch_dev_tiled): a launch
-// pointer carries in its top 16 bits E = (tile stride / 8 KiB) - 1, 0 for a
-// contiguous row.  Tile t of such a shard sits t * E * 8 KiB further than it
-// would in a row, so the kernels keep their row offsets (a VGPR) and move the
-// wave-uniform base: two SALU multiplies and an add, no branch (a select on
-// the tag made the compiler split the unrolled ring into blocks and spill).
-__device__ __forceinline__ uint64_t shard_base(uint64_t p, uint32_t tile) {
-  const uint32_t extra = uint32_t(p >> kLaunchStrideShift);
-  return (p & kLaunchAddrMask) + uint64_t(extra) * (tile * (kTileHalfChunks * 32));
-}
-
 // LDS read at an absolute LDS byte address (the dynamic LDS table starts at 0:
 // the kernel declares no static LDS).
 __device__ __forceinline__ uint2 lds_entry(const char *, uint32_t byte_addr) {
@@ -452,8 +441,7 @@ __device__ __forceinline__ bool ring_acc_ct(const KernArgs &args, const PassDesc
         // branch-free (a branch here made the compiler spill in-flight ring
         // registers; tools/inflight_check.py): select the offsets only
         const bool past = TAIL && x >= n_in;
-        gload_ct<LPOL>(A, B, shard_base(in[idx(x)], tile), past ? ln.fb : offA,
-                        past ? ln.fb : offB);
+        gload_ct<LPOL>(A, B, in[idx(x)], past ? ln.fb : offA, past ? ln.fb : offB);
       },
       [&](const u32x4 &Av, const u32x4 &Bv, uint32_t x) {
         const uint32_t r = SLOTS ? x : idx(x);
@@ -497,7 +485,7 @@ __device__ __forceinline__ void ring_tile_ct(const KernArgs &args, const PassDes
     u32x4 ol = {acc_lo[t], acc_lo[4 + t], acc_lo[8 + t], acc_lo[12 + t]};
     u32x4 oh = {acc_hi[t], acc_hi[4 + t], acc_hi[8 + t], acc_hi[12 + t]};
     halves_swap(ol, oh);  // back to the contiguous layout: ol -> run A, oh -> run B
-    const uint64_t dst = shard_base(outp[t], tile);
+    const uint64_t dst = outp[t];
     if (accumulate) {
       if (ln.okA) {
         const uint4 p = load16(dst + ln.offA);
@@ -699,15 +687,14 @@ __device__ __forceinline__ void mac_slot(const u32x4 &L, const u32x4 &H, uint32_
 }
 
 template <int N, int LPOL, bool B64, uint32_t C>
-__device__ __forceinline__ void unrolled_step(const uint64_t *in, uint32_t rot, uint32_t tile,
-                                              const CtLane &ln,
+__device__ __forceinline__ void unrolled_step(const uint64_t *in, uint32_t rot, const CtLane &ln,
                                               uint32_t mask, u32x4 (&A)[N], u32x4 (&B)[N],
                                               uint32_t (&acc_lo)[16], uint32_t (&acc_hi)[16]) {
   constexpr int D = 3;  // inputs in flight ahead of the one consumed
   if constexpr (C < uint32_t(N)) {  // issue input C
     uint32_t src = rot + C;
     src = src >= uint32_t(N) ? src - N : src;
-    gload_ct<LPOL>(A[C], B[C], shard_base(in[src], tile), ln.offA, ln.offB);
+    gload_ct<LPOL>(A[C], B[C], in[src], ln.offA, ln.offB);
   }
   if constexpr (C >= uint32_t(D) && C - D < uint32_t(N)) {  // consume input C - D
     constexpr uint32_t c = C - D;
@@ -720,12 +707,11 @@ __device__ __forceinline__ void unrolled_step(const uint64_t *in, uint32_t rot, 
 }
 
 template <int N, int LPOL, bool B64, uint32_t... Cs>
-__device__ __forceinline__ void unrolled_ring(const uint64_t *in, uint32_t rot, uint32_t tile,
-                                              const CtLane &ln,
+__device__ __forceinline__ void unrolled_ring(const uint64_t *in, uint32_t rot, const CtLane &ln,
                                               uint32_t mask, u32x4 (&A)[N], u32x4 (&B)[N],
                                               uint32_t (&acc_lo)[16], uint32_t (&acc_hi)[16],
                                               std::integer_sequence<uint32_t, Cs...>) {
-  (unrolled_step<N, LPOL, B64, Cs>(in, rot, tile, ln, mask, A, B, acc_lo, acc_hi), ...);
+  (unrolled_step<N, LPOL, B64, Cs>(in, rot, ln, mask, A, B, acc_lo, acc_hi), ...);
 }
 
 template <int N, int LPOL, bool B64>
@@ -740,7 +726,7 @@ __device__ __forceinline__ void tile_unrolled(const KernArgs &args, const PassDe
 #pragma unroll
   for (int s = 0; s < 16; ++s) acc_lo[s] = acc_hi[s] = 0;
   u32x4 A[N], B[N];
-  unrolled_ring<N, LPOL, B64>(in, rot, tile, ln, mask, A, B, acc_lo, acc_hi,
+  unrolled_ring<N, LPOL, B64>(in, rot, ln, mask, A, B, acc_lo, acc_hi,
                          std::make_integer_sequence<uint32_t, N + 3>{});
   const uint32_t n_out = P.n_out;
   const uint64_t *outp = args.ptrs + P.out;
@@ -753,7 +739,7 @@ __device__ __forceinline__ void tile_unrolled(const KernArgs &args, const PassDe
     u32x4 ol = {acc_lo[t], acc_lo[4 + t], acc_lo[8 + t], acc_lo[12 + t]};
     u32x4 oh = {acc_hi[t], acc_hi[4 + t], acc_hi[8 + t], acc_hi[12 + t]};
     halves_swap(ol, oh);
-    const uint64_t dst = shard_base(outp[t], tile);
+    const uint64_t dst = outp[t];
     if (accumulate) {
       if (ln.okA) {
         const uint4 p = load16(dst + ln.offA);
@@ -938,7 +924,7 @@ __device__ __forceinline__ void store_subrun(const KernArgs &args, const PassDes
     u32x4 ol = {acc_lo[t], acc_lo[4 + t], acc_lo[8 + t], acc_lo[12 + t]};
     u32x4 oh = {acc_hi[t], acc_hi[4 + t], acc_hi[8 + t], acc_hi[12 + t]};
     halves_swap(ol, oh);
-    const uint64_t dst = outp[t];  // row layout only (the host refuses tiled sets here)
+    const uint64_t dst = outp[t];
     if (accumulate) {
       if (ln.okA) {
         const uint4 q = load16(dst + ln.offA);
@@ -1026,7 +1012,7 @@ __global__ __launch_bounds__(64) void gf_tail_kernel(const KernArgs args) {
   const uint64_t *in = args.ptrs + P.in;
   const uint64_t *outp = args.ptrs + P.out;
   for (uint32_t i = 0; i < P.n_in; ++i) {
-    const uint8_t *src = (const uint8_t *)(uintptr_t)(in[i] & kLaunchAddrMask);
+    const uint8_t *src = (const uint8_t *)(uintptr_t)in[i];
     const uint32_t lb = src[base + s], hb = src[base + half + s];
     const uint2 *T = (const uint2 *)(uintptr_t)P.table + i * 64;
     const uint2 e0 = T[tab_idx(0, lb & 15)], e1 = T[tab_idx(1, lb >> 4)],
@@ -1035,7 +1021,7 @@ __global__ __launch_bounds__(64) void gf_tail_kernel(const KernArgs args) {
     acc_hi ^= e0.y ^ e1.y ^ e2.y ^ e3.y;
   }
   for (uint32_t t = 0; t < P.n_out; ++t) {
-    uint8_t *dst = (uint8_t *)(uintptr_t)(outp[t] & kLaunchAddrMask) + base;
+    uint8_t *dst = (uint8_t *)(uintptr_t)outp[t] + base;
     uint8_t vl = uint8_t(acc_lo >> (8 * t)), vh = uint8_t(acc_hi >> (8 * t));
     if (P.accumulate) {
       vl ^= dst[s];
@@ -1097,18 +1083,6 @@ bool ab_build() {
 #else
   return false;
 #endif
-}
-
-bool kernel_takes_tiles() {
-  switch (kernel_variant()) {
-    case 73: case 75: case 76:
-#ifdef BFRS_AB_VARIANTS
-    case 70: case 71: case 77: case 78: case 79: case 80: case 81: case 82: case 83:
-#endif
-      return true;
-    default:
-      return false;
-  }
 }
 
 #ifdef BFRS_AB_VARIANTS

@@ -689,7 +689,7 @@ int Context::run_window(const std::vector<BlockIO> &blocks, size_t shard_bytes,
         d.full_chunks = full_chunks;
         d.tail_bytes = tail;
         d.accumulate = phase > 0;
-        d.rotate = n_real == n_pad && !BFRS_AB_KNOB("BFRS_NO_ROTATE");
+        d.rotate = n_real == n_pad;
         d.n_real = n_real;
         wg += wgs_per_pass;
         max_in = std::max(max_in, n_pad);
@@ -871,8 +871,6 @@ int check_dev_ptr(const void *p, const char *what) {
   if (!p) return set_error(BFRS_E_INVALID_ARGUMENT, std::string(what) + " is NULL");
   if (reinterpret_cast<uintptr_t>(p) & 15)
     return set_error(BFRS_E_INVALID_ARGUMENT, std::string(what) + " is not 16-byte aligned");
-  if (uint64_t(reinterpret_cast<uintptr_t>(p)) > kLaunchAddrMask)  // the launch tag's bits
-    return set_error(BFRS_E_INVALID_ARGUMENT, std::string(what) + " is not a device address");
   return BFRS_OK;
 }
 
@@ -895,66 +893,13 @@ int bfrs_decode_batch_dev(bfrs_ctx *ctx, size_t nblocks, const uint32_t *ks, siz
   BFRS_API_END
 }
 
-int bfrs_encode_batch_dev_tiled(bfrs_ctx *ctx, size_t nblocks, const uint32_t *ks, size_t m,
-                                size_t shard_bytes, const uint8_t *const *d_orig,
-                                const size_t *orig_strides, uint8_t *const *d_rec,
-                                const size_t *rec_strides, void *hip_stream) {
-  BFRS_API_BEGIN
-  return encode_batch_on(ctx, nblocks, ks, m, shard_bytes, d_orig, d_rec,
-                         static_cast<hipStream_t>(hip_stream), orig_strides, rec_strides);
-  BFRS_API_END
-}
-
-int bfrs_decode_batch_dev_tiled(bfrs_ctx *ctx, size_t nblocks, const uint32_t *ks, size_t m,
-                                size_t shard_bytes, const uint8_t *const *d_orig,
-                                const size_t *orig_strides, const uint8_t *const *d_rec,
-                                const size_t *rec_strides, uint8_t *const *d_restored,
-                                const size_t *restored_strides, void *hip_stream) {
-  BFRS_API_BEGIN
-  return decode_batch_on(ctx, nblocks, ks, m, shard_bytes, d_orig, d_rec, d_restored,
-                         static_cast<hipStream_t>(hip_stream), orig_strides, rec_strides,
-                         restored_strides);
-  BFRS_API_END
-}
-
 }  // extern "C"
 
 namespace bfrs {
 
-namespace {
-// A shard pointer of a device batch, checked, with its tile stride (bytes; 0
-// = a contiguous row) in the launch tag (kernels.hpp kLaunchStrideShift).
-// A tile-major shard holds bytes [8 KiB t, 8 KiB (t + 1)) at p + t * stride.
-template <typename T>
-int launch_ptr(T *p, const size_t *strides, size_t i, size_t shard_bytes, const char *what,
-               T **out) {
-  int rc = check_dev_ptr(p, what);
-  if (rc) return rc;
-  const size_t stride = strides ? strides[i] : 0;
-  if (stride == 0) {
-    *out = p;
-    return BFRS_OK;
-  }
-  constexpr size_t kTile = size_t(kTileHalfChunks) * 32;
-  if (stride % kTile || stride / kTile - 1 > 0xFFFF)
-    return set_error(BFRS_E_INVALID_ARGUMENT, std::string(what) + ": tile stride " +
-                                                  std::to_string(stride) +
-                                                  " is not a multiple of 8192 in [8192, 2^29]");
-  if (shard_bytes % kTile || shard_bytes > Context::kMaxWindowBytes)
-    return set_error(BFRS_E_INVALID_ARGUMENT,
-                     "tile-major shards need shard_bytes a multiple of 8192, at most 2 GiB");
-  if (!kernel_takes_tiles())
-    return set_error(BFRS_E_INVALID_ARGUMENT,
-                     "the selected kernel variant does not read tile-major shards");
-  const uint64_t tag = uint64_t(stride / kTile - 1) << kLaunchStrideShift;
-  *out = reinterpret_cast<T *>(reinterpret_cast<uintptr_t>(p) | tag);
-  return BFRS_OK;
-}
-}  // namespace
-
 int encode_batch_on(bfrs_ctx *ctx, size_t nblocks, const uint32_t *ks, size_t m,
                     size_t shard_bytes, const uint8_t *const *d_orig, uint8_t *const *d_rec,
-                    hipStream_t s, const size_t *orig_strides, const size_t *rec_strides) {
+                    hipStream_t s) {
   if (!ctx || (nblocks && (!ks || !d_orig || !d_rec)))
     return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_encode_batch_dev: NULL argument");
   Context &c = ctx->impl;
@@ -967,23 +912,22 @@ int encode_batch_on(bfrs_ctx *ctx, size_t nblocks, const uint32_t *ks, size_t m,
     rc = c.get_encode_plan(ks[b], m, &blocks[b].plan);
     if (rc) return rc;
     blocks[b].in.resize(ks[b]);
-    for (uint32_t i = 0; i < ks[b]; ++i, ++oi)
-      if ((rc = launch_ptr(d_orig[oi], orig_strides, oi, shard_bytes, "original shard pointer",
-                           &blocks[b].in[i])))
-        return rc;
+    for (uint32_t i = 0; i < ks[b]; ++i) {
+      if ((rc = check_dev_ptr(d_orig[oi], "original shard pointer"))) return rc;
+      blocks[b].in[i] = d_orig[oi++];
+    }
     blocks[b].out.resize(m);
-    for (size_t j = 0; j < m; ++j)
-      if ((rc = launch_ptr(d_rec[b * m + j], rec_strides, b * m + j, shard_bytes,
-                           "recovery shard pointer", &blocks[b].out[j])))
-        return rc;
+    for (size_t j = 0; j < m; ++j) {
+      if ((rc = check_dev_ptr(d_rec[b * m + j], "recovery shard pointer"))) return rc;
+      blocks[b].out[j] = d_rec[b * m + j];
+    }
   }
   return c.run_blocks(blocks, shard_bytes, s);
 }
 
 int decode_batch_on(bfrs_ctx *ctx, size_t nblocks, const uint32_t *ks, size_t m,
                     size_t shard_bytes, const uint8_t *const *d_orig, const uint8_t *const *d_rec,
-                    uint8_t *const *d_restored, hipStream_t s, const size_t *orig_strides,
-                    const size_t *rec_strides, const size_t *restored_strides) {
+                    uint8_t *const *d_restored, hipStream_t s) {
   if (!ctx || (nblocks && (!ks || !d_orig || !d_rec || !d_restored)))
     return set_error(BFRS_E_INVALID_ARGUMENT, "bfrs_decode_batch_dev: NULL argument");
   Context &c = ctx->impl;
@@ -1013,25 +957,16 @@ int decode_batch_on(bfrs_ctx *ctx, size_t nblocks, const uint32_t *ks, size_t m,
     if ((rc = c.get_decode_plan(k, m, op, rp, &io.plan))) return rc;
     for (size_t j = 0; j < m; ++j)
       if (rp[j]) {
-        const uint8_t *p = nullptr;
-        if ((rc = launch_ptr(d_rec[b * m + j], rec_strides, b * m + j, shard_bytes,
-                             "recovery shard pointer", &p)))
-          return rc;
-        io.in.push_back(p);
+        if ((rc = check_dev_ptr(d_rec[b * m + j], "recovery shard pointer"))) return rc;
+        io.in.push_back(d_rec[b * m + j]);
       }
     for (size_t i = 0; i < k; ++i)
       if (op[i]) {
-        const uint8_t *p = nullptr;
-        if ((rc = launch_ptr(d_orig[oi + i], orig_strides, oi + i, shard_bytes,
-                             "original shard pointer", &p)))
-          return rc;
-        io.in.push_back(p);
+        if ((rc = check_dev_ptr(d_orig[oi + i], "original shard pointer"))) return rc;
+        io.in.push_back(d_orig[oi + i]);
       } else {
-        uint8_t *p = nullptr;
-        if ((rc = launch_ptr(d_restored[oi + i], restored_strides, oi + i, shard_bytes,
-                             "restored shard pointer", &p)))
-          return rc;
-        io.out.push_back(p);
+        if ((rc = check_dev_ptr(d_restored[oi + i], "restored shard pointer"))) return rc;
+        io.out.push_back(d_restored[oi + i]);
       }
     oi += k;
     blocks.push_back(std::move(io));

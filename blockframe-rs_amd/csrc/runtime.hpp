@@ -261,18 +261,12 @@ int check_shape(size_t k, size_t m, size_t shard_bytes);
 // Batch entry points with an explicit stream (the C-ABI wrappers pass the
 // caller's stream, NULL meaning HIP's default stream; the host-memory API and
 // the streaming objects pass the context's own stream).
-// The stride arrays (parallel to the pointer arrays, NULL = every shard a
-// contiguous row) give the tile stride of shards in tile-major sets
-// (bfrs_*_batch_dev_tiled); a launch pointer then carries it in its top bits
-// (kernels.hpp kLaunchStrideShift).
 int encode_batch_on(bfrs_ctx *ctx, size_t nblocks, const uint32_t *ks, size_t m,
                     size_t shard_bytes, const uint8_t *const *d_orig, uint8_t *const *d_rec,
-                    hipStream_t s, const size_t *orig_strides = nullptr,
-                    const size_t *rec_strides = nullptr);
+                    hipStream_t s);
 int decode_batch_on(bfrs_ctx *ctx, size_t nblocks, const uint32_t *ks, size_t m,
                     size_t shard_bytes, const uint8_t *const *d_orig, const uint8_t *const *d_rec,
-                    uint8_t *const *d_restored, hipStream_t s, const size_t *orig_strides = nullptr,
-                    const size_t *rec_strides = nullptr, const size_t *restored_strides = nullptr);
+                    uint8_t *const *d_restored, hipStream_t s);
 
 }  // namespace bfrs
 

@@ -234,31 +234,6 @@ int bfrs_decode_batch_dev(bfrs_ctx *ctx, size_t nblocks, const uint32_t *origina
                           const uint8_t *const *d_originals, const uint8_t *const *d_recovery,
                           uint8_t *const *d_restored, void *hip_stream);
 
-/* Tile-major shard sets (round 6; no reference counterpart: an HBM layout
- * option of the device batch above).  A shard of such a set is
- * cut into tiles of BFRS_TILE_BYTES; tile t sits at p + t * stride, so a set of
- * P shards stored tile by tile (tile t of shard 0, of shard 1, ... of shard
- * P - 1, then tile t + 1) has stride = P * BFRS_TILE_BYTES and shard i starts at
- * set + i * BFRS_TILE_BYTES.  The kernel then reads one block's tile of every
- * input from one contiguous run of HBM instead of from k runs a shard apart.
- * The stride arrays run parallel to the pointer arrays; a NULL array, or a 0
- * entry, means that shard is a contiguous row (as in bfrs_*_batch_dev).  With
- * any tiled shard: shard_bytes a multiple of BFRS_TILE_BYTES and at most 2 GiB,
- * strides multiples of BFRS_TILE_BYTES up to 65536 tiles, else
- * BFRS_E_INVALID_ARGUMENT.  Outputs are identical to the row form's. */
-#define BFRS_TILE_BYTES 8192
-int bfrs_encode_batch_dev_tiled(bfrs_ctx *ctx, size_t nblocks, const uint32_t *original_counts,
-                                size_t recovery_count, size_t shard_bytes,
-                                const uint8_t *const *d_originals, const size_t *original_strides,
-                                uint8_t *const *d_recovery, const size_t *recovery_strides,
-                                void *hip_stream);
-int bfrs_decode_batch_dev_tiled(bfrs_ctx *ctx, size_t nblocks, const uint32_t *original_counts,
-                                size_t recovery_count, size_t shard_bytes,
-                                const uint8_t *const *d_originals, const size_t *original_strides,
-                                const uint8_t *const *d_recovery, const size_t *recovery_strides,
-                                uint8_t *const *d_restored, const size_t *restored_strides,
-                                void *hip_stream);
-
 /* ---- BlockFrame wrappers (C++ restatement of the reference functions) -- */
 /* Chunker::generate_parity (src/chunker/generate.rs:59-104): pads every
  * segment to the longest one, RS(data_shards, parity_shards) encode.

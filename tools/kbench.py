@@ -83,10 +83,6 @@ def main():
 
     def build(x):
         del bufs[:]
-        x = x.split("#")[0]  # "#n": another copy of the same layout (placement study)
-        alias = x.endswith("a")  # round 6: tile-major sets over the previous layout's buffers
-        tiled = x.endswith("t")  # round 6: tile-major sets (bfrs_*_batch_dev_tiled)
-        x = x.rstrip("t").rstrip("a")
         contig = x.endswith("c")
         x = x.rstrip("c")
         single = x.endswith("s")
@@ -94,26 +90,7 @@ def main():
         per_row = x.endswith("r")
         x = x.rstrip("r")
         stagger = int(x.rstrip("b"))
-        if alias:  # the same HBM as the last row layout, carved into per-block tile-major sets
-            prev = last_rows[0]
-
-            def carve(flat, counts):
-                out, off = [], 0
-                for n in counts:
-                    v = flat[off:off + n * S].view(S // bfrs.TILE_BYTES, n, bfrs.TILE_BYTES)
-                    out += [v[:, i, :] for i in range(n)]
-                    off += n * S
-                return out
-            data = carve(prev["bufs"][0], shapes)
-            par = carve(prev["bufs"][1], [3] * nb)
-            rest = carve(prev["bufs"][2], [3] * nb)
-            bufs.extend(prev["bufs"])
-        elif tiled:  # per block: one tile-major set of its k data, one of 3 parity, one of 3 restored
-            data = [t_ for k in shapes for t_ in bfrs.empty_tiled_shards(k, S)]
-            par = [t_ for k in shapes for t_ in bfrs.empty_tiled_shards(3, S)]
-            rest = [t_ for k in shapes for t_ in bfrs.empty_tiled_shards(3, S)]
-            bufs.append(data[0])
-        elif per_row:  # every shard row its own allocation
+        if per_row:  # every shard row its own allocation
             def one(n):
                 out = []
                 for _ in range(n):
@@ -138,13 +115,8 @@ def main():
             data = rows(a.segments, S + stagger, contig)
             par = rows(3 * nb, S + stagger, contig)
             rest = rows(3 * nb, S + stagger, contig)
-        row = torch.empty(S, dtype=torch.uint8, device="cuda")
         for s_ in range(a.segments):
-            if data[s_].dim() == 2:
-                synth.fill_segment_torch(row, 0xB10C, s_)
-                data[s_].copy_(row.view(-1, bfrs.TILE_BYTES))
-            else:
-                synth.fill_segment_torch(data[s_], 0xB10C, s_)
+            synth.fill_segment_torch(data[s_], 0xB10C, s_)
         dec_in, dec_out, seg, erased = [], [], 0, []
         for b, k in enumerate(shapes):
             er = [1, k // 2, k - 1]
@@ -158,26 +130,10 @@ def main():
         for b, k in enumerate(shapes):
             dr_in += [x for x in dec_in[seg:seg + k] if x is not None] + par[3 * b:3 * b + 3]
             seg += k
-        L = dict(data=data, par=par, rest=rest, dec_in=dec_in, dec_out=dec_out, erased=erased,
-                 dr_in=dr_in, flat=bufs[0], bufs=list(bufs), alias=alias)
-        if not tiled and not alias:
-            last_rows[:] = [L]
-        return L
+        return dict(data=data, par=par, rest=rest, dec_in=dec_in, dec_out=dec_out, erased=erased,
+                    dr_in=dr_in, flat=bufs[0])
 
-    last_rows = []
     layouts = {x: build(x) for x in a.stagger.split(",")}
-
-    def refill(L):
-        """An aliasing layout shares its HBM with a row layout: rewrite its data
-        (and parity) in its own arrangement before a correctness check."""
-        row = torch.empty(S, dtype=torch.uint8, device="cuda")
-        for s_ in range(a.segments):
-            d = L["data"][s_]
-            if d.dim() == 2:
-                synth.fill_segment_torch(row, 0xB10C, s_)
-                d.copy_(row.view(-1, bfrs.TILE_BYTES))
-            else:
-                synth.fill_segment_torch(d, 0xB10C, s_)
     ctx = bfrs.Context(0)
     stream = torch.cuda.current_stream()
     alg = sum(k + 3 for k in shapes) * S
@@ -202,7 +158,7 @@ def main():
         run(L)
     torch.cuda.synchronize()
     L0 = next(iter(layouts.values()))
-    ref = torch.stack([p_.reshape(-1) for p_ in L0["par"]]).clone()
+    ref = torch.stack(L0["par"]).clone()
     t0 = time.perf_counter()  # clock settle (~1 s of launches)
     while time.perf_counter() - t0 < 1.0:
         for _ in range(16):
@@ -217,13 +173,7 @@ def main():
     rng = random.Random(0x5EED)
 
     def select(v, t):
-        base = v.split(":")[0]
-        if base.endswith("n"):  # "76n": read order not rotated (BFRS_NO_ROTATE, A/B build)
-            os.environ["BFRS_NO_ROTATE"] = "1"
-            base = base[:-1]
-        else:
-            os.environ.pop("BFRS_NO_ROTATE", None)
-        os.environ["BFRS_KERNEL_VARIANT"] = base
+        os.environ["BFRS_KERNEL_VARIANT"] = v.split(":")[0]
         if t == "0":
             os.environ.pop("BFRS_TILES_PER_WG", None)
         else:
@@ -260,21 +210,10 @@ def main():
         torch.cuda.synchronize()
         copy_ms.append(e0.elapsed_time(e1) / a.iters)
     # correctness of every codec variant, after the timing
-    aliased = any(L["alias"] for L in layouts.values())
-    if aliased:  # the reference parity from the first layout's own arrangement
-        refill(L0)
-        select("76", "0")
-        ctx.encode_batch_dev(shapes, 3, S, L0["data"], L0["par"], stream=stream)
-        torch.cuda.synchronize()
-        ref = torch.stack([p_.reshape(-1) for p_ in L0["par"]]).clone()
     for (v, t, x) in configs:
         if v in PROBES or ":" in v:  # probes and io-mode runs have no codec output to check
             continue
         L = layouts[x]
-        if aliased:  # shared HBM: this layout's own bytes and parity first
-            refill(L)
-            select("76", "0")
-            ctx.encode_batch_dev(shapes, 3, S, L["data"], L["par"], stream=stream)
         select(v, t)
         if a.decode:
             for t_ in L["rest"]:
@@ -282,11 +221,10 @@ def main():
         run(L)
         torch.cuda.synchronize()
         if not a.decode:
-            assert torch.equal(torch.stack([p_.reshape(-1) for p_ in L["par"]]), ref), \
-                f"variant {v} output differs ({x})"
+            assert torch.equal(torch.stack(L["par"]), ref), f"variant {v} output differs"
         else:
             for ri, di in L["erased"]:
-                assert torch.equal(L["rest"][ri], L["data"][di]), f"variant {v} decode differs ({x})"
+                assert torch.equal(L["rest"][ri], L["data"][di]), f"variant {v} decode differs"
     out = {}
     for (v, t, x), ms in res.items():
         m = float(np.median(ms))
@@ -297,9 +235,7 @@ def main():
     # (first half -> second half), timed like the kernels
     if a.copy_probe:
         for x, L in layouts.items():
-            fl = L["flat"].reshape(-1) if L["flat"].dim() == 1 else None
-            if fl is None:
-                continue
+            fl = L["flat"]
             h = fl.numel() // 2
             src_, dst_ = fl[:h], fl[h:2 * h]
             for _ in range(5):
