@@ -822,137 +822,6 @@ __global__ __launch_bounds__(256, 5) void gf_apply_unrolled_kernel(const KernArg
 }
 
 #ifdef BFRS_AB_VARIANTS
-// ---- v110: persistent workgroups, the input ring carried across tiles --------
-// Measurement build only (round 6).  v76 drains its 3-input ring at the end of
-// every tile: the last three consumes run with 2, 1, 0 inputs in flight, the
-// stores go out, the workgroup ends and the next one stages its tables and
-// waits a full load latency for its first input.  Here a workgroup runs T
-// tiles of one pass -- w, w + W, ..., W = ceil(n_tiles / T) workgroups per
-// pass, so the resident workgroups still cover consecutive tiles and a read
-// group's 64 workgroups still sit on one XCD -- and the last three steps of
-// tile j issue inputs 0-2 of tile j + 1.  Tile j's 2*NOUT stores go out after
-// them, so the first three consumes of tile j + 1 wait with vmcnt(6 + 2*NOUT)
-// (the gfx9 counter retires loads and stores in issue order).  The tables
-// are staged once per workgroup (the read rotation follows the workgroup, not
-// the tile).  The tile offset rides in the SGPR base (saddr form), the lane
-// offset is a per-lane constant.  Host contract (run_window): whole tiles
-// (shard_bytes % 8 KiB == 0), n_tiles % T == 0 (every workgroup runs exactly
-// T tiles: no exit branch with loads in flight), every pass 3 outputs, n_in
-// 30 / 20 / 8.
-// a wave-uniform 64-bit value the divergence analysis cannot prove uniform
-// (readfirstlane returns int: both halves go through uint32_t, or the low
-// half would be sign-extended into the high one -- the r06 fault)
-__device__ __forceinline__ uint64_t sgpr64(uint64_t x) {
-  const uint32_t hi = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(x >> 32))));
-  const uint32_t lo = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(x))));
-  return (uint64_t(hi) << 32) | lo;
-}
-
-template <int N, int NOUT, bool B64, bool FIRST, bool LAST, uint32_t C>
-__device__ __forceinline__ void pstep(const uint64_t *in, uint32_t rot, uint64_t tb,
-                                      uint64_t tb_next, uint32_t vA, uint32_t vB, uint32_t nA,
-                                      uint32_t nB, uint32_t mask, u32x4 (&A)[N], u32x4 (&B)[N],
-                                      uint32_t (&acc_lo)[16], uint32_t (&acc_hi)[16]) {
-  constexpr uint32_t D = 3;
-  if constexpr (C < uint32_t(N)) {
-    if constexpr (FIRST || C >= D) {  // a later tile's inputs 0-2 came with the previous tile
-      uint32_t src = rot + C;
-      src = src >= uint32_t(N) ? src - N : src;
-      gload_ct<1>(A[C], B[C], sgpr64(in[src] + tb), vA, vB);
-    }
-  } else if constexpr (!LAST && C - N < D) {  // the next tile's input C - N
-    constexpr uint32_t x = C - N;
-    uint32_t src = rot + x;
-    src = src >= uint32_t(N) ? src - N : src;
-    gload_ct<1>(A[x], B[x], sgpr64(in[src] + tb_next), nA, nB);
-  }
-  if constexpr (C >= D && C - D < uint32_t(N)) {
-    constexpr uint32_t c = C - D;
-    constexpr int after = LAST ? ((N - 1 - int(c)) < int(D) ? (N - 1 - int(c)) : int(D)) : int(D);
-    constexpr int stores = (!FIRST && c < D) ? 2 * NOUT : 0;
-    vm_wait<2 * after + stores>(A[c], B[c]);
-    u32x4 L = A[c], H = B[c];
-    halves_swap(L, H);
-    mac_slot<c, B64>(L, H, mask, acc_lo, acc_hi);
-  }
-}
-
-template <int N, int NOUT, bool B64, bool FIRST, bool LAST, uint32_t... Cs>
-__device__ __forceinline__ void psteps(const uint64_t *in, uint32_t rot, uint64_t tb,
-                                       uint64_t tb_next, uint32_t vA, uint32_t vB, uint32_t nA,
-                                       uint32_t nB, uint32_t mask, u32x4 (&A)[N], u32x4 (&B)[N],
-                                       uint32_t (&acc_lo)[16], uint32_t (&acc_hi)[16],
-                                       std::integer_sequence<uint32_t, Cs...>) {
-  (pstep<N, NOUT, B64, FIRST, LAST, Cs>(in, rot, tb, tb_next, vA, vB, nA, nB, mask, A, B, acc_lo,
-                                        acc_hi),
-   ...);
-}
-
-// Tile J of the workgroup's T (the host makes every one whole and present).
-template <int N, int NOUT, bool B64, int T, int J>
-__device__ __forceinline__ void ptile(const KernArgs &args, const PassDesc &P, uint32_t w,
-                                      uint32_t W, uint32_t rot, uint32_t lane_off, uint32_t mask,
-                                      u32x4 (&A)[N], u32x4 (&B)[N]) {
-  constexpr bool FIRST = J == 0, LAST = J == T - 1;
-  const uint64_t tb = uint64_t(w + uint32_t(J) * W) * (kTileHalfChunks * 32);
-  const uint64_t tb_next = tb + uint64_t(W) * (kTileHalfChunks * 32);
-  const uint64_t *in = args.ptrs + P.in;
-  uint32_t acc_lo[16], acc_hi[16];
-#pragma unroll
-  for (int s = 0; s < 16; ++s) acc_lo[s] = acc_hi[s] = 0;
-  psteps<N, NOUT, B64, FIRST, LAST>(in, rot, tb, tb_next, lane_off, lane_off + 1024, lane_off,
-                                    lane_off + 1024, mask, A, B, acc_lo, acc_hi,
-                                    std::make_integer_sequence<uint32_t, N + 3>{});
-  const uint64_t *outp = args.ptrs + P.out;
-  transpose_outputs(acc_lo);
-  transpose_outputs(acc_hi);
-#pragma unroll
-  for (int t = 0; t < NOUT; ++t) {
-    u32x4 ol = {acc_lo[t], acc_lo[4 + t], acc_lo[8 + t], acc_lo[12 + t]};
-    u32x4 oh = {acc_hi[t], acc_hi[4 + t], acc_hi[8 + t], acc_hi[12 + t]};
-    halves_swap(ol, oh);
-    const uint64_t dst = outp[t] + tb + lane_off;
-    store16_nt(dst, ol);
-    store16_nt(dst + 1024, oh);
-  }
-  if constexpr (!LAST) ptile<N, NOUT, B64, T, J + 1>(args, P, w, W, rot, lane_off, mask, A, B);
-}
-
-template <int N, int NOUT, bool B64, int T>
-__device__ __forceinline__ void tiles_persistent(const KernArgs &args, const PassDesc &P,
-                                                 uint32_t w, uint32_t W, uint32_t wave_id,
-                                                 uint32_t rot) {
-  const uint32_t l = threadIdx.x & 63;
-  const uint32_t lane_off = wave_id * 2048 + ((l & 31) >> 1) * 64 + (l >> 5) * 32 + (l & 1) * 16;
-  const uint32_t mask = __builtin_amdgcn_readfirstlane(0xF0u);
-  u32x4 A[N], B[N];
-  ptile<N, NOUT, B64, T, 0>(args, P, w, W, rot, lane_off, mask, A, B);
-}
-
-// Host contract: every pass subfield with n_out == 3 and no accumulation,
-// tiles_per_wg == T, a pass's workgroups ceil(n_tiles / T).
-template <bool B64, int T>
-__global__ __launch_bounds__(256, 5) void gf_apply_persistent_kernel(const KernArgs args) {
-  const uint32_t wg = xcd_group_remap<64>(blockIdx.x, gridDim.x);
-  const PassDesc &P = find_pass(args, wg);
-  const uint32_t w = wg - P.wg_begin;
-  const uint32_t W = P.n_tiles / T;
-  const uint32_t n_in = P.n_in;
-  const uint32_t rot = P.rotate ? ((w >> 6) * 4) % n_in : 0;
-  stage_tables_rotated(P, rot);
-  if (w >= W) return;
-  const uint32_t wave_id = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (P.n_out != 3 || P.accumulate) return;  // the host's contract, checked again
-  if (n_in == 30)
-    tiles_persistent<30, 3, B64, T>(args, P, w, W, wave_id, rot);
-  else if (n_in == 8)
-    tiles_persistent<8, 3, B64, T>(args, P, w, W, wave_id, rot);
-  else if (n_in == 20)
-    tiles_persistent<20, 3, B64, T>(args, P, w, W, wave_id, rot);
-}
-#endif  // BFRS_AB_VARIANTS
-
-#ifdef BFRS_AB_VARIANTS
 // ---- LDS-DMA input ring, 4 KiB per wave and input (v107-v109, round 6) -------
 // Measurement build only.  The traffic probes put 4 KiB of
 // columns per wave and input 3-4% ahead of v76's 2 KiB in both HBM placement
@@ -1187,7 +1056,7 @@ static bool variant_known(int v) {
   switch (v) {
     case 5: case 36: case 37: case 40: case 41: case 42: case 58: case 70: case 71:
     case 73: case 75: case 76: case 77: case 78: case 79: case 80: case 81: case 82: case 83:
-    case 107: case 108: case 109: case 110:
+    case 107: case 108: case 109:
       return true;
     case 44: case 72: case 74:
       return std::getenv("BFRS_ALLOW_PROBE") != nullptr;
@@ -1328,15 +1197,6 @@ hipError_t launch_gf_apply(const KernArgs &args, uint32_t n_wgs, uint32_t max_in
     case 77:  // 76 with 4-byte low-byte lookups
       if (!unrolled_ok) return launch_gf_default(args, n_wgs, lds, subfield, stream);
       hipLaunchKernelGGL(gf_apply_unrolled_kernel<false>, dim3(n_wgs), dim3(256), lds, stream, args);
-      break;
-    case 110:  // persistent workgroups, ring carried across T tiles (run_window sets T)
-      if (!subfield || args.tiles_per_wg < 2) return launch_gf_default(args, n_wgs, lds, subfield, stream);
-      if (args.tiles_per_wg == 2)
-        hipLaunchKernelGGL((gf_apply_persistent_kernel<true, 2>), dim3(n_wgs), dim3(256), lds, stream, args);
-      else if (args.tiles_per_wg == 4)
-        hipLaunchKernelGGL((gf_apply_persistent_kernel<true, 4>), dim3(n_wgs), dim3(256), lds, stream, args);
-      else  // T = 8 spills (105 VGPRs to scratch): not built
-        return launch_gf_default(args, n_wgs, lds, subfield, stream);
       break;
     case 78: case 79: case 80: case 81: case 82: case 83:
       if (!unrolled_ok) return launch_gf_default(args, n_wgs, lds, subfield, stream);

@@ -657,21 +657,6 @@ int Context::run_window(const std::vector<BlockIO> &blocks, size_t shard_bytes,
         const uint64_t total_tiles = uint64_t(n_tiles) * (last - first);
         tpw = uint32_t(std::max<uint64_t>(1, total_tiles / 65536));
         if (const char *e = BFRS_AB_KNOB("BFRS_TILES_PER_WG")) tpw = std::max(1, atoi(e));
-        if (ab_build() && kernel_variant() == 110) {
-          // v110 (A/B build): T tiles per persistent workgroup, when every
-          // pass of the launch is a 3-output subfield pass of phase 0
-          const char *e = BFRS_AB_KNOB("BFRS_PERSIST_T");
-          const int T = e ? atoi(e) : 4;
-          const size_t tile = size_t(kTileHalfChunks) * 32;
-          bool ok = phase == 0 && shard_bytes % tile == 0 && T > 0 &&
-                    (shard_bytes / tile) % size_t(T) == 0;
-          for (size_t it = first; it < last; ++it) {
-            const PlanPass &p = *items[it].p;
-            const uint32_t n_pad = (p.c1 - p.c0 + 1) & ~1u;
-            ok = ok && p.subfield && p.r1 - p.r0 == 3 && (n_pad == 30 || n_pad == 20 || n_pad == 8);
-          }
-          tpw = ok && (T == 2 || T == 4) ? uint32_t(T) : 1;
-        }
         // the wide tiles exist only for one tile per workgroup: otherwise
         // the launch falls back to 8 KiB tiles, so size the grid for them
         if (tpw == 1 || !unrolled_sizes || tb == tile_bytes(false)) break;

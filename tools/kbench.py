@@ -174,13 +174,7 @@ def main():
     rng = random.Random(0x5EED)
 
     def select(v, t):
-        base = v.split(":")[0]
-        if "t" in base:  # "110t2": v110 with T = 2 tiles per workgroup (BFRS_PERSIST_T, A/B build)
-            base, T = base.split("t")
-            os.environ["BFRS_PERSIST_T"] = T
-        else:
-            os.environ.pop("BFRS_PERSIST_T", None)
-        os.environ["BFRS_KERNEL_VARIANT"] = base
+        os.environ["BFRS_KERNEL_VARIANT"] = v.split(":")[0]
         if t == "0":
             os.environ.pop("BFRS_TILES_PER_WG", None)
         else:
