@@ -146,6 +146,10 @@ void *pinned_alloc(size_t bytes) {
       if (r + kHugePage > a) munmap(reinterpret_cast<void *>(a + len), r + kHugePage - a);
       void *p = reinterpret_cast<void *>(a);
       (void)madvise(p, len, MADV_HUGEPAGE);
+      // not inherited by a fork()ed child (the bench's subprocesses, a
+      // caller's workers): the parent's registered pages never turn
+      // copy-on-write under the GPU's mapping, as with RDMA registrations
+      (void)madvise(p, len, MADV_DONTFORK);
       if (madvise(p, len, MADV_POPULATE_WRITE) != 0) std::memset(p, 0, len);  // first touch
       if (hipHostRegister(p, len, hipHostRegisterPortable) == hipSuccess) {
         Registry &reg = registry();
